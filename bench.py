@@ -1,0 +1,250 @@
+"""SMEM-seeding benchmark (BASELINE.json metric) on 1..N MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Workload (BASELINE.json configs[1]): an FM index resident in HBM and 1M x
+150 bp single-end reads per GPU (2% substitutions, 0.1% N, both strands).
+human_g1k_v37 is not available offline, so the index is built from a seeded
+synthetic genome (random sequence with repeat families, exact and tandem
+repeats; smemgpu/synth.py) by this repo's own `bwa index -a is`-identical
+builder; its size is reported in `config`.
+
+A step = one pass of the seeding hot path (mem_insert_seed's smem_next2 loop
+for every read, software/bwamem.c:453-460) over the resident batch: the
+seeding kernel plus result compaction, outputs left in HBM (host transfers
+excluded; DESIGN.md gives the PCIe-inclusive rate).  Reads shard across ranks
+with no collective in the data path (index replicated): scaling "weak".
+
+roofline: dominant kernel = seed_kernel; achieved = algorithmic bytes per
+launch (64 B x distinct Occ buckets per extend + read length
++ 32 B x intervals out, counted by the CPU oracle on a sample of the same
+reads) / the kernel's HIP-event duration measured here.
+
+cpu_baseline: the reference's own C (oracle/_ref/ref_harness, compiled from
+the reference sources) when present, else the C restatement, timed on this
+host's cores on a bounded sample of the same reads, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "SMEM reads/sec on human_g1k_v37 150bp at 1/2/4/8 MI355X; achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
+    p.add_argument("--read-len", type=int, default=150)
+    p.add_argument("--sub", type=float, default=0.02)
+    p.add_argument("--genome-mbp", type=float, default=100.0)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--lanes-per-cu", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--stats-sample", type=int, default=20000, help="reads counted by the oracle for bytes/read")
+    p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
+    p.add_argument("--traffic-json", default="", help="per-launch HBM bytes measured by rocprofv3 --pmc")
+    return p.parse_args()
+
+
+def get_index(args, rank, world, barrier):
+    import smemgpu
+    from smemgpu import synth
+    os.makedirs(args.cache, exist_ok=True)
+    n_bp = int(args.genome_mbp * 1e6)
+    key = os.path.join(args.cache, f"genome_{n_bp}_{args.seed}.bwt")
+    if rank == 0 and not os.path.exists(key):
+        t = time.time()
+        g = synth.make_genome(n_bp, seed=args.seed, n_chrom=24)
+        idx = smemgpu.Index.build(g.codes)
+        idx.write(key + ".tmp")
+        os.replace(key + ".tmp", key)
+        del g
+        log(f"index built: {n_bp} bp genome, {idx.words.nbytes / 1e6:.1f} MB in {time.time() - t:.1f} s")
+    barrier()
+    return smemgpu.Index.read(key), key
+
+
+def make_reads(args, rank, genome_codes=None):
+    from smemgpu import synth
+    if genome_codes is None:
+        genome_codes = synth.make_genome(int(args.genome_mbp * 1e6), seed=args.seed, n_chrom=24).codes
+    # seeds differ per rank: each GPU gets its own shard of the read set
+    return synth.make_reads(genome_codes, args.reads, args.read_len, seed=1000 + args.seed * 7919 + rank,
+                            sub_rate=args.sub, n_rate=0.001)
+
+
+def cpu_baseline(args, idx, idx_path, reads, cores):
+    """Time the CPU seeding loop on a bounded sample of the same reads."""
+    from oracle import oracle
+    from smemgpu import synth
+    oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
+    # calibrate on a small slice, then size the sample for ~cpu_seconds
+    cal = reads.subset(np.arange(min(reads.n, 2000)))
+    t, _ = oracle.seed_timed(oi, cal.codes, cal.offs, threads=cores)
+    rate = cal.n / max(t, 1e-6)
+    n = int(min(reads.n, max(cal.n, rate * args.cpu_seconds)))
+    sample = reads.subset(np.arange(n))
+    kind = "port"
+    if oracle.ref_available():
+        with tempfile.TemporaryDirectory() as d:
+            p = os.path.join(d, "s.smrd")
+            synth.write_smrd(p, sample)
+            r = oracle.ref_bench(idx_path, p, cores, n)
+            secs, kind = r["seconds"], "reference"
+    else:
+        secs, _ = oracle.seed_timed(oi, sample.codes, sample.offs, threads=cores)
+    oi.close()
+    return {"value": round(n / secs, 1), "unit": "reads/s", "cores": cores, "kind": kind,
+            "sample": f"first {n} of the benchmark's {args.read_len} bp reads on rank 0, {secs:.1f} s wall, "
+                      f"{cores} pthreads"}
+
+
+def algorithmic_bytes(args, idx, reads):
+    """SURVEY.md §8(d) bytes/read, counted by the oracle on a sample."""
+    from oracle import oracle
+    oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
+    n = min(reads.n, args.stats_sample)
+    s = reads.subset(np.arange(n))
+    per, st = oracle.seed_stats(oi, s.codes, s.offs, threads=min(16, os.cpu_count() or 1))
+    oi.close()
+    return float(per["bytes"].mean()), st, n
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import smemgpu
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        torch.cuda.set_device(local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def allmax(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allsum(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    idx, idx_path = get_index(args, rank, world, barrier)
+    reads = make_reads(args, rank)
+    gpu = smemgpu.Gpu(idx, device=local, lanes_per_cu=args.lanes_per_cu)
+    batch = gpu.batch(reads.n, int(reads.codes.size), int(reads.lens.max()))
+    batch.set_reads(reads.codes, reads.offs)  # inputs resident in HBM before timing
+    torch.cuda.synchronize()
+
+    opt = smemgpu.Options()
+    for _ in range(args.warmup):
+        batch.run(opt)
+    kernel_ms = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.run(opt)
+        kernel_ms.append(batch.stats()["kernel_ms"])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = batch.stats()
+    elapsed_max = allmax(elapsed)
+    total_reads = allsum(float(reads.n)) * args.steps
+    value = total_reads / elapsed_max
+
+    if rank == 0:
+        bpr, ostats, n_counted = algorithmic_bytes(args, idx, reads)
+        k_ms = float(np.mean(kernel_ms))
+        achieved = bpr * reads.n / (k_ms * 1e-3) / 1e9
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            with open(args.traffic_json) as fh:
+                traffic = json.load(fh).get("bytes_per_launch")
+        cores = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
+        cpu = None
+        if args.cpu_seconds > 0:
+            cpu = cpu_baseline(args, idx, idx_path, reads, cores)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "reads/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"synthetic {args.genome_mbp:g} Mbp genome index in HBM (stand-in for human_g1k_v37), "
+                            f"{reads.n} x {args.read_len} bp SE reads per GPU, {args.sub:.0%} subs, 0.1% N, "
+                            f"k=19 r=1.5 s=10",
+                "reads_per_gpu": reads.n,
+                "read_len": args.read_len,
+                "genome_bp": int(args.genome_mbp * 1e6),
+                "index_bytes": int(idx.words.nbytes),
+                "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collectives",
+                "grid": st["grid"], "block": st["block"],
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "seed_kernel",
+                "kernel_ms": round(k_ms, 3),
+                "bytes_per_read": round(bpr, 1),
+                "bytes_per_read_sample": n_counted,
+                "extends_per_read": round(ostats["n_ext"] / max(n_counted, 1), 1),
+            },
+            "cpu_baseline": cpu,
+            "compact_ms": round(st["compact_ms"], 3),
+            "overflow_reads": st["n_overflow"],
+        }
+        print(json.dumps(out), flush=True)
+    batch.close()
+    gpu.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

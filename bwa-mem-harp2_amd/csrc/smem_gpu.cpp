@@ -1,0 +1,557 @@
+// smem_gpu.cpp — runtime behind the C ABI in include/smem_gpu.h.
+//
+// Replaces the reference's accelerator plumbing:
+//   * AAL runtime + 3 GB shared buffer + CSR writes (software/HelloALINLB.cpp:254-485)
+//     -> one HIP device context per smem_gpu_t, index resident in HBM;
+//   * the FPGA index upload (software/bwa.c:286-307) -> smem_gpu_init;
+//   * the HARP manager thread that serialises every worker's batch through
+//     one FPGA buffer with polled hand-shakes (software/fastmap.c:320-429)
+//     -> per-worker smem_batch_t objects, each with its own HIP stream and
+//     device buffers, so concurrent kt_for_batch workers never wait on a
+//     manager and never get rejected.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "smem_gpu.h"
+#include "smem_kernels.h"
+
+using smem::Intv;
+
+static_assert(sizeof(Intv) == sizeof(smem_intv_t), "interval layout");
+
+namespace {
+
+thread_local char g_err[512];
+
+int fail(int code, const char* what, hipError_t e = hipSuccess) {
+    if (e != hipSuccess)
+        snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    else
+        snprintf(g_err, sizeof(g_err), "%s", what);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                   \
+    do {                                                                \
+        hipError_t _e = (expr);                                         \
+        if (_e != hipSuccess) return fail(SMEM_E_DEVICE, #expr, _e);    \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+template <class T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct smem_gpu {
+    int device = 0;
+    int n_cu = 0;
+    int lanes_per_cu = 1024;
+    int intv_cap = 0;
+    uint32_t* d_bwt = nullptr;
+    uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
+    std::mutex mu;
+    std::unordered_map<std::thread::id, smem_batch_t*> per_thread;
+};
+
+struct smem_batch {
+    smem_gpu_t* g = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int max_reads = 0, max_len = 0;
+    uint64_t max_bases = 0;
+    uint32_t cap_intv = 0, cap_calls = 0, cap_list = 0;
+    int lanes = 0;
+    // staged reads
+    int n_reads = 0;
+    HostBuf<uint8_t> h_codes;
+    HostBuf<uint64_t> h_offs;
+    DevBuf<uint8_t> d_codes;
+    DevBuf<uint64_t> d_offs;
+    // seeding outputs
+    DevBuf<Intv> d_out_intv;
+    DevBuf<uint32_t> d_out_calls, d_n_intv, d_n_calls;
+    DevBuf<int32_t> d_ctr;  // [0] head, [1] ovf_count, [2] ovf head, [3] ovf-ovf count
+    DevBuf<int32_t> d_ovf_items, d_ovf_slot, d_ovf_items2;
+    DevBuf<Intv> d_scratch;
+    // overflow pass
+    DevBuf<Intv> d_ovf_intv;
+    DevBuf<uint32_t> d_ovf_calls, d_ovf_n_intv, d_ovf_n_calls;
+    uint32_t ovf_cap_intv = 0, ovf_cap_calls = 0;
+    // compaction
+    DevBuf<uint64_t> d_sz_intv, d_sz_calls, d_intv_off, d_call_off;
+    DevBuf<uint8_t> d_scan_tmp;
+    DevBuf<Intv> d_flat_intv;
+    DevBuf<uint32_t> d_flat_calls;
+    HostBuf<int32_t> h_ctr;
+    HostBuf<uint64_t> h_tot;
+    // fetched results
+    HostBuf<Intv> h_intv;
+    HostBuf<uint32_t> h_calls;
+    HostBuf<uint64_t> h_intv_off, h_call_off;
+    bool fetched = false, ran = false;
+    uint64_t tot_intv = 0, tot_calls = 0;
+    smem_batch_stats_t stats{};
+};
+
+extern "C" {
+
+const char* smem_strerror(int code) {
+    if (g_err[0]) return g_err;
+    switch (code) {
+        case SMEM_OK: return "ok";
+        case SMEM_E_ARG: return "bad argument";
+        case SMEM_E_NOMEM: return "out of memory";
+        case SMEM_E_IO: return "i/o error";
+        case SMEM_E_DEVICE: return "HIP device error";
+        case SMEM_E_CAPACITY: return "batch capacity exceeded";
+        default: return "internal error";
+    }
+}
+
+void smem_opt_default(smem_opt_t* o) {
+    if (!o) return;
+    o->min_seed_len = 19;   // software/bwamem.c:58
+    o->split_factor = 1.5f; // software/bwamem.c:65
+    o->split_width = 10;    // software/bwamem.c:59
+    o->start_width = 1;     // software/bwamem.c:457 without MEM_F_NO_EXACT
+}
+
+int smem_gpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bwt_size, uint64_t primary,
+                  const uint64_t L2[5]) {
+    g_err[0] = 0;
+    if (!out || !bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_init: bad index");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_init: no HIP device");
+    if (device < 0 || device >= n) return fail(SMEM_E_ARG, "smem_gpu_init: device out of range");
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    smem_gpu_t* g = new (std::nothrow) smem_gpu_t();
+    if (!g) return fail(SMEM_E_NOMEM, "smem_gpu_init");
+    g->device = device;
+    g->n_cu = prop.multiProcessorCount;
+    g->bwt_size = bwt_size;
+    g->primary = primary;
+    std::memcpy(g->L2, L2, sizeof(g->L2));
+    // +16 words: a whole 64-B bucket can be loaded at the very end
+    hipError_t e = hipMalloc(&g->d_bwt, (bwt_size + 16) * sizeof(uint32_t));
+    if (e != hipSuccess) { delete g; return fail(SMEM_E_NOMEM, "smem_gpu_init: hipMalloc(index)", e); }
+    e = hipMemcpy(g->d_bwt, bwt, bwt_size * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(g->d_bwt + bwt_size, 0, 16 * sizeof(uint32_t));
+    if (e != hipSuccess) { (void)hipFree(g->d_bwt); delete g; return fail(SMEM_E_DEVICE, "smem_gpu_init: upload", e); }
+    *out = g;
+    return SMEM_OK;
+}
+
+int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
+    if (!g) return SMEM_E_ARG;
+    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 1024;
+    return SMEM_OK;
+}
+
+int smem_gpu_set_intv_cap(smem_gpu_t* g, int cap_per_read) {
+    if (!g || cap_per_read < 0) return SMEM_E_ARG;
+    g->intv_cap = cap_per_read;
+    return SMEM_OK;
+}
+
+void smem_batch_destroy(smem_batch_t* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->g->device);
+    if (b->st) (void)hipStreamSynchronize(b->st);
+    b->h_codes.release(); b->h_offs.release(); b->d_codes.release(); b->d_offs.release();
+    b->d_out_intv.release(); b->d_out_calls.release(); b->d_n_intv.release(); b->d_n_calls.release();
+    b->d_ctr.release(); b->d_ovf_items.release(); b->d_ovf_slot.release(); b->d_ovf_items2.release();
+    b->d_scratch.release(); b->d_ovf_intv.release(); b->d_ovf_calls.release(); b->d_ovf_n_intv.release();
+    b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
+    b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
+    b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
+    b->h_intv_off.release(); b->h_call_off.release();
+    for (auto& ev : b->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (b->st) (void)hipStreamDestroy(b->st);
+    delete b;
+}
+
+void smem_gpu_shutdown(smem_gpu_t* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
+    g->per_thread.clear();
+    if (g->d_bwt) (void)hipFree(g->d_bwt);
+    delete g;
+}
+
+int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_len, smem_batch_t** out) {
+    g_err[0] = 0;
+    if (!g || !out || max_reads <= 0 || max_len <= 0 || max_len > (1 << 24)) return fail(SMEM_E_ARG, "smem_batch_create");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(g->device));
+    smem_batch_t* b = new (std::nothrow) smem_batch_t();
+    if (!b) return fail(SMEM_E_NOMEM, "smem_batch_create");
+    b->g = g;
+    b->max_reads = max_reads;
+    b->max_bases = std::max<uint64_t>(max_bases, 1);
+    b->max_len = max_len;
+    // output capacity per read; reads that need more go through the overflow pass
+    b->cap_intv = g->intv_cap > 0 ? (uint32_t)g->intv_cap : (uint32_t)std::max(32, max_len / 2 + 32);
+    b->cap_calls = (uint32_t)max_len + 1;  // every list advances itr->start by >= 1
+    b->cap_list = (uint32_t)max_len + 2;   // forward/backward lists hold <= len+1 intervals
+    const int want_lanes = g->n_cu * g->lanes_per_cu;
+    const int read_lanes = (max_reads + 255) / 256 * 256;
+    b->lanes = std::max(256, std::min(want_lanes, read_lanes));
+    int rc = SMEM_OK;
+    hipError_t e = hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking);
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&b->ev[k]);
+    const size_t R = (size_t)max_reads;
+    if (e == hipSuccess) e = b->h_codes.ensure(b->max_bases);
+    if (e == hipSuccess) e = b->h_offs.ensure(R + 1);
+    if (e == hipSuccess) e = b->d_codes.ensure(b->max_bases);
+    if (e == hipSuccess) e = b->d_offs.ensure(R + 1);
+    if (e == hipSuccess) e = b->d_out_intv.ensure(R * b->cap_intv);
+    if (e == hipSuccess) e = b->d_out_calls.ensure(R * b->cap_calls);
+    if (e == hipSuccess) e = b->d_n_intv.ensure(R);
+    if (e == hipSuccess) e = b->d_n_calls.ensure(R);
+    if (e == hipSuccess) e = b->d_ctr.ensure(8);
+    if (e == hipSuccess) e = b->d_ovf_items.ensure(R);
+    if (e == hipSuccess) e = b->d_ovf_items2.ensure(R);
+    if (e == hipSuccess) e = b->d_ovf_slot.ensure(R);
+    if (e == hipSuccess) e = b->d_scratch.ensure((size_t)b->lanes * 4 * b->cap_list);
+    if (e == hipSuccess) e = b->d_sz_intv.ensure(R);
+    if (e == hipSuccess) e = b->d_sz_calls.ensure(R);
+    if (e == hipSuccess) e = b->d_intv_off.ensure(R + 1);
+    if (e == hipSuccess) e = b->d_call_off.ensure(R + 1);
+    if (e == hipSuccess) e = b->h_ctr.ensure(8);
+    if (e == hipSuccess) e = b->h_tot.ensure(4);
+    if (e == hipSuccess) e = b->h_intv_off.ensure(R + 1);
+    if (e == hipSuccess) e = b->h_call_off.ensure(R + 1);
+    if (e == hipSuccess) {
+        size_t tmp = 0;
+        e = smem_launch_offsets(nullptr, nullptr, max_reads, nullptr, &tmp, b->st);
+        if (e == hipSuccess) e = b->d_scan_tmp.ensure(tmp + 256);
+    }
+    if (e != hipSuccess) {
+        rc = fail(SMEM_E_NOMEM, "smem_batch_create: allocation", e);
+        smem_batch_destroy(b);
+        return rc;
+    }
+    b->stats.block = 256;
+    *out = b;
+    return SMEM_OK;
+}
+
+static int upload_reads(smem_batch_t* b, int n_reads) {
+    HIP_TRY(hipSetDevice(b->g->device));
+    const uint64_t nb = b->h_offs.p[n_reads];
+    HIP_TRY(hipMemcpyAsync(b->d_codes.p, b->h_codes.p, std::max<uint64_t>(nb, 1), hipMemcpyHostToDevice, b->st));
+    HIP_TRY(hipMemcpyAsync(b->d_offs.p, b->h_offs.p, sizeof(uint64_t) * (n_reads + 1), hipMemcpyHostToDevice, b->st));
+    b->n_reads = n_reads;
+    b->ran = b->fetched = false;
+    return SMEM_OK;
+}
+
+int smem_batch_set_reads(smem_batch_t* b, int n_reads, const uint8_t* const* seq, const int* len) {
+    g_err[0] = 0;
+    if (!b || n_reads < 0 || (n_reads > 0 && (!seq || !len))) return fail(SMEM_E_ARG, "smem_batch_set_reads");
+    if (n_reads > b->max_reads) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads: too many reads");
+    HIP_TRY(hipStreamSynchronize(b->st));  // staging buffer may still feed a copy
+    uint64_t o = 0;
+    for (int i = 0; i < n_reads; ++i) {
+        if (len[i] < 0 || len[i] > b->max_len) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads: read too long");
+        if (o + (uint64_t)len[i] > b->max_bases) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads: too many bases");
+        b->h_offs.p[i] = o;
+        if (len[i]) std::memcpy(b->h_codes.p + o, seq[i], (size_t)len[i]);
+        o += (uint64_t)len[i];
+    }
+    b->h_offs.p[n_reads] = o;
+    return upload_reads(b, n_reads);
+}
+
+int smem_batch_set_reads_packed(smem_batch_t* b, int n_reads, const uint8_t* codes, const uint64_t* offsets) {
+    g_err[0] = 0;
+    if (!b || n_reads < 0 || !offsets || (n_reads > 0 && !codes)) return fail(SMEM_E_ARG, "smem_batch_set_reads_packed");
+    if (n_reads > b->max_reads) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads_packed: too many reads");
+    HIP_TRY(hipStreamSynchronize(b->st));
+    const uint64_t o0 = offsets[0], nb = offsets[n_reads] - o0;
+    if (nb > b->max_bases) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads_packed: too many bases");
+    for (int i = 0; i < n_reads; ++i) {
+        const uint64_t l = offsets[i + 1] - offsets[i];
+        if (offsets[i + 1] < offsets[i] || l > (uint64_t)b->max_len)
+            return fail(SMEM_E_CAPACITY, "smem_batch_set_reads_packed: bad offsets / read too long");
+        b->h_offs.p[i] = offsets[i] - o0;
+    }
+    b->h_offs.p[n_reads] = nb;
+    if (nb) std::memcpy(b->h_codes.p, codes + o0, nb);
+    return upload_reads(b, n_reads);
+}
+
+static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& P) {
+    std::memset(&P, 0, sizeof(P));
+    P.bwt = b->g->d_bwt;
+    P.primary = b->g->primary;
+    std::memcpy(P.L2, b->g->L2, sizeof(P.L2));
+    P.codes = b->d_codes.p;
+    P.offs = b->d_offs.p;
+    P.min_seed_len = o->min_seed_len;
+    // exactly mem_insert_seed's expression (software/bwamem.c:456): int * float, + double, truncate
+    P.split_len_init = (int)(o->min_seed_len * o->split_factor + .499);
+    P.split_width = o->split_width;
+    P.start_width = o->start_width;
+    P.scratch = b->d_scratch.p;
+    P.cap_list = b->cap_list;
+}
+
+int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
+    g_err[0] = 0;
+    if (!b || !opt) return fail(SMEM_E_ARG, "smem_batch_run");
+    smem_gpu_t* g = b->g;
+    HIP_TRY(hipSetDevice(g->device));
+    const int n = b->n_reads;
+    b->fetched = false;
+    b->stats = smem_batch_stats_t{};
+    b->stats.block = 256;
+    smem::SeedParams P;
+    fill_params(b, opt, P);
+    // main pass: every read, output capacity cap_intv
+    P.read_ids = nullptr;
+    P.n_items = n;
+    P.out_intv = b->d_out_intv.p;
+    P.cap_intv = b->cap_intv;
+    P.out_call_n = b->d_out_calls.p;
+    P.cap_calls = b->cap_calls;
+    P.n_intv = b->d_n_intv.p;
+    P.n_calls = b->d_n_calls.p;
+    P.head = b->d_ctr.p + 0;
+    P.ovf_count = b->d_ctr.p + 1;
+    P.ovf_items = b->d_ovf_items.p;
+    const int lanes = std::min(b->lanes, std::max(256, (n + 255) / 256 * 256));
+    const int grid = lanes / 256;
+    b->stats.grid = grid;
+    HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
+    HIP_TRY(hipEventRecord(b->ev[0], b->st));
+    if (n > 0) HIP_TRY(smem_launch_seed(&P, grid, 256, b->st));
+    HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_ctr.p, b->d_ctr.p, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    int n_ovf = b->h_ctr.p[1];
+    b->stats.n_overflow = (uint32_t)n_ovf;
+    if (n_ovf > 0) {
+        // overflow pass: re-run the overflowed reads with a 4x larger
+        // capacity until every one fits (bounded: results are finite)
+        HIP_TRY(smem_launch_fill_i32(b->d_ovf_slot.p, -1, n, b->st));
+        uint32_t cap_i = b->cap_intv * 4, cap_c = b->cap_calls;
+        for (int round = 0;; ++round) {
+            if (round > 12) return fail(SMEM_E_INTERNAL, "smem_batch_run: overflow pass did not converge");
+            HIP_TRY(b->d_ovf_intv.ensure((size_t)n_ovf * cap_i));
+            HIP_TRY(b->d_ovf_calls.ensure((size_t)n_ovf * cap_c));
+            HIP_TRY(b->d_ovf_n_intv.ensure((size_t)n_ovf));
+            HIP_TRY(b->d_ovf_n_calls.ensure((size_t)n_ovf));
+            smem::SeedParams Q = P;
+            Q.read_ids = b->d_ovf_items.p;  // overflowed read indices (main items == reads)
+            Q.n_items = n_ovf;
+            Q.out_intv = b->d_ovf_intv.p;
+            Q.cap_intv = cap_i;
+            Q.out_call_n = b->d_ovf_calls.p;
+            Q.cap_calls = cap_c;
+            Q.n_intv = b->d_ovf_n_intv.p;
+            Q.n_calls = b->d_ovf_n_calls.p;
+            Q.head = b->d_ctr.p + 2;
+            Q.ovf_count = b->d_ctr.p + 3;
+            Q.ovf_items = b->d_ovf_items2.p;
+            HIP_TRY(hipMemsetAsync(b->d_ctr.p + 2, 0, 2 * sizeof(int32_t), b->st));
+            const int ql = std::min(b->lanes, (n_ovf + 255) / 256 * 256);
+            HIP_TRY(smem_launch_seed(&Q, std::max(1, ql / 256), 256, b->st));
+            HIP_TRY(hipMemcpyAsync(b->h_ctr.p, b->d_ctr.p, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, b->st));
+            HIP_TRY(hipStreamSynchronize(b->st));
+            if (b->h_ctr.p[3] == 0) break;
+            cap_i *= 4;
+        }
+        b->ovf_cap_intv = cap_i;
+        b->ovf_cap_calls = cap_c;
+        HIP_TRY(smem_launch_ovf_slot(b->d_ovf_items.p, n_ovf, b->d_ovf_slot.p, b->st));
+    }
+    // compaction: sizes -> offsets -> gather into flat arrays
+    HIP_TRY(hipEventRecord(b->ev[2], b->st));
+    HIP_TRY(smem_launch_sizes(b->d_n_intv.p, b->d_n_calls.p, n_ovf ? b->d_ovf_slot.p : nullptr, b->d_ovf_n_intv.p,
+                              b->d_ovf_n_calls.p, b->d_sz_intv.p, b->d_sz_calls.p, n, b->st));
+    size_t tmp = b->d_scan_tmp.n;
+    HIP_TRY(smem_launch_offsets(b->d_sz_intv.p, b->d_intv_off.p, n, b->d_scan_tmp.p, &tmp, b->st));
+    HIP_TRY(smem_launch_offsets(b->d_sz_calls.p, b->d_call_off.p, n, b->d_scan_tmp.p, &tmp, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_tot.p, b->d_intv_off.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_tot.p + 1, b->d_call_off.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    b->tot_intv = b->h_tot.p[0];
+    b->tot_calls = b->h_tot.p[1];
+    if (b->d_flat_intv.n < b->tot_intv || !b->d_flat_intv.p) {
+        // grow with headroom so steady-state runs never reallocate
+        HIP_TRY(b->d_flat_intv.ensure(std::max<size_t>(b->tot_intv + b->tot_intv / 4, (size_t)b->max_reads * 8)));
+    }
+    if (b->d_flat_calls.n < b->tot_calls || !b->d_flat_calls.p) {
+        HIP_TRY(b->d_flat_calls.ensure(std::max<size_t>(b->tot_calls + b->tot_calls / 4, (size_t)b->max_reads * 4)));
+    }
+    smem::GatherParams G;
+    G.n = n;
+    G.n_intv = b->d_n_intv.p;
+    G.main_intv = b->d_out_intv.p;
+    G.main_calls = b->d_out_calls.p;
+    G.cap_intv = b->cap_intv;
+    G.cap_calls = b->cap_calls;
+    G.ovf_slot = b->d_ovf_slot.p;
+    G.ovf_intv = b->d_ovf_intv.p;
+    G.ovf_calls = b->d_ovf_calls.p;
+    G.ovf_cap_intv = b->ovf_cap_intv;
+    G.ovf_cap_calls = b->ovf_cap_calls;
+    G.intv_off = b->d_intv_off.p;
+    G.call_off = b->d_call_off.p;
+    G.flat_intv = b->d_flat_intv.p;
+    G.flat_calls = b->d_flat_calls.p;
+    HIP_TRY(smem_launch_gather(&G, b->st));
+    HIP_TRY(hipEventRecord(b->ev[3], b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
+    b->stats.kernel_ms = ms;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev[2], b->ev[3]));
+    b->stats.compact_ms = ms;
+    b->stats.n_intv = b->tot_intv;
+    b->stats.n_calls = b->tot_calls;
+    b->ran = true;
+    return SMEM_OK;
+}
+
+int smem_batch_fetch(smem_batch_t* b) {
+    g_err[0] = 0;
+    if (!b || !b->ran) return fail(SMEM_E_ARG, "smem_batch_fetch: batch has not run");
+    HIP_TRY(hipSetDevice(b->g->device));
+    const int n = b->n_reads;
+    HIP_TRY(b->h_intv.ensure(std::max<uint64_t>(b->tot_intv, 1)));
+    HIP_TRY(b->h_calls.ensure(std::max<uint64_t>(b->tot_calls, 1)));
+    HIP_TRY(hipMemcpyAsync(b->h_intv_off.p, b->d_intv_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_call_off.p, b->d_call_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
+    if (b->tot_intv)
+        HIP_TRY(hipMemcpyAsync(b->h_intv.p, b->d_flat_intv.p, sizeof(Intv) * b->tot_intv, hipMemcpyDeviceToHost, b->st));
+    if (b->tot_calls)
+        HIP_TRY(hipMemcpyAsync(b->h_calls.p, b->d_flat_calls.p, sizeof(uint32_t) * b->tot_calls, hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    b->fetched = true;
+    return SMEM_OK;
+}
+
+int smem_batch_read(const smem_batch_t* b, int i, const smem_intv_t** intv, int* n_intv, const uint32_t** call_n,
+                    int* n_calls) {
+    if (!b || !b->fetched || i < 0 || i >= b->n_reads) return SMEM_E_ARG;
+    const uint64_t o = b->h_intv_off.p[i], co = b->h_call_off.p[i];
+    if (intv) *intv = reinterpret_cast<const smem_intv_t*>(b->h_intv.p + o);
+    if (n_intv) *n_intv = (int)(b->h_intv_off.p[i + 1] - o);
+    if (call_n) *call_n = b->h_calls.p + co;
+    if (n_calls) *n_calls = (int)(b->h_call_off.p[i + 1] - co);
+    return SMEM_OK;
+}
+
+int smem_batch_results(const smem_batch_t* b, const smem_intv_t** intv, const uint64_t** intv_off,
+                       const uint32_t** call_n, const uint64_t** call_off) {
+    if (!b || !b->fetched) return SMEM_E_ARG;
+    if (intv) *intv = reinterpret_cast<const smem_intv_t*>(b->h_intv.p);
+    if (intv_off) *intv_off = b->h_intv_off.p;
+    if (call_n) *call_n = b->h_calls.p;
+    if (call_off) *call_off = b->h_call_off.p;
+    return SMEM_OK;
+}
+
+int smem_batch_stats(const smem_batch_t* b, smem_batch_stats_t* st) {
+    if (!b || !st) return SMEM_E_ARG;
+    *st = b->stats;
+    return SMEM_OK;
+}
+
+int smem_gpu_collect(smem_gpu_t* g, int n_reads, const uint8_t* const* seq, const int* len, const smem_opt_t* opt,
+                     smem_batch_t** batch_out) {
+    g_err[0] = 0;
+    if (!g || !opt || !batch_out || n_reads < 0 || (n_reads > 0 && (!seq || !len)))
+        return fail(SMEM_E_ARG, "smem_gpu_collect");
+    *batch_out = nullptr;
+    int max_len = 1;
+    uint64_t bases = 0;
+    for (int i = 0; i < n_reads; ++i) {
+        if (len[i] < 0) return fail(SMEM_E_ARG, "smem_gpu_collect: negative length");
+        max_len = std::max(max_len, len[i]);
+        bases += (uint64_t)len[i];
+    }
+    smem_batch_t* b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        auto it = g->per_thread.find(std::this_thread::get_id());
+        if (it != g->per_thread.end()) b = it->second;
+    }
+    if (!b || b->max_reads < n_reads || b->max_len < max_len || b->max_bases < bases) {
+        const int mr = std::max(n_reads, b ? b->max_reads : 1);
+        const int ml = std::max(max_len, b ? b->max_len : 1);
+        const uint64_t mb = std::max(bases, b ? b->max_bases : 1);
+        smem_batch_t* nb = nullptr;
+        int rc = smem_batch_create(g, std::max(mr, 1), std::max<uint64_t>(mb, 1), ml, &nb);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (b) smem_batch_destroy(b);
+        g->per_thread[std::this_thread::get_id()] = nb;
+        b = nb;
+    }
+    int rc = smem_batch_set_reads(b, n_reads, seq, len);
+    if (!rc) rc = smem_batch_run(b, opt);
+    if (!rc) rc = smem_batch_fetch(b);
+    if (!rc) *batch_out = b;
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,293 @@
+"""ctypes binding of libsmemgpu.so (include/smem_gpu.h).
+
+The library is built in-tree by `make -C bwa-mem-harp2_amd` (or
+__graft_entry__.build()).  Loading fails loudly if it is missing: there is no
+Python or CPU fallback for the seeding path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libsmemgpu.so")
+
+SMEM_OK = 0
+ERRORS = {-1: "SMEM_E_ARG", -2: "SMEM_E_NOMEM", -3: "SMEM_E_IO", -4: "SMEM_E_DEVICE",
+          -5: "SMEM_E_INTERNAL", -6: "SMEM_E_CAPACITY"}
+
+# every symbol include/smem_gpu.h declares
+EXPORTED = [
+    "smem_opt_default", "smem_bwt_build", "smem_bwt_read", "smem_bwt_write", "smem_index_free",
+    "smem_gpu_device_count", "smem_gpu_init", "smem_gpu_shutdown", "smem_gpu_collect",
+    "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
+    "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
+    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_strerror",
+]
+
+
+class SmemError(RuntimeError):
+    pass
+
+
+class Intv(C.Structure):
+    _fields_ = [("x", C.c_uint64 * 3), ("info", C.c_uint64)]
+
+
+class IndexT(C.Structure):
+    _fields_ = [("primary", C.c_uint64), ("L2", C.c_uint64 * 5), ("seq_len", C.c_uint64),
+                ("bwt_size", C.c_uint64), ("bwt", C.POINTER(C.c_uint32)), ("owns", C.c_int)]
+
+
+class OptT(C.Structure):
+    _fields_ = [("min_seed_len", C.c_int), ("split_factor", C.c_float), ("split_width", C.c_int),
+                ("start_width", C.c_int)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
+                ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SmemError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` (no fallback exists)")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    lib.smem_opt_default.argtypes = [P(OptT)]
+    lib.smem_opt_default.restype = None
+    lib.smem_bwt_build.argtypes = [C.c_void_p, C.c_uint64, P(IndexT)]
+    lib.smem_bwt_read.argtypes = [C.c_char_p, P(IndexT)]
+    lib.smem_bwt_write.argtypes = [C.c_char_p, P(IndexT)]
+    lib.smem_index_free.argtypes = [P(IndexT)]
+    lib.smem_index_free.restype = None
+    lib.smem_gpu_device_count.argtypes = []
+    lib.smem_gpu_init.argtypes = [P(C.c_void_p), C.c_int, C.c_void_p, C.c_uint64, C.c_uint64, P(C.c_uint64)]
+    lib.smem_gpu_shutdown.argtypes = [C.c_void_p]
+    lib.smem_gpu_shutdown.restype = None
+    lib.smem_gpu_collect.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, P(OptT), P(C.c_void_p)]
+    lib.smem_batch_create.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_int, P(C.c_void_p)]
+    lib.smem_batch_destroy.argtypes = [C.c_void_p]
+    lib.smem_batch_destroy.restype = None
+    lib.smem_batch_set_reads.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.smem_batch_set_reads_packed.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.smem_batch_run.argtypes = [C.c_void_p, P(OptT)]
+    lib.smem_batch_fetch.argtypes = [C.c_void_p]
+    lib.smem_batch_read.argtypes = [C.c_void_p, C.c_int, P(P(Intv)), P(C.c_int), P(P(C.c_uint32)), P(C.c_int)]
+    lib.smem_batch_results.argtypes = [C.c_void_p, P(P(Intv)), P(P(C.c_uint64)), P(P(C.c_uint32)), P(P(C.c_uint64))]
+    lib.smem_batch_stats.argtypes = [C.c_void_p, P(BatchStats)]
+    lib.smem_gpu_set_lanes_per_cu.argtypes = [C.c_void_p, C.c_int]
+    lib.smem_gpu_set_intv_cap.argtypes = [C.c_void_p, C.c_int]
+    lib.smem_strerror.argtypes = [C.c_int]
+    lib.smem_strerror.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != SMEM_OK:
+        msg = load().smem_strerror(rc).decode(errors="replace")
+        raise SmemError(f"{what} failed: {ERRORS.get(rc, rc)}: {msg}")
+
+
+@dataclass
+class Options:
+    """mem_opt_t fields of the seeding loop (defaults: software/bwamem.c:58-65)."""
+    min_seed_len: int = 19
+    split_factor: float = 1.5
+    split_width: int = 10
+    start_width: int = 1
+
+    def c(self) -> OptT:
+        return OptT(self.min_seed_len, self.split_factor, self.split_width, self.start_width)
+
+
+class Index:
+    """BWA .bwt FM-index in host memory (owned by the library)."""
+
+    def __init__(self, raw: IndexT):
+        self._raw = raw
+
+    @classmethod
+    def build(cls, fwd_codes: np.ndarray) -> "Index":
+        fwd = np.ascontiguousarray(fwd_codes, dtype=np.uint8)
+        raw = IndexT()
+        _check(load().smem_bwt_build(fwd.ctypes.data, fwd.size, C.byref(raw)), "smem_bwt_build")
+        return cls(raw)
+
+    @classmethod
+    def read(cls, path: str) -> "Index":
+        raw = IndexT()
+        _check(load().smem_bwt_read(path.encode(), C.byref(raw)), f"smem_bwt_read({path})")
+        return cls(raw)
+
+    def write(self, path: str) -> None:
+        _check(load().smem_bwt_write(path.encode(), C.byref(self._raw)), f"smem_bwt_write({path})")
+
+    @property
+    def primary(self) -> int:
+        return int(self._raw.primary)
+
+    @property
+    def L2(self) -> np.ndarray:
+        return np.array(list(self._raw.L2), dtype=np.uint64)
+
+    @property
+    def seq_len(self) -> int:
+        return int(self._raw.seq_len)
+
+    @property
+    def words(self) -> np.ndarray:
+        """uint32 view (no copy) of the interleaved BWT + Occ words."""
+        n = int(self._raw.bwt_size)
+        return np.ctypeslib.as_array(self._raw.bwt, shape=(n,))
+
+    def close(self) -> None:
+        if self._raw.bwt:
+            load().smem_index_free(C.byref(self._raw))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    return int(load().smem_gpu_device_count())
+
+
+@dataclass
+class Results:
+    intv: np.ndarray      # (N, 4) uint64: x0, x1, x2, info
+    intv_off: np.ndarray  # (n_reads + 1,) uint64
+    call_n: np.ndarray    # (n_lists,) uint32
+    call_off: np.ndarray  # (n_reads + 1,) uint64
+
+    def read_calls(self, i: int) -> list:
+        """The lists smem_next2 returned for read i, in order."""
+        iv = self.intv[self.intv_off[i]:self.intv_off[i + 1]]
+        ns = self.call_n[self.call_off[i]:self.call_off[i + 1]]
+        out, p = [], 0
+        for n in ns:
+            out.append(iv[p:p + int(n)])
+            p += int(n)
+        return out
+
+    def to_smgo(self) -> bytes:
+        import struct
+        n = self.intv_off.size - 1
+        parts = [b"SMGO0001", struct.pack("<Q", n)]
+        for i in range(n):
+            calls = self.read_calls(i)
+            parts.append(struct.pack("<I", len(calls)))
+            for arr in calls:
+                parts.append(struct.pack("<I", arr.shape[0]))
+                parts.append(np.ascontiguousarray(arr, dtype="<u8").tobytes())
+        return b"".join(parts)
+
+
+class Gpu:
+    """One HIP device with the index resident in HBM (smem_gpu_init)."""
+
+    def __init__(self, index: Index, device: int = 0, lanes_per_cu: int = 0, intv_cap: int = 0):
+        lib = load()
+        self._h = C.c_void_p()
+        words = index.words
+        L2 = (C.c_uint64 * 5)(*[int(v) for v in index.L2])
+        _check(lib.smem_gpu_init(C.byref(self._h), device, words.ctypes.data, words.size, index.primary, L2),
+               "smem_gpu_init")
+        if lanes_per_cu:
+            _check(lib.smem_gpu_set_lanes_per_cu(self._h, lanes_per_cu), "smem_gpu_set_lanes_per_cu")
+        if intv_cap:
+            _check(lib.smem_gpu_set_intv_cap(self._h, intv_cap), "smem_gpu_set_intv_cap")
+        self.device = device
+
+    def batch(self, max_reads: int, max_bases: int, max_len: int) -> "Batch":
+        return Batch(self, max_reads, max_bases, max_len)
+
+    def close(self) -> None:
+        if self._h:
+            load().smem_gpu_shutdown(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batch:
+    """A worker's device-resident reads and results (smem_batch_*)."""
+
+    def __init__(self, gpu: Gpu, max_reads: int, max_bases: int, max_len: int):
+        self._gpu = gpu
+        self._h = C.c_void_p()
+        _check(load().smem_batch_create(gpu._h, max_reads, max_bases, max_len, C.byref(self._h)), "smem_batch_create")
+
+    def set_reads(self, codes: np.ndarray, offs: np.ndarray) -> None:
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        self._keep = (codes, offs)
+        _check(load().smem_batch_set_reads_packed(self._h, offs.size - 1, codes.ctypes.data, offs.ctypes.data),
+               "smem_batch_set_reads_packed")
+
+    def run(self, opt: Options = Options()) -> None:
+        o = opt.c()
+        _check(load().smem_batch_run(self._h, C.byref(o)), "smem_batch_run")
+
+    def stats(self) -> dict:
+        s = BatchStats()
+        _check(load().smem_batch_stats(self._h, C.byref(s)), "smem_batch_stats")
+        return {k: getattr(s, k) for k, _ in BatchStats._fields_}
+
+    def fetch(self) -> Results:
+        lib = load()
+        _check(lib.smem_batch_fetch(self._h), "smem_batch_fetch")
+        iv = C.POINTER(Intv)()
+        io = C.POINTER(C.c_uint64)()
+        cn = C.POINTER(C.c_uint32)()
+        co = C.POINTER(C.c_uint64)()
+        _check(lib.smem_batch_results(self._h, C.byref(iv), C.byref(io), C.byref(cn), C.byref(co)), "smem_batch_results")
+        n = int(self._keep[1].size - 1)
+        intv_off = np.ctypeslib.as_array(io, shape=(n + 1,)).copy()
+        call_off = np.ctypeslib.as_array(co, shape=(n + 1,)).copy()
+        ni, nc = int(intv_off[-1]), int(call_off[-1])
+        intv = (np.ctypeslib.as_array(C.cast(iv, C.POINTER(C.c_uint64)), shape=(max(ni, 1) * 4,))[:ni * 4]
+                .reshape(ni, 4).copy())
+        call_n = np.ctypeslib.as_array(cn, shape=(max(nc, 1),))[:nc].copy()
+        return Results(intv, intv_off, call_n, call_off)
+
+    def close(self) -> None:
+        if self._h:
+            load().smem_batch_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def seed(gpu: Gpu, codes: np.ndarray, offs: np.ndarray, opt: Options = Options()) -> Results:
+    """Seed all reads on the GPU (one batch) and return the results."""
+    offs = np.asarray(offs, dtype=np.uint64)
+    lens = np.diff(offs)
+    b = gpu.batch(max(1, offs.size - 1), max(1, int(offs[-1] - offs[0])), max(1, int(lens.max()) if lens.size else 1))
+    try:
+        b.set_reads(codes, offs)
+        b.run(opt)
+        return b.fetch()
+    finally:
+        b.close()

@@ -1,0 +1,233 @@
+"""Deterministic synthetic genomes and reads for the SMEM seeding path.
+
+There is no network and no human_g1k_v37 / E. coli index in this image, so
+every benchmark and parity case runs on seeded synthetic data of the shapes
+SURVEY.md §8(d) names (C1..C5): a random genome with diverged repeat families
+and exact/tandem repeats, reads sampled from both strands with substitutions
+and 0.1% ambiguous bases.
+
+All randomness flows from numpy's PCG64 with an explicit seed, so the same
+call always yields byte-identical output.
+
+The file formats (SMRD reads, SMGO SMEM streams) are documented in
+include/smem_formats.h.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+NT4 = np.full(256, 4, dtype=np.uint8)  # software/bntseq.c:44 (nst_nt4_table)
+for _ch, _v in zip(b"ACGTacgt", [0, 1, 2, 3, 0, 1, 2, 3]):
+    NT4[_ch] = _v
+NT4[ord("-")] = 5
+ACGT = np.frombuffer(b"ACGTN", dtype=np.uint8)
+
+
+@dataclass
+class Genome:
+    codes: np.ndarray        # uint8 0..3, all chromosomes concatenated
+    chrom_names: list
+    chrom_starts: np.ndarray  # int64 offsets into codes, len = n_chrom + 1
+
+
+def _mutate(seq: np.ndarray, rate: float, rng: np.random.Generator) -> np.ndarray:
+    out = seq.copy()
+    if rate <= 0 or out.size == 0:
+        return out
+    hit = rng.random(out.size) < rate
+    out[hit] = (out[hit] + rng.integers(1, 4, size=int(hit.sum()), dtype=np.uint8)) & 3
+    return out
+
+
+def make_genome(n_bp: int, seed: int = 1, n_chrom: int = 4, repeat_frac: float = 0.02,
+                n_families: int = 200, exact_frac: float = 0.002, tandem_frac: float = 0.001) -> Genome:
+    """Random genome with structure that exercises the SMEM path.
+
+    - repeat_frac of the genome is overwritten by copies of n_families random
+      families (300..3000 bp), each copy diverged by 0..15% substitutions and
+      inserted on a random strand (multi-occurrence intervals, re-seeding);
+    - exact_frac is covered by exact duplicated segments (long identical
+      matches, x2 >= 2);
+    - tandem_frac is covered by short-period tandem repeats / homopolymers
+      (large intervals, max_occ filtering downstream).
+    """
+    rng = np.random.default_rng(seed)
+    g = rng.integers(0, 4, size=n_bp, dtype=np.uint8)
+    if n_bp >= 5000 and repeat_frac > 0:
+        fam = [rng.integers(0, 4, size=int(rng.integers(300, 3001)), dtype=np.uint8) for _ in range(n_families)]
+        budget = int(n_bp * repeat_frac)
+        while budget > 0:
+            f = fam[int(rng.integers(0, n_families))]
+            div = float(rng.random() * 0.15)
+            c = _mutate(f, div, rng)
+            if rng.random() < 0.5:
+                c = (3 - c)[::-1]
+            if c.size >= n_bp:
+                break
+            p = int(rng.integers(0, n_bp - c.size))
+            g[p:p + c.size] = c
+            budget -= c.size
+    if n_bp >= 20000 and exact_frac > 0:
+        budget = int(n_bp * exact_frac)
+        while budget > 0:
+            ln = int(rng.integers(200, 2001))
+            src = int(rng.integers(0, n_bp - ln))
+            dst = int(rng.integers(0, n_bp - ln))
+            seg = g[src:src + ln].copy()
+            if rng.random() < 0.5:
+                seg = (3 - seg)[::-1]
+            g[dst:dst + ln] = seg
+            budget -= ln
+    if n_bp >= 20000 and tandem_frac > 0:
+        budget = int(n_bp * tandem_frac)
+        while budget > 0:
+            period = int(rng.integers(1, 7))
+            unit = rng.integers(0, 4, size=period, dtype=np.uint8)
+            ln = int(rng.integers(20, 400))
+            seg = np.resize(unit, ln)
+            dst = int(rng.integers(0, n_bp - ln))
+            g[dst:dst + ln] = seg
+            budget -= ln
+    n_chrom = max(1, min(n_chrom, n_bp // 1000 if n_bp >= 1000 else 1))
+    cuts = np.sort(rng.choice(np.arange(1, n_bp), size=n_chrom - 1, replace=False)) if n_chrom > 1 else np.array([], dtype=np.int64)
+    starts = np.concatenate([[0], cuts, [n_bp]]).astype(np.int64)
+    names = [f"chr{i + 1}" for i in range(n_chrom)]
+    return Genome(g, names, starts)
+
+
+def write_fasta(path: str, genome: Genome, width: int = 60) -> None:
+    with open(path, "wb") as fh:
+        for i, name in enumerate(genome.chrom_names):
+            s = ACGT[genome.codes[genome.chrom_starts[i]:genome.chrom_starts[i + 1]]].tobytes()
+            fh.write(b">" + name.encode() + b"\n")
+            for k in range(0, len(s), width):
+                fh.write(s[k:k + width] + b"\n")
+
+
+def forward_reverse_text(codes: np.ndarray) -> np.ndarray:
+    """The text BWA indexes: forward pac followed by its reverse complement
+    (software/bntseq.c:303-309, bns_fasta2bntseq with for_only=0)."""
+    return np.concatenate([codes, (3 - codes)[::-1]]).astype(np.uint8)
+
+
+@dataclass
+class Reads:
+    lens: np.ndarray   # int32
+    codes: np.ndarray  # uint8, concatenated
+    offs: np.ndarray   # int64, n + 1
+
+    @property
+    def n(self) -> int:
+        return int(self.lens.size)
+
+    def read(self, i: int) -> np.ndarray:
+        return self.codes[self.offs[i]:self.offs[i + 1]]
+
+    def subset(self, idx) -> "Reads":
+        idx = np.asarray(idx, dtype=np.int64)
+        parts = [self.read(int(i)) for i in idx]
+        lens = np.array([p.size for p in parts], dtype=np.int32)
+        codes = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        return Reads(lens, codes.astype(np.uint8), np.concatenate([[0], np.cumsum(lens, dtype=np.int64)]))
+
+
+def make_reads(genome_codes: np.ndarray, n_reads: int, read_len, seed: int = 1, sub_rate: float = 0.02,
+               n_rate: float = 0.001, revcomp_frac: float = 0.5, random_frac: float = 0.0) -> Reads:
+    """Sample reads uniformly from the genome (both strands).
+
+    read_len: an int (fixed) or a (lo, hi) tuple (uniform, inclusive).
+    random_frac: fraction of reads replaced by unrelated random sequence.
+    Substitutions at sub_rate, then ambiguous bases (code 4) at n_rate.
+    """
+    rng = np.random.default_rng(seed)
+    G = genome_codes.size
+    if isinstance(read_len, (tuple, list)):
+        lens = rng.integers(read_len[0], read_len[1] + 1, size=n_reads).astype(np.int32)
+    else:
+        lens = np.full(n_reads, int(read_len), dtype=np.int32)
+    lens = np.minimum(lens, G).astype(np.int32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)])
+    total = int(offs[-1])
+    codes = np.empty(total, dtype=np.uint8)
+    if n_reads and np.all(lens == lens[0]) and lens[0] > 0:
+        L = int(lens[0])
+        pos = rng.integers(0, G - L + 1, size=n_reads)
+        idx = pos[:, None] + np.arange(L)[None, :]
+        mat = genome_codes[idx]
+        rc = rng.random(n_reads) < revcomp_frac
+        mat[rc] = (3 - mat[rc])[:, ::-1]
+        codes[:] = mat.reshape(-1)
+    else:
+        pos = rng.integers(0, np.maximum(G - lens + 1, 1))
+        rc = rng.random(n_reads) < revcomp_frac
+        for i in range(n_reads):
+            s = genome_codes[pos[i]:pos[i] + lens[i]]
+            if rc[i]:
+                s = (3 - s)[::-1]
+            codes[offs[i]:offs[i + 1]] = s
+    if random_frac > 0 and n_reads:
+        rnd = np.nonzero(rng.random(n_reads) < random_frac)[0]
+        for i in rnd:
+            codes[offs[i]:offs[i + 1]] = rng.integers(0, 4, size=int(lens[i]), dtype=np.uint8)
+    if sub_rate > 0 and total:
+        hit = rng.random(total) < sub_rate
+        codes[hit] = (codes[hit] + rng.integers(1, 4, size=int(hit.sum()), dtype=np.uint8)) & 3
+    if n_rate > 0 and total:
+        codes[rng.random(total) < n_rate] = 4
+    return Reads(lens, codes, offs)
+
+
+def concat_reads(parts) -> Reads:
+    lens = np.concatenate([p.lens for p in parts]).astype(np.int32)
+    codes = np.concatenate([p.codes for p in parts]).astype(np.uint8)
+    return Reads(lens, codes, np.concatenate([[0], np.cumsum(lens, dtype=np.int64)]))
+
+
+def write_smrd(path: str, reads: Reads) -> None:
+    with open(path, "wb") as fh:
+        fh.write(b"SMRD0001")
+        fh.write(struct.pack("<QQ", reads.n, int(reads.codes.size)))
+        fh.write(reads.lens.astype("<i4").tobytes())
+        fh.write(reads.codes.astype(np.uint8).tobytes())
+
+
+def read_smrd(path: str) -> Reads:
+    with open(path, "rb") as fh:
+        data = fh.read()
+    if data[:8] != b"SMRD0001":
+        raise ValueError(f"{path}: not an SMRD file")
+    n, nb = struct.unpack_from("<QQ", data, 8)
+    lens = np.frombuffer(data, dtype="<i4", count=n, offset=24).astype(np.int32)
+    codes = np.frombuffer(data, dtype=np.uint8, count=nb, offset=24 + 4 * n).copy()
+    return Reads(lens, codes, np.concatenate([[0], np.cumsum(lens, dtype=np.int64)]))
+
+
+def read_smgo(path_or_bytes) -> list:
+    """Parse an SMGO stream into [read][call] -> (n, 4) uint64 arrays."""
+    if isinstance(path_or_bytes, (bytes, bytearray)):
+        data = bytes(path_or_bytes)
+    else:
+        with open(path_or_bytes, "rb") as fh:
+            data = fh.read()
+    if data[:8] != b"SMGO0001":
+        raise ValueError("not an SMGO stream")
+    (n_reads,) = struct.unpack_from("<Q", data, 8)
+    pos = 16
+    out = []
+    for _ in range(n_reads):
+        (nc,) = struct.unpack_from("<I", data, pos)
+        pos += 4
+        calls = []
+        for _ in range(nc):
+            (n,) = struct.unpack_from("<I", data, pos)
+            pos += 4
+            arr = np.frombuffer(data, dtype="<u8", count=4 * n, offset=pos).reshape(n, 4).copy()
+            pos += 32 * n
+            calls.append(arr)
+        out.append(calls)
+    if pos != len(data):
+        raise ValueError("trailing bytes in SMGO stream")
+    return out

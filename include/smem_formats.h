@@ -1,0 +1,75 @@
+/*
+ * smem_formats.h — on-disk formats shared by the oracle harnesses, the C host
+ * driver and the Python bindings.  Header-only, plain C99.
+ *
+ * Reads file ("SMRD0001"), little-endian:
+ *   char     magic[8]      = "SMRD0001"
+ *   uint64_t n_reads
+ *   uint64_t n_bases        total bases over all reads
+ *   int32_t  len[n_reads]
+ *   uint8_t  codes[n_bases] nt4 codes as produced by nst_nt4_table
+ *                           (software/bntseq.c:44): 0..3 = A,C,G,T, >3 = ambiguous
+ *
+ * SMEM stream file ("SMGO0001") — the exact sequence of lists returned by
+ * smem_next2() (software/bwamem.c:244-305) while mem_insert_seed()
+ * (software/bwamem.c:453-460) drives it:
+ *   char     magic[8]      = "SMGO0001"
+ *   uint64_t n_reads
+ *   per read:  uint32_t n_calls
+ *              per call: uint32_t n ; n x { uint64_t x0, x1, x2, info }
+ */
+#ifndef SMEM_FORMATS_H
+#define SMEM_FORMATS_H
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define SMRD_MAGIC "SMRD0001"
+#define SMGO_MAGIC "SMGO0001"
+
+typedef struct {
+	uint64_t n_reads, n_bases;
+	int32_t *len;
+	uint64_t *off;     /* n_reads + 1 prefix offsets (computed on load) */
+	uint8_t *codes;
+} smrd_reads_t;
+
+static inline void smrd_free(smrd_reads_t *r)
+{
+	if (!r) return;
+	free(r->len); free(r->off); free(r->codes);
+	memset(r, 0, sizeof(*r));
+}
+
+/* returns 0 on success */
+static inline int smrd_load(const char *fn, smrd_reads_t *r)
+{
+	char magic[8];
+	uint64_t i;
+	FILE *fp = fopen(fn, "rb");
+	memset(r, 0, sizeof(*r));
+	if (!fp) return -1;
+	if (fread(magic, 1, 8, fp) != 8 || memcmp(magic, SMRD_MAGIC, 8) != 0) { fclose(fp); return -2; }
+	if (fread(&r->n_reads, 8, 1, fp) != 1 || fread(&r->n_bases, 8, 1, fp) != 1) { fclose(fp); return -3; }
+	r->len = (int32_t*)malloc(sizeof(int32_t) * (r->n_reads ? r->n_reads : 1));
+	r->off = (uint64_t*)malloc(sizeof(uint64_t) * (r->n_reads + 1));
+	r->codes = (uint8_t*)malloc(r->n_bases ? r->n_bases : 1);
+	if (fread(r->len, 4, r->n_reads, fp) != r->n_reads) { fclose(fp); smrd_free(r); return -4; }
+	if (fread(r->codes, 1, r->n_bases, fp) != r->n_bases) { fclose(fp); smrd_free(r); return -5; }
+	fclose(fp);
+	r->off[0] = 0;
+	for (i = 0; i < r->n_reads; ++i) r->off[i + 1] = r->off[i] + (uint64_t)r->len[i];
+	if (r->off[r->n_reads] != r->n_bases) { smrd_free(r); return -6; }
+	return 0;
+}
+
+static inline int smgo_write_header(FILE *fp, uint64_t n_reads)
+{
+	if (fwrite(SMGO_MAGIC, 1, 8, fp) != 8) return -1;
+	if (fwrite(&n_reads, 8, 1, fp) != 1) return -1;
+	return 0;
+}
+
+#endif

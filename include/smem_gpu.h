@@ -1,0 +1,141 @@
+/*
+ * smem_gpu.h — C ABI of the MI355X SMEM seeding engine (libsmemgpu.so).
+ *
+ * Drop-in boundary for BWA-MEM's seeding loop.  In the
+ * reference, every kt_for_batch worker (software/kthread_batch.c:29-59)
+ * runs mem_chain_batched -> mem_insert_seed_batched -> smem_next2_batched ->
+ * bwt_smem1_batched (software/bwamem.c:542-591,357-451,110-241,
+ * software/bwt.c:444-774), which packs <=128 reads per FPGA hand-shake
+ * through the HARP manager thread (software/fastmap.c:320-429) and the AAL
+ * glue (software/HelloALINLB.cpp:254-485).  This library replaces that whole
+ * chain: one call seeds a batch of reads on the GPU and returns, per read,
+ * exactly the sequence of interval lists smem_next2() (software/bwamem.c:244)
+ * returns under mem_insert_seed() (software/bwamem.c:453-460) — bit-exact,
+ * in order — so the caller's chaining body (software/bwamem.c:462-499) runs
+ * unchanged.
+ *
+ * Plain C types only.  All entry points return 0 (SMEM_OK) or a negative
+ * SMEM_E_* code; on a negative code the caller may fall back to its own CPU
+ * path, mirroring the reference's reject -> CPU semantics
+ * (software/bwt.c:686-717).  No entry point silently computes on the CPU.
+ */
+#ifndef SMEM_GPU_H
+#define SMEM_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMEM_OK           0
+#define SMEM_E_ARG       -1   /* bad argument / shape */
+#define SMEM_E_NOMEM     -2   /* host or device allocation failed */
+#define SMEM_E_IO        -3   /* file I/O */
+#define SMEM_E_DEVICE    -4   /* no usable HIP device or a HIP runtime error */
+#define SMEM_E_INTERNAL  -5
+#define SMEM_E_CAPACITY  -6   /* batch larger than the capacity it was created with */
+
+/* bi-interval; identical layout to bwtintv_t (software/bwt.h:60-62):
+ * x[0] forward SA start, x[1] reverse-complement SA start, x[2] size,
+ * info = (query begin << 32) | query end (end exclusive). */
+typedef struct { uint64_t x[3], info; } smem_intv_t;
+
+/* FM-index in host memory.  The leading fields follow bwt_t
+ * (software/bwt.h:46-51): primary, L2[5], seq_len, bwt_size, bwt. */
+typedef struct {
+	uint64_t primary;     /* S^-1(0): BWT row of the $ suffix */
+	uint64_t L2[5];       /* cumulative base counts, L2[0] = 0 */
+	uint64_t seq_len;     /* = L2[4] */
+	uint64_t bwt_size;    /* number of uint32 words (Occ checkpoints interleaved) */
+	uint32_t *bwt;        /* interleaved BWT + Occ, software/bwtindex.c:128-150 layout */
+	int owns;             /* bwt was allocated by this library */
+} smem_index_t;
+
+/* the mem_opt_t fields the seeding loop reads (software/bwamem.h:44-48,
+ * software/bwamem.c:456-458) */
+typedef struct {
+	int min_seed_len;     /* -k, default 19 */
+	float split_factor;   /* -r, default 1.5 */
+	int split_width;      /* -s, default 10 */
+	int start_width;      /* 1, or 2 when MEM_F_NO_EXACT (-e) */
+} smem_opt_t;
+
+typedef struct smem_gpu smem_gpu_t;       /* one device + its resident index */
+typedef struct smem_batch smem_batch_t;   /* one worker's reads/results + HIP stream */
+
+/* defaults of mem_opt_init() (software/bwamem.c:58-65) */
+void smem_opt_default(smem_opt_t *opt);
+
+/* ---------------------------------------------------------------- index */
+/* Build the .bwt of genome codes (0..3, forward strand only; the reverse
+ * complement is appended as bns_fasta2bntseq(for_only=0) does).  Output is
+ * byte-identical to `bwa index -a is` (software/bwtindex.c:187). */
+int  smem_bwt_build(const uint8_t *fwd_codes, uint64_t n_fwd, smem_index_t *idx);
+/* .bwt file I/O (software/bwt.c:841-850, 899-918) */
+int  smem_bwt_read(const char *fn, smem_index_t *idx);
+int  smem_bwt_write(const char *fn, const smem_index_t *idx);
+void smem_index_free(smem_index_t *idx);
+
+/* --------------------------------------------------------------- device */
+/* Number of visible HIP devices (0 on a machine without a GPU). */
+int  smem_gpu_device_count(void);
+
+/* Upload the index to `device` and keep it resident in HBM.  Replaces the
+ * FPGA index upload in bwa_idx_load_bwt (software/bwa.c:286-307) and the
+ * AAL buffer setup (software/HelloALINLB.cpp:344-451).  The words are copied;
+ * the caller's arrays may be freed afterwards. */
+int  smem_gpu_init(smem_gpu_t **gpu, int device, const uint32_t *bwt, uint64_t bwt_size,
+                   uint64_t primary, const uint64_t L2[5]);
+void smem_gpu_shutdown(smem_gpu_t *gpu);
+
+/* ------------------------------------------------------------ one shot */
+/* Thread-safe; may be called concurrently from kt_for_batch workers (each
+ * calling thread gets its own stream and buffers, created on first use and
+ * freed by smem_gpu_shutdown).  seq[i] are nt4 codes (0..3, >3 ambiguous),
+ * len[i] their lengths; the results stay valid until the same thread calls
+ * smem_gpu_collect again.  Read them with smem_batch_read(*batch_out, i, ...). */
+int  smem_gpu_collect(smem_gpu_t *gpu, int n_reads, const uint8_t *const *seq, const int *len,
+                      const smem_opt_t *opt, smem_batch_t **batch_out);
+
+/* ------------------------------------------------------- batch (explicit) */
+int  smem_batch_create(smem_gpu_t *gpu, int max_reads, uint64_t max_bases, int max_len, smem_batch_t **b);
+void smem_batch_destroy(smem_batch_t *b);
+/* stage reads: per-read pointers (bseq1_t style) or one concatenated array
+ * with offsets[n_reads+1]; copied host -> device on the batch stream */
+int  smem_batch_set_reads(smem_batch_t *b, int n_reads, const uint8_t *const *seq, const int *len);
+int  smem_batch_set_reads_packed(smem_batch_t *b, int n_reads, const uint8_t *codes, const uint64_t *offsets);
+/* run the seeding loop on the resident reads; results stay in HBM */
+int  smem_batch_run(smem_batch_t *b, const smem_opt_t *opt);
+/* copy results device -> host (pinned) */
+int  smem_batch_fetch(smem_batch_t *b);
+/* per-read view of fetched results: the concatenation of all smem_next2
+ * lists in order (n_intv intervals) and the size of each list (n_calls) */
+int  smem_batch_read(const smem_batch_t *b, int i, const smem_intv_t **intv, int *n_intv,
+                     const uint32_t **call_n, int *n_calls);
+/* whole-batch views of fetched results: intv_off/call_off have n_reads+1 entries */
+int  smem_batch_results(const smem_batch_t *b, const smem_intv_t **intv, const uint64_t **intv_off,
+                        const uint32_t **call_n, const uint64_t **call_off);
+
+/* ---------------------------------------------------------- telemetry */
+typedef struct {
+	double kernel_ms;        /* seeding kernel(s), HIP events on the batch stream */
+	double compact_ms;       /* result compaction kernels */
+	uint64_t n_intv;         /* intervals produced */
+	uint64_t n_calls;        /* smem_next2 lists produced */
+	uint32_t n_overflow;     /* reads re-run with a larger output capacity */
+	int grid, block;         /* launch shape of the seeding kernel */
+} smem_batch_stats_t;
+int  smem_batch_stats(const smem_batch_t *b, smem_batch_stats_t *st);
+
+/* tuning knobs (0 = default) — lanes per CU of the persistent seeding grid */
+int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
+/* per-read output capacity (intervals) of batches created afterwards;
+ * reads needing more go through the overflow pass (0 = len/2 + 32) */
+int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
+const char *smem_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,166 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the C restatement
+(oracle/smem_oracle.c -> oracle/_build/liboracle.so) and of the compiled
+reference harness (oracle/_ref/ref_harness).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module; the product never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+CLI = os.path.join(HERE, "_build", "smem_oracle")
+REF = os.path.join(HERE, "_ref", "ref_harness")
+REF_SRC = "/root/reference/software"
+
+
+def build(ref: bool = True) -> None:
+    """Compile the restatement, and the reference harness when /root/reference exists."""
+    subprocess.run(["make", "-s", "-C", HERE, "port"], check=True)
+    if ref and os.path.isdir(REF_SRC):
+        subprocess.run(["make", "-s", "-C", HERE, "ref", "-j8"], check=True)
+
+
+class OptT(C.Structure):
+    _fields_ = [("min_seed_len", C.c_int), ("split_factor", C.c_float), ("split_width", C.c_int),
+                ("start_width", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("n_calls", "n_intv", "n_smem1", "n_ext", "n_ext_ref", "n_bkt",
+                                          "n_bkt_ref", "n_bases")]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build(ref=False)
+        lib = C.CDLL(LIB)
+        lib.orc_bwt_load.argtypes = [C.c_char_p]
+        lib.orc_bwt_load.restype = C.c_void_p
+        lib.orc_bwt_wrap.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
+        lib.orc_bwt_wrap.restype = C.c_void_p
+        lib.orc_bwt_free.argtypes = [C.c_void_p]
+        lib.orc_bwt_free.restype = None
+        lib.orc_seed.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.POINTER(OptT), C.c_int,
+                                 C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64), C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.POINTER(Stats)]
+        lib.orc_seed_timed.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.POINTER(OptT), C.c_int,
+                                       C.POINTER(Stats)]
+        lib.orc_seed_timed.restype = C.c_double
+        lib.orc_free.argtypes = [C.c_void_p]
+        lib.orc_free.restype = None
+        lib.orc_occ4.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        lib.orc_occ4.restype = None
+        _lib = lib
+    return _lib
+
+
+class OracleIndex:
+    def __init__(self, path: str | None = None, words=None, primary=None, L2=None):
+        lib = load()
+        if path is not None:
+            self._h = lib.orc_bwt_load(path.encode())
+            if not self._h:
+                raise IOError(path)
+            self._keep = None
+        else:
+            w = np.ascontiguousarray(words, dtype=np.uint32)
+            self._keep = w
+            l2 = (C.c_uint64 * 5)(*[int(v) for v in L2])
+            self._h = lib.orc_bwt_wrap(w.ctypes.data, w.size, int(primary), l2)
+
+    def occ4(self, k: int) -> np.ndarray:
+        out = (C.c_uint64 * 4)()
+        load().orc_occ4(self._h, C.c_uint64(k & 0xFFFFFFFFFFFFFFFF), out)
+        return np.array(list(out), dtype=np.uint64)
+
+    def close(self):
+        if self._h:
+            load().orc_bwt_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _opt(min_seed_len=19, split_factor=1.5, split_width=10, start_width=1) -> OptT:
+    return OptT(min_seed_len, split_factor, split_width, start_width)
+
+
+def seed(index: OracleIndex, codes: np.ndarray, offs: np.ndarray, threads: int = 1, **opt):
+    """Run the restated seeding loop. Returns (smgo_bytes, per_read dict, stats dict)."""
+    lib = load()
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    n = offs.size - 1
+    n_intv = np.zeros(max(n, 1), dtype=np.uint32)
+    n_calls = np.zeros(max(n, 1), dtype=np.uint32)
+    nbytes = np.zeros(max(n, 1), dtype=np.uint64)
+    out = C.POINTER(C.c_uint8)()
+    out_len = C.c_uint64()
+    st = Stats()
+    o = _opt(**opt)
+    rc = lib.orc_seed(index._h, n, codes.ctypes.data, offs.ctypes.data, C.byref(o), threads, C.byref(out),
+                      C.byref(out_len), n_intv.ctypes.data, n_calls.ctypes.data, nbytes.ctypes.data, C.byref(st))
+    if rc != 0:
+        raise RuntimeError("orc_seed failed")
+    data = C.string_at(out, out_len.value)
+    lib.orc_free(out)
+    return data, {"n_intv": n_intv[:n], "n_calls": n_calls[:n], "bytes": nbytes[:n]}, st.as_dict()
+
+
+def seed_stats(index: OracleIndex, codes, offs, threads: int = 1, **opt):
+    """Counters only (no stream materialised)."""
+    _, per, st = seed(index, codes, offs, threads, **opt)
+    return per, st
+
+
+def seed_timed(index: OracleIndex, codes, offs, threads: int = 1, **opt):
+    lib = load()
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    st = Stats()
+    o = _opt(**opt)
+    t = lib.orc_seed_timed(index._h, offs.size - 1, codes.ctypes.data, offs.ctypes.data, C.byref(o), threads,
+                           C.byref(st))
+    return float(t), st.as_dict()
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF)
+
+
+def ref_index(fasta: str, prefix: str) -> None:
+    """bwa index -a is via the compiled reference."""
+    subprocess.run([REF, "index", fasta, prefix], check=True, capture_output=True)
+
+
+def ref_smem(bwt: str, smrd: str, out: str, min_seed_len=19, split_factor=1.5, split_width=10, start_width=1) -> None:
+    subprocess.run([REF, "smem", bwt, smrd, out, str(min_seed_len), str(split_factor), str(split_width),
+                    str(start_width)], check=True)
+
+
+def ref_bench(bwt: str, smrd: str, threads: int, max_reads: int, min_seed_len=19, split_factor=1.5, split_width=10,
+              start_width=1) -> dict:
+    p = subprocess.run([REF, "bench", bwt, smrd, str(threads), str(max_reads), str(min_seed_len), str(split_factor),
+                        str(split_width), str(start_width)], check=True, capture_output=True, text=True)
+    kv = dict(tok.split("=") for tok in p.stdout.split())
+    return {k: float(v) for k, v in kv.items()}

@@ -1,0 +1,189 @@
+/*
+ * ref_harness.c — TEST INFRASTRUCTURE ONLY.  Drives the *unmodified* reference
+ * C sources (compiled in place from /root/reference/software by
+ * oracle/Makefile into oracle/_ref/) so that golden vectors and the
+ * "reference" CPU baseline come from the reference itself.  Nothing in the
+ * product links this file.
+ *
+ * Commands
+ *   index <in.fa> <prefix>
+ *       bwa_index(-a is) — software/bwtindex.c:187 (BWT by software/is.c:208,
+ *       Occ interleave by software/bwtindex.c:128-150, .bwt dump software/bwt.c:841)
+ *   smem  <in.bwt> <reads.smrd> <out.smgo> <k> <split_factor> <split_width> <start_width>
+ *       For every read, the mem_chain() guard (software/bwamem.c:600) and the
+ *       mem_insert_seed() loop (software/bwamem.c:453-460) calling the
+ *       reference smem_next2() (software/bwamem.c:244); every returned list
+ *       is written in SMGO format (include/smem_formats.h).
+ *   bench <in.bwt> <reads.smrd> <n_threads> <max_reads> <k> <split_factor> <split_width> <start_width>
+ *       Same loop, timed, pthreads over contiguous read chunks; prints one
+ *       line: "reads=<n> seconds=<t> threads=<T> reads_per_s=<r>".
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include <pthread.h>
+#include <sys/time.h>
+
+#include "bwt.h"
+#include "bwamem.h"
+#include "smem_formats.h"
+
+/* defined in software/bwamem.c:244 (not exported by software/bwamem.h) */
+extern const bwtintv_v *smem_next2(smem_i *itr, int split_len, int split_width, int start_width);
+/* defined in software/bwtindex.c:187 */
+extern int bwa_index(int argc, char *argv[]);
+
+static double now_s(void)
+{
+	struct timeval tv;
+	gettimeofday(&tv, 0);
+	return tv.tv_sec + tv.tv_usec * 1e-6;
+}
+
+typedef struct {
+	int k, split_width, start_width;
+	float split_factor;
+} opts_t;
+
+/* The seeding loop exactly as mem_chain()/mem_insert_seed() drive it. Emits
+ * each returned list through cb (may be NULL). Returns number of calls. */
+static int seed_one(const bwt_t *bwt, smem_i *itr, const opts_t *o, int len, const uint8_t *q,
+		FILE *out, uint64_t *n_intv)
+{
+	const bwtintv_v *a;
+	int n_calls = 0, split_len;
+	long pos = 0;
+	uint32_t zero = 0;
+	if (out) { pos = ftell(out); fwrite(&zero, 4, 1, out); }
+	if (len < o->k) goto done; /* software/bwamem.c:600 */
+	split_len = (int)(o->k * o->split_factor + .499);
+	split_len = split_len < len ? split_len : len;
+	smem_set_query(itr, len, q);
+	while ((a = smem_next2(itr, split_len, o->split_width, o->start_width)) != 0) {
+		++n_calls;
+		if (n_intv) *n_intv += a->n;
+		if (out) {
+			uint32_t n = (uint32_t)a->n;
+			size_t i;
+			fwrite(&n, 4, 1, out);
+			for (i = 0; i < a->n; ++i) {
+				uint64_t v[4] = { a->a[i].x[0], a->a[i].x[1], a->a[i].x[2], a->a[i].info };
+				fwrite(v, 8, 4, out);
+			}
+		}
+	}
+done:
+	if (out) {
+		long end = ftell(out);
+		uint32_t nc = (uint32_t)n_calls;
+		fseek(out, pos, SEEK_SET);
+		fwrite(&nc, 4, 1, out);
+		fseek(out, end, SEEK_SET);
+	}
+	(void)bwt;
+	return n_calls;
+}
+
+static int parse_opts(char **argv, opts_t *o)
+{
+	o->k = atoi(argv[0]);
+	o->split_factor = (float)atof(argv[1]);
+	o->split_width = atoi(argv[2]);
+	o->start_width = atoi(argv[3]);
+	return 0;
+}
+
+static int cmd_smem(int argc, char **argv)
+{
+	bwt_t *bwt;
+	smrd_reads_t r;
+	smem_i *itr;
+	opts_t o;
+	FILE *out;
+	uint64_t i;
+	if (argc < 8) { fprintf(stderr, "usage: smem <bwt> <reads> <out> <k> <r> <s> <start_width>\n"); return 1; }
+	parse_opts(argv + 4, &o);
+	bwt = bwt_restore_bwt(argv[1]);
+	if (smrd_load(argv[2], &r) != 0) { fprintf(stderr, "cannot load reads %s\n", argv[2]); return 1; }
+	out = fopen(argv[3], "wb");
+	if (!out) return 1;
+	smgo_write_header(out, r.n_reads);
+	itr = smem_itr_init(bwt);
+	for (i = 0; i < r.n_reads; ++i)
+		seed_one(bwt, itr, &o, r.len[i], r.codes + r.off[i], out, 0);
+	smem_itr_destroy(itr);
+	fclose(out);
+	smrd_free(&r);
+	bwt_destroy(bwt);
+	return 0;
+}
+
+typedef struct {
+	const bwt_t *bwt;
+	const smrd_reads_t *r;
+	const opts_t *o;
+	uint64_t beg, end, n_intv;
+} bench_job_t;
+
+static void *bench_worker(void *data)
+{
+	bench_job_t *j = (bench_job_t*)data;
+	smem_i *itr = smem_itr_init(j->bwt);
+	uint64_t i;
+	for (i = j->beg; i < j->end; ++i)
+		seed_one(j->bwt, itr, j->o, j->r->len[i], j->r->codes + j->r->off[i], 0, &j->n_intv);
+	smem_itr_destroy(itr);
+	return 0;
+}
+
+static int cmd_bench(int argc, char **argv)
+{
+	bwt_t *bwt;
+	smrd_reads_t r;
+	opts_t o;
+	int t, n_threads;
+	uint64_t n, n_intv = 0;
+	double t0, t1;
+	pthread_t *tid;
+	bench_job_t *jobs;
+	if (argc < 9) { fprintf(stderr, "usage: bench <bwt> <reads> <threads> <max_reads> <k> <r> <s> <sw>\n"); return 1; }
+	parse_opts(argv + 5, &o);
+	bwt = bwt_restore_bwt(argv[1]);
+	if (smrd_load(argv[2], &r) != 0) return 1;
+	n_threads = atoi(argv[3]);
+	n = (uint64_t)atoll(argv[4]);
+	if (n == 0 || n > r.n_reads) n = r.n_reads;
+	tid = (pthread_t*)calloc(n_threads, sizeof(pthread_t));
+	jobs = (bench_job_t*)calloc(n_threads, sizeof(bench_job_t));
+	t0 = now_s();
+	for (t = 0; t < n_threads; ++t) {
+		jobs[t].bwt = bwt; jobs[t].r = &r; jobs[t].o = &o;
+		jobs[t].beg = n * t / n_threads; jobs[t].end = n * (t + 1) / n_threads;
+		pthread_create(&tid[t], 0, bench_worker, &jobs[t]);
+	}
+	for (t = 0; t < n_threads; ++t) { pthread_join(tid[t], 0); n_intv += jobs[t].n_intv; }
+	t1 = now_s();
+	printf("reads=%llu seconds=%.6f threads=%d reads_per_s=%.3f intervals=%llu\n",
+			(unsigned long long)n, t1 - t0, n_threads, n / (t1 - t0), (unsigned long long)n_intv);
+	free(tid); free(jobs); smrd_free(&r); bwt_destroy(bwt);
+	return 0;
+}
+
+int main(int argc, char **argv)
+{
+	if (argc < 2) {
+		fprintf(stderr, "usage: ref_harness index|smem|bench ...\n");
+		return 1;
+	}
+	if (strcmp(argv[1], "index") == 0) {
+		char *av[7];
+		if (argc < 4) return 1;
+		av[0] = "index"; av[1] = "-a"; av[2] = "is"; av[3] = "-p"; av[4] = argv[3]; av[5] = argv[2]; av[6] = 0;
+		return bwa_index(6, av);
+	}
+	if (strcmp(argv[1], "smem") == 0) return cmd_smem(argc - 1, argv + 1);
+	if (strcmp(argv[1], "bench") == 0) return cmd_bench(argc - 1, argv + 1);
+	fprintf(stderr, "unknown command %s\n", argv[1]);
+	return 1;
+}

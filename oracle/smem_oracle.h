@@ -1,0 +1,88 @@
+/*
+ * smem_oracle.h — TEST INFRASTRUCTURE ONLY (parity checker + CPU "port"
+ * baseline).  A plain-C restatement of the reference SMEM seeding path:
+ *
+ *   mem_insert_seed loop   software/bwamem.c:453-460
+ *   smem_next2             software/bwamem.c:244-305
+ *   bwt_smem1              software/bwt.c:776-835
+ *   bwt_extend             software/bwt.c:416-429
+ *   bwt_2occ4 / bwt_occ4   software/bwt.c:207-215 / 187-204
+ *   .bwt reader            software/bwt.c:899-918
+ *
+ * Pinned against golden vectors produced by the compiled reference
+ * (oracle/_ref/ref_harness, see tests/golden/make_golden.py).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it; the
+ * product (bwa-mem-harp2_amd/) never links it.
+ */
+#ifndef SMEM_ORACLE_H
+#define SMEM_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+	uint64_t primary;
+	uint64_t L2[5];
+	uint64_t seq_len;
+	uint64_t bwt_size;     /* in uint32 words, Occ checkpoints included */
+	uint32_t *bwt;
+	uint32_t cnt_table[256];
+	int owns;
+} orc_bwt_t;
+
+typedef struct { uint64_t x[3], info; } orc_intv_t;
+
+typedef struct {
+	int min_seed_len;      /* -k, software/bwamem.c:58 */
+	float split_factor;    /* -r, software/bwamem.c:65 */
+	int split_width;       /* -s, software/bwamem.c:59 */
+	int start_width;       /* 1, or 2 with MEM_F_NO_EXACT (software/bwamem.c:457) */
+} orc_opt_t;
+
+typedef struct {
+	uint64_t n_calls;       /* non-NULL smem_next2 returns */
+	uint64_t n_intv;        /* intervals returned */
+	uint64_t n_smem1;       /* bwt_smem1 invocations */
+	uint64_t n_ext;         /* bwt_extend calls whose result is used */
+	uint64_t n_ext_ref;     /* bwt_extend calls the reference makes (incl. c<0 ones) */
+	uint64_t n_bkt;         /* distinct 64-B Occ buckets over n_ext (1 or 2 each) */
+	uint64_t n_bkt_ref;     /* same over n_ext_ref */
+	uint64_t n_bases;       /* query bases of reads that entered the loop */
+} orc_stats_t;
+
+orc_bwt_t *orc_bwt_load(const char *fn);
+/* wrap caller memory (not copied, not freed) */
+orc_bwt_t *orc_bwt_wrap(const uint32_t *bwt, uint64_t bwt_size, uint64_t primary, const uint64_t L2[5]);
+void orc_bwt_free(orc_bwt_t *b);
+
+void orc_occ4(const orc_bwt_t *b, uint64_t k, uint64_t cnt[4]);
+void orc_extend(const orc_bwt_t *b, const orc_intv_t *ik, orc_intv_t ok[4], int is_back);
+
+/*
+ * Seed n_reads reads (codes concatenated, offs[n_reads+1]).  For each read
+ * writes the SMGO record into *out (malloc'ed, caller frees with
+ * orc_free) when out != NULL, and accumulates stats.  Also fills
+ * per-read arrays when non-NULL: n_intv_per_read, n_calls_per_read,
+ * bytes_per_read (algorithmic bytes).
+ * n_threads > 1 splits reads into contiguous chunks (pthreads).
+ * Returns 0 on success.
+ */
+int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,
+		const orc_opt_t *opt, int n_threads,
+		uint8_t **out, uint64_t *out_len,
+		uint32_t *n_intv_per_read, uint32_t *n_calls_per_read, uint64_t *bytes_per_read,
+		orc_stats_t *stats);
+
+/* timed variant for the CPU baseline: seeds reads, returns wall seconds */
+double orc_seed_timed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,
+		const orc_opt_t *opt, int n_threads, orc_stats_t *stats);
+
+void orc_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,66 @@
+"""Loader for the committed golden fixtures (tests/golden/, made by
+tests/golden/make_golden.py from the compiled reference)."""
+import gzip
+import hashlib
+import json
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _gz(name: str) -> bytes:
+    with gzip.open(os.path.join(GOLDEN, name), "rb") as fh:
+        return fh.read()
+
+
+def fasta_codes(data: bytes) -> np.ndarray:
+    from smemgpu import synth
+    seq = b"".join(line for line in data.split(b"\n") if line and not line.startswith(b">"))
+    return synth.NT4[np.frombuffer(seq, dtype=np.uint8)]
+
+
+@dataclass
+class Fixture:
+    manifest: dict
+    genome: np.ndarray
+    bwt_bytes: bytes
+    reads: object
+    index: object
+
+    @property
+    def cases(self):
+        return self.manifest["cases"]
+
+    def stream(self, case) -> bytes:
+        data = _gz(f"g1_{case['name']}.smgo.gz")
+        assert hashlib.sha256(data).hexdigest() == case["sha256"], "fixture corrupted"
+        return data
+
+
+_cache = None
+
+
+def load() -> Fixture:
+    global _cache
+    if _cache is None:
+        import tempfile
+        import smemgpu
+        from smemgpu import synth
+        with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+            manifest = json.load(fh)
+        genome = fasta_codes(_gz("g1.fa.gz"))
+        bwt_bytes = _gz("g1.bwt.gz")
+        with tempfile.TemporaryDirectory() as d:
+            p = os.path.join(d, "r1.smrd")
+            with open(p, "wb") as fh:
+                fh.write(_gz("r1.smrd.gz"))
+            reads = synth.read_smrd(p)
+            b = os.path.join(d, "g1.bwt")
+            with open(b, "wb") as fh:
+                fh.write(bwt_bytes)
+            index = smemgpu.Index.read(b)
+        _cache = Fixture(manifest, genome, bwt_bytes, reads, index)
+    return _cache

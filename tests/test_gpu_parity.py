@@ -1,0 +1,179 @@
+"""GPU parity: the HIP seeding path (through the C ABI) against the oracle.
+
+Bar: bit-exact — every interval list smem_next2 would return, in order
+(SURVEY.md §8(b) parity unit).  Cases cover the edge cases the reference's
+code paths have: ambiguous bases (software/bwt.c:800-803, bwamem.c:252),
+reads shorter than the seed length (bwamem.c:600), split_len = len
+(bwamem.c:458), -e start width 2 (bwamem.c:457), re-seeding and the ordered
+merge (bwamem.c:272-301), multi-occurrence / tandem intervals, random
+reads, output-capacity overflow, empty batches, and concurrent host workers.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+OPTS = {
+    "default": dict(min_seed_len=19, split_factor=1.5, split_width=10, start_width=1),
+    "noexact": dict(min_seed_len=19, split_factor=1.5, split_width=10, start_width=2),
+    "k14s20": dict(min_seed_len=14, split_factor=1.5, split_width=20, start_width=1),
+    "reseed": dict(min_seed_len=19, split_factor=1.0, split_width=500, start_width=1),
+    "k30": dict(min_seed_len=30, split_factor=2.0, split_width=3, start_width=1),
+}
+
+
+@pytest.fixture(scope="module")
+def world(gpu_device):
+    import smemgpu
+    from smemgpu import synth
+    genome = synth.make_genome(400_000, seed=21)
+    idx = smemgpu.Index.build(genome.codes)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    ref = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
+    yield dict(genome=genome, idx=idx, gpu=gpu, ref=ref)
+    gpu.close()
+
+
+def _reads(genome, kind, seed):
+    from smemgpu import synth
+    g = genome.codes
+    if kind == "150bp":
+        return synth.make_reads(g, 2000, 150, seed=seed)
+    if kind == "mixed":
+        return synth.concat_reads([
+            synth.make_reads(g, 500, (1, 320), seed=seed, n_rate=0.02),
+            synth.make_reads(g, 200, (15, 40), seed=seed + 1),
+            synth.make_reads(g, 200, 101, seed=seed + 2, sub_rate=0.05, random_frac=0.3),
+        ])
+    if kind == "250bp5":
+        return synth.make_reads(g, 800, 250, seed=seed, sub_rate=0.05)
+    raise ValueError(kind)
+
+
+def _compare(world, reads, opt, **gpu_kw):
+    import smemgpu
+    want, per, st = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4, **opt)
+    res = smemgpu.seed(world["gpu"], reads.codes, reads.offs, smemgpu.Options(**opt))
+    got = res.to_smgo()
+    if got != want:
+        from smemgpu import synth
+        a, b = synth.read_smgo(got), synth.read_smgo(want)
+        bad = [i for i in range(len(b)) if len(a[i]) != len(b[i]) or any(
+            x.shape != y.shape or (x != y).any() for x, y in zip(a[i], b[i]))]
+        pytest.fail(f"{len(bad)} reads differ, first {bad[:5]}")
+    return st
+
+
+@pytest.mark.parametrize("kind", ["150bp", "mixed", "250bp5"])
+@pytest.mark.parametrize("optname", list(OPTS))
+def test_parity_vs_oracle(world, kind, optname):
+    reads = _reads(world["genome"], kind, seed=100 + len(optname))
+    st = _compare(world, reads, OPTS[optname])
+    assert st["n_intv"] > 0
+
+
+def test_parity_golden_fixture(gpu_device):
+    """GPU vs the compiled reference's own output on the committed fixture."""
+    import smemgpu
+    from smemgpu import synth
+    from tests import golden_data
+    fx = golden_data.load()
+    gpu = smemgpu.Gpu(fx.index, device=gpu_device)
+    try:
+        for case in fx.cases:
+            reads = fx.reads.subset(np.arange(case["n_reads"]))
+            res = smemgpu.seed(gpu, reads.codes, reads.offs, smemgpu.Options(**case["opt"]))
+            assert res.to_smgo() == fx.stream(case), case["name"]
+    finally:
+        gpu.close()
+
+
+def test_edge_cases(world):
+    from smemgpu import synth
+    g = world["genome"].codes
+    parts = []
+    lens = [0, 1, 2, 18, 19, 20, 28, 29, 30, 31]
+    for L in lens:
+        parts.append(synth.Reads(np.array([L], np.int32), g[1000:1000 + L].copy(),
+                                 np.array([0, L], np.int64)))
+    # all-N, N at both ends, alternating Ns, poly-A
+    for arr in (np.full(60, 4, np.uint8), np.concatenate([[4], g[5000:5100], [4]]).astype(np.uint8),
+                np.where(np.arange(120) % 7 == 0, 4, g[9000:9120]).astype(np.uint8), np.zeros(150, np.uint8)):
+        parts.append(synth.Reads(np.array([arr.size], np.int32), arr, np.array([0, arr.size], np.int64)))
+    reads = synth.concat_reads(parts)
+    for opt in OPTS.values():
+        _compare(world, reads, opt)
+
+
+def test_empty_batch(world):
+    import smemgpu
+    res = smemgpu.seed(world["gpu"], np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    assert res.intv.shape == (0, 4)
+    assert res.intv_off.tolist() == [0]
+
+
+def test_overflow_pass(world, gpu_device):
+    """Tiny per-read output capacity forces the overflow re-run path."""
+    import smemgpu
+    from smemgpu import synth
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, intv_cap=2)
+    try:
+        reads = _reads(world["genome"], "mixed", seed=7)
+        want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4)
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        assert b.stats()["n_overflow"] > 0
+        assert b.fetch().to_smgo() == want
+        b.close()
+    finally:
+        gpu.close()
+
+
+def test_few_lanes_many_reads_per_lane(world, gpu_device):
+    import smemgpu
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, lanes_per_cu=64)
+    try:
+        reads = _reads(world["genome"], "150bp", seed=9)
+        want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4)
+        assert smemgpu.seed(gpu, reads.codes, reads.offs).to_smgo() == want
+    finally:
+        gpu.close()
+
+
+def test_batch_reuse(world):
+    """One batch object, several runs with different reads (no stale state)."""
+    from smemgpu import synth
+    g = world["genome"].codes
+    r1 = synth.make_reads(g, 700, 150, seed=31)
+    r2 = synth.make_reads(g, 300, (20, 150), seed=32, n_rate=0.01)
+    b = world["gpu"].batch(1000, 200_000, 150)
+    for r in (r1, r2, r1):
+        want, _, _ = oracle.seed(world["ref"], r.codes, r.offs, threads=4)
+        b.set_reads(r.codes, r.offs)
+        b.run()
+        assert b.fetch().to_smgo() == want
+    b.close()
+
+
+def test_host_driver_threads(world, tmp_path):
+    """The C host driver (kt_for_batch workers calling smem_gpu_collect
+    concurrently) writes the same stream as the oracle."""
+    from smemgpu import synth
+    from smemgpu.lib import PKG_DIR
+    reads = _reads(world["genome"], "mixed", seed=41)
+    bwt = str(tmp_path / "g.bwt")
+    world["idx"].write(bwt)
+    smrd = str(tmp_path / "r.smrd")
+    synth.write_smrd(smrd, reads)
+    out = str(tmp_path / "o.smgo")
+    exe = os.path.join(PKG_DIR, "bin", "smem_seed")
+    subprocess.run([exe, "-t", "4", "-b", "97", bwt, smrd, out], check=True, timeout=300)
+    want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4)
+    with open(out, "rb") as fh:
+        assert fh.read() == want
