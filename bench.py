@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--sub", type=float, default=0.02)
     p.add_argument("--genome-mbp", type=float, default=100.0)
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu", help="index construction (same bytes)")
     p.add_argument("--lanes-per-cu", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--stats-sample", type=int, default=20000, help="reads counted by the oracle for bytes/read")
@@ -75,11 +76,11 @@ def get_index(args, rank, world, barrier):
     if rank == 0 and not os.path.exists(key):
         t = time.time()
         g = synth.make_genome(n_bp, seed=args.seed, n_chrom=24)
-        idx = smemgpu.Index.build(g.codes)
+        idx = smemgpu.Index.build_gpu(g.codes, device=0) if args.builder == "gpu" else smemgpu.Index.build(g.codes)
         idx.write(key + ".tmp")
         os.replace(key + ".tmp", key)
         del g
-        log(f"index built: {n_bp} bp genome, {idx.words.nbytes / 1e6:.1f} MB in {time.time() - t:.1f} s")
+        log(f"index built ({args.builder}): {n_bp} bp genome, {idx.words.nbytes / 1e6:.1f} MB in {time.time() - t:.1f} s")
     barrier()
     return smemgpu.Index.read(key), key
 

@@ -44,10 +44,13 @@ static void worker(void *data, int start, int batch, int tid)
 {
 	shared_t *s = (shared_t*)data;
 	smem_gpu_t *g = s->gpus[tid % s->n_gpus];
-	const uint8_t **seq = (const uint8_t**)malloc(sizeof(*seq) * batch);
-	int *len = (int*)malloc(sizeof(int) * batch);
+	const uint8_t **seq;
+	int *len;
 	smem_batch_t *b = 0;
 	int i, rc;
+	if (batch <= 0) return;
+	seq = (const uint8_t**)malloc(sizeof(*seq) * batch);
+	len = (int*)malloc(sizeof(int) * batch);
 	for (i = 0; i < batch; ++i) {
 		seq[i] = s->reads->codes + s->reads->off[start + i];
 		len[i] = s->reads->len[start + i];

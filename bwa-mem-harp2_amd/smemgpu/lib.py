@@ -21,7 +21,7 @@ ERRORS = {-1: "SMEM_E_ARG", -2: "SMEM_E_NOMEM", -3: "SMEM_E_IO", -4: "SMEM_E_DEV
 
 # every symbol include/smem_gpu.h declares
 EXPORTED = [
-    "smem_opt_default", "smem_bwt_build", "smem_bwt_read", "smem_bwt_write", "smem_index_free",
+    "smem_opt_default", "smem_bwt_build", "smem_bwt_build_gpu", "smem_bwt_read", "smem_bwt_write", "smem_index_free",
     "smem_gpu_device_count", "smem_gpu_init", "smem_gpu_shutdown", "smem_gpu_collect",
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
@@ -66,6 +66,7 @@ def load() -> C.CDLL:
     lib.smem_opt_default.argtypes = [P(OptT)]
     lib.smem_opt_default.restype = None
     lib.smem_bwt_build.argtypes = [C.c_void_p, C.c_uint64, P(IndexT)]
+    lib.smem_bwt_build_gpu.argtypes = [C.c_int, C.c_void_p, C.c_uint64, P(IndexT)]
     lib.smem_bwt_read.argtypes = [C.c_char_p, P(IndexT)]
     lib.smem_bwt_write.argtypes = [C.c_char_p, P(IndexT)]
     lib.smem_index_free.argtypes = [P(IndexT)]
@@ -122,6 +123,14 @@ class Index:
         fwd = np.ascontiguousarray(fwd_codes, dtype=np.uint8)
         raw = IndexT()
         _check(load().smem_bwt_build(fwd.ctypes.data, fwd.size, C.byref(raw)), "smem_bwt_build")
+        return cls(raw)
+
+    @classmethod
+    def build_gpu(cls, fwd_codes: np.ndarray, device: int = 0) -> "Index":
+        """Same bytes as build(), constructed on a HIP device (prefix doubling)."""
+        fwd = np.ascontiguousarray(fwd_codes, dtype=np.uint8)
+        raw = IndexT()
+        _check(load().smem_bwt_build_gpu(device, fwd.ctypes.data, fwd.size, C.byref(raw)), "smem_bwt_build_gpu")
         return cls(raw)
 
     @classmethod

@@ -72,6 +72,9 @@ void smem_opt_default(smem_opt_t *opt);
  * complement is appended as bns_fasta2bntseq(for_only=0) does).  Output is
  * byte-identical to `bwa index -a is` (software/bwtindex.c:187). */
 int  smem_bwt_build(const uint8_t *fwd_codes, uint64_t n_fwd, smem_index_t *idx);
+/* Same .bwt, built on a HIP device by prefix doubling + radix sort
+ * (seconds for Gbp genomes); 2 x n_fwd must stay below 2^32 - 1. */
+int  smem_bwt_build_gpu(int device, const uint8_t *fwd_codes, uint64_t n_fwd, smem_index_t *idx);
 /* .bwt file I/O (software/bwt.c:841-850, 899-918) */
 int  smem_bwt_read(const char *fn, smem_index_t *idx);
 int  smem_bwt_write(const char *fn, const smem_index_t *idx);

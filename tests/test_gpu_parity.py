@@ -177,3 +177,25 @@ def test_host_driver_threads(world, tmp_path):
     want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4)
     with open(out, "rb") as fh:
         assert fh.read() == want
+
+
+@pytest.mark.parametrize("n_bp,seed", [(1, 1), (7, 2), (64, 3), (1000, 4), (4099, 5), (250_000, 6)])
+def test_gpu_index_builder_matches_cpu(gpu_device, n_bp, seed):
+    """smem_bwt_build_gpu (prefix doubling) == smem_bwt_build (SA-IS) byte for byte;
+    the CPU builder is itself pinned to `bwa index -a is` (tests/test_oracle.py)."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(n_bp, seed=seed, n_chrom=1)
+    a = smemgpu.Index.build(g.codes)
+    b = smemgpu.Index.build_gpu(g.codes, device=gpu_device)
+    assert a.primary == b.primary and a.L2.tolist() == b.L2.tolist()
+    assert np.array_equal(a.words, b.words)
+
+
+def test_gpu_index_builder_golden(gpu_device):
+    import smemgpu
+    from tests import golden_data
+    fx = golden_data.load()
+    b = smemgpu.Index.build_gpu(fx.genome, device=gpu_device)
+    assert b.primary == fx.index.primary
+    assert np.array_equal(b.words, fx.index.words)
