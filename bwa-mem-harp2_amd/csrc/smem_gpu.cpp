@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -23,6 +24,7 @@
 #include "smem_gpu.h"
 #include "smem_kernels.h"
 
+using smem::CallRec;
 using smem::Intv;
 
 static_assert(sizeof(Intv) == sizeof(smem_intv_t), "interval layout");
@@ -92,6 +94,7 @@ struct smem_gpu {
     int n_cu = 0;
     int lanes_per_cu = 1024;
     int intv_cap = 0;
+    int variant = 2;  // 2: cooperative LDS-DMA bucket fetch, 1: per-lane fetch
     uint32_t* d_bwt = nullptr;
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
     std::mutex mu;
@@ -113,14 +116,16 @@ struct smem_batch {
     DevBuf<uint8_t> d_codes;
     DevBuf<uint64_t> d_offs;
     // seeding outputs
-    DevBuf<Intv> d_out_intv;
-    DevBuf<uint32_t> d_out_calls, d_n_intv, d_n_calls;
+    DevBuf<Intv> d_out_intv;       // raw per-read lists
+    DevBuf<CallRec> d_out_call;    // per-read list records
+    DevBuf<uint32_t> d_n_intv, d_n_calls;
     DevBuf<int32_t> d_ctr;  // [0] head, [1] ovf_count, [2] ovf head, [3] ovf-ovf count
     DevBuf<int32_t> d_ovf_items, d_ovf_slot, d_ovf_items2;
-    DevBuf<Intv> d_scratch;
+    DevBuf<uint4> d_scratch;
     // overflow pass
     DevBuf<Intv> d_ovf_intv;
-    DevBuf<uint32_t> d_ovf_calls, d_ovf_n_intv, d_ovf_n_calls;
+    DevBuf<CallRec> d_ovf_call;
+    DevBuf<uint32_t> d_ovf_n_intv, d_ovf_n_calls;
     uint32_t ovf_cap_intv = 0, ovf_cap_calls = 0;
     // compaction
     DevBuf<uint64_t> d_sz_intv, d_sz_calls, d_intv_off, d_call_off;
@@ -171,6 +176,8 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
                   const uint64_t L2[5]) {
     g_err[0] = 0;
     if (!out || !bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_init: bad index");
+    // packed list entries hold SA coordinates in 34 bits
+    if (L2[4] >= (1ull << 34) - 2) return fail(SMEM_E_ARG, "smem_gpu_init: seq_len >= 2^34 not supported");
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_init: no HIP device");
@@ -201,6 +208,12 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
     return SMEM_OK;
 }
 
+int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
+    if (!g || variant < 0 || variant > 2) return SMEM_E_ARG;
+    g->variant = variant == 0 ? 2 : variant;
+    return SMEM_OK;
+}
+
 int smem_gpu_set_intv_cap(smem_gpu_t* g, int cap_per_read) {
     if (!g || cap_per_read < 0) return SMEM_E_ARG;
     g->intv_cap = cap_per_read;
@@ -212,9 +225,9 @@ void smem_batch_destroy(smem_batch_t* b) {
     (void)hipSetDevice(b->g->device);
     if (b->st) (void)hipStreamSynchronize(b->st);
     b->h_codes.release(); b->h_offs.release(); b->d_codes.release(); b->d_offs.release();
-    b->d_out_intv.release(); b->d_out_calls.release(); b->d_n_intv.release(); b->d_n_calls.release();
+    b->d_out_intv.release(); b->d_out_call.release(); b->d_n_intv.release(); b->d_n_calls.release();
     b->d_ctr.release(); b->d_ovf_items.release(); b->d_ovf_slot.release(); b->d_ovf_items2.release();
-    b->d_scratch.release(); b->d_ovf_intv.release(); b->d_ovf_calls.release(); b->d_ovf_n_intv.release();
+    b->d_scratch.release(); b->d_ovf_intv.release(); b->d_ovf_call.release(); b->d_ovf_n_intv.release();
     b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
     b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
@@ -247,7 +260,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     b->max_len = max_len;
     // output capacity per read; reads that need more go through the overflow pass
     b->cap_intv = g->intv_cap > 0 ? (uint32_t)g->intv_cap : (uint32_t)std::max(32, max_len / 2 + 32);
-    b->cap_calls = (uint32_t)max_len + 1;  // every list advances itr->start by >= 1
+    b->cap_calls = (uint32_t)(max_len / 4 + 16);  // ~6 lists per 150 bp read; more -> overflow pass
     b->cap_list = (uint32_t)max_len + 2;   // forward/backward lists hold <= len+1 intervals
     const int want_lanes = g->n_cu * g->lanes_per_cu;
     const int read_lanes = (max_reads + 255) / 256 * 256;
@@ -258,17 +271,17 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     const size_t R = (size_t)max_reads;
     if (e == hipSuccess) e = b->h_codes.ensure(b->max_bases);
     if (e == hipSuccess) e = b->h_offs.ensure(R + 1);
-    if (e == hipSuccess) e = b->d_codes.ensure(b->max_bases);
+    if (e == hipSuccess) e = b->d_codes.ensure(b->max_bases + 32);  // 16-B query windows may read past the end
     if (e == hipSuccess) e = b->d_offs.ensure(R + 1);
     if (e == hipSuccess) e = b->d_out_intv.ensure(R * b->cap_intv);
-    if (e == hipSuccess) e = b->d_out_calls.ensure(R * b->cap_calls);
+    if (e == hipSuccess) e = b->d_out_call.ensure(R * b->cap_calls);
     if (e == hipSuccess) e = b->d_n_intv.ensure(R);
     if (e == hipSuccess) e = b->d_n_calls.ensure(R);
     if (e == hipSuccess) e = b->d_ctr.ensure(8);
     if (e == hipSuccess) e = b->d_ovf_items.ensure(R);
     if (e == hipSuccess) e = b->d_ovf_items2.ensure(R);
     if (e == hipSuccess) e = b->d_ovf_slot.ensure(R);
-    if (e == hipSuccess) e = b->d_scratch.ensure((size_t)b->lanes * 4 * b->cap_list);
+    if (e == hipSuccess) e = b->d_scratch.ensure((size_t)b->lanes * 2 * b->cap_list);  // 2 packed lists per lane
     if (e == hipSuccess) e = b->d_sz_intv.ensure(R);
     if (e == hipSuccess) e = b->d_sz_calls.ensure(R);
     if (e == hipSuccess) e = b->d_intv_off.ensure(R + 1);
@@ -351,6 +364,8 @@ static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& 
     P.start_width = o->start_width;
     P.scratch = b->d_scratch.p;
     P.cap_list = b->cap_list;
+    const char* dbg = getenv("SMEM_DEBUG_FLAGS");
+    P.dbg = dbg ? atoi(dbg) : 0;
 }
 
 int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
@@ -364,12 +379,12 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->stats.block = 256;
     smem::SeedParams P;
     fill_params(b, opt, P);
-    // main pass: every read, output capacity cap_intv
+    // main pass: every read, output capacity cap_intv / cap_calls
     P.read_ids = nullptr;
     P.n_items = n;
     P.out_intv = b->d_out_intv.p;
     P.cap_intv = b->cap_intv;
-    P.out_call_n = b->d_out_calls.p;
+    P.out_call = b->d_out_call.p;
     P.cap_calls = b->cap_calls;
     P.n_intv = b->d_n_intv.p;
     P.n_calls = b->d_n_calls.p;
@@ -381,21 +396,21 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->stats.grid = grid;
     HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
-    if (n > 0) HIP_TRY(smem_launch_seed(&P, grid, 256, b->st));
+    if (n > 0) HIP_TRY(smem_launch_seed(&P, grid, 256, g->variant, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
     HIP_TRY(hipMemcpyAsync(b->h_ctr.p, b->d_ctr.p, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, b->st));
     HIP_TRY(hipStreamSynchronize(b->st));
     int n_ovf = b->h_ctr.p[1];
     b->stats.n_overflow = (uint32_t)n_ovf;
     if (n_ovf > 0) {
-        // overflow pass: re-run the overflowed reads with a 4x larger
-        // capacity until every one fits (bounded: results are finite)
+        // overflow pass: re-run the overflowed reads with larger capacities
+        // until every one fits (bounded: results are finite)
         HIP_TRY(smem_launch_fill_i32(b->d_ovf_slot.p, -1, n, b->st));
-        uint32_t cap_i = b->cap_intv * 4, cap_c = b->cap_calls;
+        uint32_t cap_i = b->cap_intv * 4, cap_c = (uint32_t)b->max_len + 1;  // <= len lists per read
         for (int round = 0;; ++round) {
             if (round > 12) return fail(SMEM_E_INTERNAL, "smem_batch_run: overflow pass did not converge");
             HIP_TRY(b->d_ovf_intv.ensure((size_t)n_ovf * cap_i));
-            HIP_TRY(b->d_ovf_calls.ensure((size_t)n_ovf * cap_c));
+            HIP_TRY(b->d_ovf_call.ensure((size_t)n_ovf * cap_c));
             HIP_TRY(b->d_ovf_n_intv.ensure((size_t)n_ovf));
             HIP_TRY(b->d_ovf_n_calls.ensure((size_t)n_ovf));
             smem::SeedParams Q = P;
@@ -403,7 +418,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
             Q.n_items = n_ovf;
             Q.out_intv = b->d_ovf_intv.p;
             Q.cap_intv = cap_i;
-            Q.out_call_n = b->d_ovf_calls.p;
+            Q.out_call = b->d_ovf_call.p;
             Q.cap_calls = cap_c;
             Q.n_intv = b->d_ovf_n_intv.p;
             Q.n_calls = b->d_ovf_n_calls.p;
@@ -412,7 +427,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
             Q.ovf_items = b->d_ovf_items2.p;
             HIP_TRY(hipMemsetAsync(b->d_ctr.p + 2, 0, 2 * sizeof(int32_t), b->st));
             const int ql = std::min(b->lanes, (n_ovf + 255) / 256 * 256);
-            HIP_TRY(smem_launch_seed(&Q, std::max(1, ql / 256), 256, b->st));
+            HIP_TRY(smem_launch_seed(&Q, std::max(1, ql / 256), 256, g->variant, b->st));
             HIP_TRY(hipMemcpyAsync(b->h_ctr.p, b->d_ctr.p, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, b->st));
             HIP_TRY(hipStreamSynchronize(b->st));
             if (b->h_ctr.p[3] == 0) break;
@@ -422,10 +437,29 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
         b->ovf_cap_calls = cap_c;
         HIP_TRY(smem_launch_ovf_slot(b->d_ovf_items.p, n_ovf, b->d_ovf_slot.p, b->st));
     }
-    // compaction: sizes -> offsets -> gather into flat arrays
+    // finalize: raw lists -> smem_next2 lists (count, scan, write)
     HIP_TRY(hipEventRecord(b->ev[2], b->st));
-    HIP_TRY(smem_launch_sizes(b->d_n_intv.p, b->d_n_calls.p, n_ovf ? b->d_ovf_slot.p : nullptr, b->d_ovf_n_intv.p,
-                              b->d_ovf_n_calls.p, b->d_sz_intv.p, b->d_sz_calls.p, n, b->st));
+    smem::FinalizeParams F;
+    std::memset(&F, 0, sizeof(F));
+    F.n = n;
+    F.offs = b->d_offs.p;
+    F.n_intv = b->d_n_intv.p;
+    F.n_calls = b->d_n_calls.p;
+    F.main_intv = b->d_out_intv.p;
+    F.main_call = b->d_out_call.p;
+    F.cap_intv = b->cap_intv;
+    F.cap_calls = b->cap_calls;
+    F.ovf_slot = b->d_ovf_slot.p;
+    F.ovf_intv = b->d_ovf_intv.p;
+    F.ovf_call = b->d_ovf_call.p;
+    F.ovf_n_calls = b->d_ovf_n_calls.p;
+    F.ovf_cap_intv = b->ovf_cap_intv;
+    F.ovf_cap_calls = b->ovf_cap_calls;
+    F.s_intv = b->d_sz_intv.p;
+    F.s_calls = b->d_sz_calls.p;
+    F.intv_off = b->d_intv_off.p;
+    F.call_off = b->d_call_off.p;
+    HIP_TRY(smem_launch_finalize(&F, 0, b->st));
     size_t tmp = b->d_scan_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_sz_intv.p, b->d_intv_off.p, n, b->d_scan_tmp.p, &tmp, b->st));
     HIP_TRY(smem_launch_offsets(b->d_sz_calls.p, b->d_call_off.p, n, b->d_scan_tmp.p, &tmp, b->st));
@@ -441,23 +475,9 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     if (b->d_flat_calls.n < b->tot_calls || !b->d_flat_calls.p) {
         HIP_TRY(b->d_flat_calls.ensure(std::max<size_t>(b->tot_calls + b->tot_calls / 4, (size_t)b->max_reads * 4)));
     }
-    smem::GatherParams G;
-    G.n = n;
-    G.n_intv = b->d_n_intv.p;
-    G.main_intv = b->d_out_intv.p;
-    G.main_calls = b->d_out_calls.p;
-    G.cap_intv = b->cap_intv;
-    G.cap_calls = b->cap_calls;
-    G.ovf_slot = b->d_ovf_slot.p;
-    G.ovf_intv = b->d_ovf_intv.p;
-    G.ovf_calls = b->d_ovf_calls.p;
-    G.ovf_cap_intv = b->ovf_cap_intv;
-    G.ovf_cap_calls = b->ovf_cap_calls;
-    G.intv_off = b->d_intv_off.p;
-    G.call_off = b->d_call_off.p;
-    G.flat_intv = b->d_flat_intv.p;
-    G.flat_calls = b->d_flat_calls.p;
-    HIP_TRY(smem_launch_gather(&G, b->st));
+    F.flat_intv = b->d_flat_intv.p;
+    F.flat_calls = b->d_flat_calls.p;
+    HIP_TRY(smem_launch_finalize(&F, 1, b->st));
     HIP_TRY(hipEventRecord(b->ev[3], b->st));
     HIP_TRY(hipStreamSynchronize(b->st));
     float ms = 0.f;

@@ -25,7 +25,7 @@ EXPORTED = [
     "smem_gpu_device_count", "smem_gpu_init", "smem_gpu_shutdown", "smem_gpu_collect",
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
-    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_strerror",
+    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_strerror",
 ]
 
 
@@ -88,6 +88,7 @@ def load() -> C.CDLL:
     lib.smem_batch_stats.argtypes = [C.c_void_p, P(BatchStats)]
     lib.smem_gpu_set_lanes_per_cu.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_set_intv_cap.argtypes = [C.c_void_p, C.c_int]
+    lib.smem_gpu_set_kernel_variant.argtypes = [C.c_void_p, C.c_int]
     lib.smem_strerror.argtypes = [C.c_int]
     lib.smem_strerror.restype = C.c_char_p
     _lib = lib
@@ -208,7 +209,7 @@ class Results:
 class Gpu:
     """One HIP device with the index resident in HBM (smem_gpu_init)."""
 
-    def __init__(self, index: Index, device: int = 0, lanes_per_cu: int = 0, intv_cap: int = 0):
+    def __init__(self, index: Index, device: int = 0, lanes_per_cu: int = 0, intv_cap: int = 0, variant: int = 0):
         lib = load()
         self._h = C.c_void_p()
         words = index.words
@@ -219,6 +220,8 @@ class Gpu:
             _check(lib.smem_gpu_set_lanes_per_cu(self._h, lanes_per_cu), "smem_gpu_set_lanes_per_cu")
         if intv_cap:
             _check(lib.smem_gpu_set_intv_cap(self._h, intv_cap), "smem_gpu_set_intv_cap")
+        if variant:
+            _check(lib.smem_gpu_set_kernel_variant(self._h, variant), "smem_gpu_set_kernel_variant")
         self.device = device
 
     def batch(self, max_reads: int, max_bases: int, max_len: int) -> "Batch":

@@ -136,6 +136,9 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
 /* per-read output capacity (intervals) of batches created afterwards;
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
+/* seeding-kernel variant: 2 (default) cooperative LDS-DMA Occ-bucket fetch,
+ * 1 per-lane fetch; both bit-exact, kept for A/B measurement */
+int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
 const char *smem_strerror(int code);
 
 #ifdef __cplusplus

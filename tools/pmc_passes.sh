@@ -1,0 +1,21 @@
+#!/bin/bash
+# Counter passes for the seeding kernel (one rocprofv3 run per pass; no trace
+# domains combined with --pmc).  Usage: tools/pmc_passes.sh <outdir> [prof_run args]
+set -o pipefail
+OUT=${1:-gpurun_out/pmc}; shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PASSES=(
+  "FETCH_SIZE"
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM"
+  "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS TA_TA_BUSY TA_TOTAL_WAVEFRONTS"
+  "TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ TCP_PENDING_STALL_CYCLES TCP_TCP_TA_DATA_STALL_CYCLES TCC_HIT TCC_MISS TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM"
+  "TCP_UTCL1_REQUEST TCP_UTCL1_TRANSLATION_MISS TCP_TCC_READ_REQ_LATENCY TD_TD_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES"
+  "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU"
+)
+i=0
+for P in "${PASSES[@]}"; do
+  timeout -k 10 240 rocprofv3 --pmc $P --kernel-include-regex seed_kernel --output-format csv -d "$OUT" -o pass$i -- python tools/prof_run.py "$@" > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  i=$((i+1))
+done
+echo "all passes ok"
