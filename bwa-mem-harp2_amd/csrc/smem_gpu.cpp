@@ -92,9 +92,9 @@ struct HostBuf {
 struct smem_gpu {
     int device = 0;
     int n_cu = 0;
-    int lanes_per_cu = 1024;
+    int lanes_per_cu = 768;  // 3 blocks of 256 per CU: the default kernel runs 3 waves/SIMD
     int intv_cap = 0;
-    int variant = 2;  // 2: cooperative LDS-DMA bucket fetch, 1: per-lane fetch
+    int variant = 2;  // see smem_gpu_set_kernel_variant
     uint32_t* d_bwt = nullptr;
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
     std::mutex mu;
@@ -122,6 +122,7 @@ struct smem_batch {
     DevBuf<int32_t> d_ctr;  // [0] head, [1] ovf_count, [2] ovf head, [3] ovf-ovf count
     DevBuf<int32_t> d_ovf_items, d_ovf_slot, d_ovf_items2;
     DevBuf<uint4> d_scratch;
+    DevBuf<uint64_t> d_dbg;        // stamped variant only
     // overflow pass
     DevBuf<Intv> d_ovf_intv;
     DevBuf<CallRec> d_ovf_call;
@@ -178,6 +179,10 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
     if (!out || !bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_init: bad index");
     // packed list entries hold SA coordinates in 34 bits
     if (L2[4] >= (1ull << 34) - 2) return fail(SMEM_E_ARG, "smem_gpu_init: seq_len >= 2^34 not supported");
+    // Occ buckets are addressed as 32-bit byte offsets from the index base
+    // (seq_len up to ~8.5 Gbp: both strands of a human genome are 6.2 Gbp)
+    if ((bwt_size + 16) * sizeof(uint32_t) > (1ull << 32))
+        return fail(SMEM_E_ARG, "smem_gpu_init: index larger than 4 GiB not supported");
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_init: no HIP device");
@@ -204,12 +209,12 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
 
 int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
     if (!g) return SMEM_E_ARG;
-    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 1024;
+    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 768;
     return SMEM_OK;
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || variant < 0 || variant > 2) return SMEM_E_ARG;
+    if (!g || variant < 0 || (variant > 3 && variant != 9)) return SMEM_E_ARG;
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }
@@ -227,7 +232,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->h_codes.release(); b->h_offs.release(); b->d_codes.release(); b->d_offs.release();
     b->d_out_intv.release(); b->d_out_call.release(); b->d_n_intv.release(); b->d_n_calls.release();
     b->d_ctr.release(); b->d_ovf_items.release(); b->d_ovf_slot.release(); b->d_ovf_items2.release();
-    b->d_scratch.release(); b->d_ovf_intv.release(); b->d_ovf_call.release(); b->d_ovf_n_intv.release();
+    b->d_scratch.release(); b->d_dbg.release(); b->d_ovf_intv.release(); b->d_ovf_call.release(); b->d_ovf_n_intv.release();
     b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
     b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
@@ -250,6 +255,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
 int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_len, smem_batch_t** out) {
     g_err[0] = 0;
     if (!g || !out || max_reads <= 0 || max_len <= 0 || max_len > (1 << 24)) return fail(SMEM_E_ARG, "smem_batch_create");
+    if (max_bases >= (1ull << 32) - 64) return fail(SMEM_E_ARG, "smem_batch_create: >= 2^32 bases per batch");
     *out = nullptr;
     HIP_TRY(hipSetDevice(g->device));
     smem_batch_t* b = new (std::nothrow) smem_batch_t();
@@ -396,6 +402,11 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->stats.grid = grid;
     HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
+    if (g->variant == 9) {
+        HIP_TRY(b->d_dbg.ensure((size_t)grid * 4 * 8));
+        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, (size_t)grid * 4 * 8 * sizeof(uint64_t), b->st));
+        P.dbg_buf = b->d_dbg.p;
+    }
     if (n > 0) HIP_TRY(smem_launch_seed(&P, grid, 256, g->variant, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
     HIP_TRY(hipMemcpyAsync(b->h_ctr.p, b->d_ctr.p, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, b->st));
@@ -528,6 +539,13 @@ int smem_batch_results(const smem_batch_t* b, const smem_intv_t** intv, const ui
     if (call_n) *call_n = b->h_calls.p;
     if (call_off) *call_off = b->h_call_off.p;
     return SMEM_OK;
+}
+
+int smem_batch_debug(const smem_batch_t* b, uint64_t* out, uint64_t n_words) {
+    if (!b || !out || !b->d_dbg.p) return SMEM_E_ARG;
+    const uint64_t n = std::min<uint64_t>(n_words, b->d_dbg.n);
+    if (hipMemcpy(out, b->d_dbg.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return SMEM_E_DEVICE;
+    return (int)n;
 }
 
 int smem_batch_stats(const smem_batch_t* b, smem_batch_stats_t* st) {

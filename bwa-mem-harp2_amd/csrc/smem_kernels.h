@@ -41,6 +41,7 @@ struct SeedParams {
     uint4* scratch;            // per lane: 2 * cap_list packed 16-B list entries
     uint32_t cap_list;
     int dbg;                   // debug switches (0 in production)
+    uint64_t* dbg_buf;         // stamped diagnostic variant: 8 x u64 per wave
 };
 
 // raw logs -> final smem_next2 lists (reverse + ordered merge, software/bwamem.c:280-301)

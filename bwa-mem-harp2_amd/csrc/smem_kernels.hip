@@ -88,15 +88,11 @@ __device__ __forceinline__ uint64_t p_x1(const uint4& v) { return (uint64_t)((v.
 __device__ __forceinline__ uint64_t p_x2(const uint4& v) { return (uint64_t)((v.w >> 4) & 3) << 32 | v.z; }
 __device__ __forceinline__ uint32_t p_end(const uint4& v) { return v.w >> 6; }
 
-// ---- query bases through a 16-byte register window (one load per 16 bases)
-__device__ __forceinline__ int qget(const uint8_t* __restrict__ codes, uint64_t o0, int i, uint4& qv, uint64_t& qb) {
-    const uint64_t a = o0 + (uint64_t)i;
-    const uint64_t blk = a & ~15ull;
-    if (blk != qb) {
-        qv = *reinterpret_cast<const uint4*>(codes + blk);
-        qb = blk;
-    }
-    const uint32_t sel = (uint32_t)(a >> 2) & 3;
+// ---- query bases through a 16-byte window held in registers; the window
+// is loaded in the uniform section (the state machine yields until it is)
+__device__ __forceinline__ int qsel(uint32_t o0, int i, const uint4& qv) {
+    const uint32_t a = o0 + (uint32_t)i;  // batches hold < 2^32 bases
+    const uint32_t sel = (a >> 2) & 3;
     const uint32_t w = sel == 0 ? qv.x : (sel == 1 ? qv.y : (sel == 2 ? qv.z : qv.w));
     return (int)((w >> ((a & 3) * 8)) & 0xff);
 }
@@ -118,38 +114,62 @@ enum Phase : int {
 
 constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
 
-// LDS image of the wave's Occ buckets: [wave][k|l][lane][4 x 16 B]
+// Wave-private LDS: the Occ bucket images [k|l][lane][4 x 16 B] and one
+// 16-B landing slot per lane for prev[j+1] and for the query window, all
+// filled by LDS-DMA (10 KB per wave, 40 KB per 256-thread block).
 struct WaveLds {
     uint4 k[64][4];
     uint4 l[64][4];
+    uint4 pn[64];
+    uint4 q[64];
 };
 
 // Fetch the 64-B Occ buckets of every live lane.  COOP: each wave-instruction
 // moves 16 whole buckets (4 lanes x 16 B per bucket, one L1 access each)
 // straight into the wave's LDS image with LDS-DMA; the owner lane then reads
 // its bucket from LDS.  !COOP: each lane loads its own bucket (4 x 16 B).
-template <bool COOP>
+// The lane id, recomputed where it is used: the register allocator would
+// otherwise keep it (and addresses derived from it) live across the whole
+// state machine, or spill them.
+__device__ __forceinline__ int vlane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// bucket b's 16-B chunk as scalar base + 32-bit byte offset (the host keeps
+// the index below 4 GiB), so the DMA takes the saddr form
+__device__ __forceinline__ const uint32_t* boff(const uint32_t* __restrict__ bwt, uint32_t b, uint32_t chunk) {
+    return reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(bwt) + (b * 64u + chunk * 4u));
+}
+
+template <bool COOP, int AUX>
 __device__ __forceinline__ void fetch_buckets(const uint32_t* __restrict__ bwt, WaveLds* W, int lane, bool want,
                                               uint64_t kk, uint64_t ll, Bucket& vk, Bucket& vl) {
     const bool needl = want && (kk >> 7) != (ll >> 7);
     if constexpr (COOP) {
         const uint32_t bk = want ? (uint32_t)(kk >> 7) : NO_BUCKET;
         const uint32_t bl = needl ? (uint32_t)(ll >> 7) : NO_BUCKET;
+        lane = vlane();
         const uint32_t chunk = (uint32_t)(lane & 3) * 4;
+        // all 8 source lookups first (one LDS wait), then the 8 DMAs
+        uint32_t sk[4], sl[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const uint32_t s = __shfl(bk, 16 * r + (lane >> 2));
-            if (s != NO_BUCKET)
-                __builtin_amdgcn_global_load_lds(bwt + (uint64_t)s * 16 + chunk,
-                                                 (__attribute__((address_space(3))) void*)&W->k[16 * r][0], 16, 0, 0);
+            const int src = (16 * r + (lane >> 2)) << 2;  // ds_bpermute byte address
+            sk[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)bk);
+            sl[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)bl);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t s = __shfl(bl, 16 * r + (lane >> 2));
-            if (s != NO_BUCKET)
-                __builtin_amdgcn_global_load_lds(bwt + (uint64_t)s * 16 + chunk,
-                                                 (__attribute__((address_space(3))) void*)&W->l[16 * r][0], 16, 0, 0);
-        }
+        for (int r = 0; r < 4; ++r)
+            if (sk[r] != NO_BUCKET)
+                __builtin_amdgcn_global_load_lds(boff(bwt, sk[r], chunk),
+                                                 (__attribute__((address_space(3))) void*)&W->k[16 * r][0], 16, 0, AUX);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (sl[r] != NO_BUCKET)
+                __builtin_amdgcn_global_load_lds(boff(bwt, sl[r], chunk),
+                                                 (__attribute__((address_space(3))) void*)&W->l[16 * r][0], 16, 0, AUX);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         vk = Bucket{W->k[lane][0], W->k[lane][1], W->k[lane][2], W->k[lane][3]};
         const int ls = needl ? 1 : 0;  // read the l image only where it was fetched
@@ -190,33 +210,56 @@ __device__ __forceinline__ void extend_counts(const SeedParams& P, uint64_t a, u
     nb = b + (uint64_t)(a <= P.primary && a + s - 1 >= P.primary) + gt;
 }
 
-// Overwrite the query window with the 16-byte block holding position pos,
-// ahead of its use, so the load is in flight with this iteration's buckets.
-__device__ __forceinline__ void qprefetch(const uint8_t* __restrict__ codes, uint64_t o0, int pos, uint4& qv,
-                                          uint64_t& qb) {
-    const uint64_t blk = (o0 + (uint64_t)pos) & ~15ull;
-    if (blk != qb) {
-        qv = *reinterpret_cast<const uint4*>(codes + blk);
-        qb = blk;
+// offsets of work item `it` (read_ids maps overflow-pass items to reads)
+__device__ __forceinline__ void next_offsets(const SeedParams& P, int it, uint32_t& o0, int& len) {
+    if (it >= P.n_items) {
+        len = 0;
+        return;
     }
+    const int rid = P.read_ids ? P.read_ids[it] : it;
+    const uint64_t a = P.offs[rid], b = P.offs[rid + 1];
+    o0 = (uint32_t)a;
+    len = (int)(b - a);
 }
 
-template <bool COOP>
-__global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
-    __shared__ WaveLds lds[COOP ? 4 : 1];  // COOP: 4 waves per 256-thread block, 8 KB each
+// AUX: cache-policy bits of the LDS-DMA loads (0 default, 2 nt, 16 sc1, 17 sc0|sc1)
+// chip-wide 100 MHz clock: wave start / end times comparable across XCDs
+__device__ __forceinline__ uint64_t rtstamp() {
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+// STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
+template <bool COOP, int AUX, bool STAMP, int WPE, bool FAST>
+__global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
+    __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
     const int lane = threadIdx.x & 63;
-    WaveLds* W = &lds[COOP ? (threadIdx.x >> 6) : 0];
+    WaveLds* W = &lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const uint64_t lane_g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t cap = P.cap_list;
     // per-lane scratch: two packed lists (B0 | B1) used as forward / prev / curr
     PIntv* __restrict__ bp = reinterpret_cast<PIntv*>(P.scratch + lane_g * 2ull * cap);
 
+    // All loads the state machine needs are issued in the uniform section
+    // below, next to the bucket DMAs, and consumed in the following
+    // iteration: a load consumed inside the divergent advance would stall
+    // the whole wave for one memory round trip.  A lane whose next step needs
+    // data that is not in flight yet "yields" one iteration instead.
     int phase = P_FETCH;
     int item = -1, len = 0;
-    uint64_t o0 = 0, qb = ~0ull;
+    int nitem = 0, nlen = -2;  // next read: -2 nothing claimed, -1 claimed, >= 0 offsets loaded
+    uint32_t o0 = 0, no0 = 0;
+    uint32_t qb = ~0u, qwant = ~0u;      // 16-B query window held / wanted (offsets into codes)
     uint4 qv = {0, 0, 0, 0};
-    uint32_t raw_n = 0, calls_n = 0;   // raw intervals / lists logged for the read
-    int start = 0, ori_start = 0, split_len = 0;
+    uint32_t raw_n = 0, calls_n = 0;     // raw intervals / lists logged for the read
+    int start = 0, ori_start = 0;
     int x = 0, min_intv = 1, middle = 0, i = 0, j = 0, ret = 0, cur_c = 0;
     uint64_t ik0 = 0, ik1 = 0, ik2 = 0;
     uint32_t ikend = 0;
@@ -226,12 +269,22 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
     // longest match of the first bwt_smem1 (software/bwamem.c:266-270), tracked
     // as matches are emitted: pushes come in reverse final order, so ">="
     // keeps the first maximum in final order
-    uint32_t max_len = 0;
-    uint64_t max_x2 = 0, max_info = 0;
-    uint4 pc = {0, 0, 0, 0}, pn = {0, 0, 0, 0}, head = {0, 0, 0, 0};
+    uint32_t max_len = 0, max_x2 = 0, max_mid = 0;  // x2 saturated to 32 bits
+    uint4 pn = {0, 0, 0, 0}, head = {0, 0, 0, 0};  // prev[j+1] in flight, curr[0]
     uint64_t na = 0, nb = 0, ns = 0;
+    uint64_t st_adv = 0, st_fetch = 0, st_comp = 0, st_iter = 0, st_active = 0, st_t0 = 0, st_t1 = 0;
+    if constexpr (STAMP) st_t0 = rtstamp();
+
+#define QBLK(pos) ((o0 + (uint32_t)(pos)) & ~15u)
+#define YIELD_FOR(pos)            \
+    {                             \
+        qwant = QBLK(pos);        \
+        break;                    \
+    }
 
     for (;;) {
+        uint64_t ta = 0;
+        if constexpr (STAMP) ta = stamp();
         // ---- advance the state machine until the lane needs an extend ----
         // one transition per pass (every block ends in continue/break: this
         // keeps the register allocation at 4 waves/SIMD); blocks are ordered
@@ -244,42 +297,47 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                         if (raw_n >= P.cap_intv) {
                             phase = P_OVF;
                         } else {
-                            const uint64_t info = (uint64_t)p_end(pc) | ((uint64_t)(i + 1) << 32);
-                            P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{p_x0(pc), p_x1(pc), p_x2(pc), info};
+                            const uint64_t info = (uint64_t)ikend | ((uint64_t)(i + 1) << 32);
+                            P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{ik0, ik1, ik2, info};
                             ++mem_n;
                             mem_last_start = (uint32_t)(i + 1);
-                            if (!middle && p_end(pc) - (uint32_t)(i + 1) >= max_len) {
-                                max_len = p_end(pc) - (uint32_t)(i + 1);
-                                max_x2 = p_x2(pc);
-                                max_info = info;
+                            if (!middle && ikend - (uint32_t)(i + 1) >= max_len) {
+                                max_len = ikend - (uint32_t)(i + 1);
+                                max_x2 = ik2 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ik2;
+                                max_mid = (ikend + (uint32_t)(i + 1)) >> 1;
                             }
                         }
                     }
                 } else if (curr_n == 0 || ns != curr_last_x2) {
-                    const uint4 e = pack_p(na, nb, ns, p_end(pc));
+                    const uint4 e = pack_p(na, nb, ns, ikend);
                     *reinterpret_cast<uint4*>(bp + curr_off + curr_n) = e;
                     if (curr_n == 0) head = e;  // prev[0] of the next step
                     ++curr_n;
                     curr_last_x2 = ns;
                 }
                 ++j;
-                if (phase != P_OVF) phase = P_BWD_J;
+                if (phase == P_OVF) continue;
+                if (FAST && (uint32_t)j < prev_n) {  // fast path: extend prev[j] right away (P_BWD_J, j > 0)
+                    ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
+                    break;
+                }
+                phase = P_BWD_J;
                 continue;
             }
             if (phase == P_BWD_J) {
                 if ((uint32_t)j < prev_n) {
-                    pc = pn;
-                    if ((uint32_t)j + 1 < prev_n) pn = load_p(bp + prev_off + j + 1);  // prefetch prev[j+1]
-                    if (j == 0 && i > 0 && !(P.dbg & 1)) qprefetch(P.codes, o0, i - 1, qv, qb);       // next step's base
+                    // prev[j] (loaded by the previous iteration) into the ik registers
+                    ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
+                    if (j == 0 && i > 0) qwant = QBLK(i - 1);  // next step's base
                     phase = P_BWD_RES;
-                    break;  // -> extend (backward)
+                    break;  // -> extend (backward); prev[j+1] is fetched meanwhile
                 }
                 if (curr_n == 0) {
                     phase = P_SMEM_END;  // software/bwt.c:827
                 } else {
                     prev_off = curr_off;
                     prev_n = curr_n;
-                    pn = (P.dbg & 2) ? load_p(bp + curr_off) : head;  // curr[0], kept in registers
+                    pn = head;  // curr[0], kept in registers
                     curr_off = curr_off == cap ? 0 : cap;
                     --i;
                     phase = P_BWD_STEP;
@@ -295,20 +353,29 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 }
                 if (stop) {
                     phase = P_FWD_DONE;
-                } else {
-                    ik0 = nb; ik1 = na; ik2 = ns;
-                    ikend = (uint32_t)(i + 1);
-                    ++i;
-                    phase = P_FWD;
+                    continue;
                 }
+                ik0 = nb; ik1 = na; ik2 = ns;
+                ikend = (uint32_t)(i + 1);
+                ++i;
+                if (FAST && i < len && QBLK(i) == qb) {  // fast path: the next forward extend (P_FWD)
+                    const int qi = qsel(o0, i, qv);
+                    if (qi < 4) {
+                        cur_c = 3 - qi;
+                        if (i + 1 < len) qwant = QBLK(i + 1);
+                        break;
+                    }
+                }
+                phase = P_FWD;
                 continue;
             }
             if (phase == P_FWD) {
                 if (i < len) {
-                    const int qi = qget(P.codes, o0, i, qv, qb);
+                    if (QBLK(i) != qb) YIELD_FOR(i);
+                    const int qi = qsel(o0, i, qv);
                     if (qi < 4) {
                         cur_c = 3 - qi;
-                        if (i + 1 < len && !(P.dbg & 1)) qprefetch(P.codes, o0, i + 1, qv, qb);
+                        if (i + 1 < len) qwant = QBLK(i + 1);
                         phase = P_FWD_RES;
                         break;  // -> extend (forward)
                     }
@@ -321,9 +388,10 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
             }
             if (phase == P_FWD_DONE) {
                 // the last push becomes prev[0] after the reversal; it is always the
-                // current ik (the stop path pushes ik without advancing it)
-                pn = (P.dbg & 2) ? load_p(bp + cap - fwd_n) : pack_p(ik0, ik1, ik2, ikend);
-                ret = (int)p_end(pn);
+                // current ik (the stop path pushes ik without advancing it).  From
+                // here on ik holds the backward interval being extended (prev[j]).
+                pn = pack_p(ik0, ik1, ik2, ikend);
+                ret = (int)ikend;
                 prev_off = cap - fwd_n;  // pushed downward: ascending = reversed
                 prev_n = fwd_n;
                 curr_off = cap;
@@ -332,7 +400,8 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 continue;
             }
             if (phase == P_BWD_STEP) {
-                cur_c = i < 0 ? -1 : qget(P.codes, o0, i, qv, qb);
+                if (i >= 0 && QBLK(i) != qb) YIELD_FOR(i);
+                cur_c = i < 0 ? -1 : qsel(o0, i, qv);
                 if (cur_c > 3) cur_c = -1;
                 curr_n = 0;
                 if (cur_c < 0) {
@@ -347,8 +416,8 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                             mem_last_start = (uint32_t)(i + 1);
                             if (!middle && p_end(pn) - (uint32_t)(i + 1) >= max_len) {
                                 max_len = p_end(pn) - (uint32_t)(i + 1);
-                                max_x2 = p_x2(pn);
-                                max_info = info;
+                                max_x2 = p_x2(pn) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)p_x2(pn);
+                                max_mid = (p_end(pn) + (uint32_t)(i + 1)) >> 1;
                             }
                         }
                     }
@@ -356,7 +425,6 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 } else {
                     j = 0;
                     phase = P_BWD_J;
-                    continue;
                 }
                 continue;
             }
@@ -364,10 +432,12 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 if (!middle) {  // software/bwamem.c:261-272
                     start = ret;
                     m_n = mem_n;
+                    // split_len = min(k * split_factor + .499, len) (software/bwamem.c:456-458)
+                    const int split_len = P.split_len_init < len ? P.split_len_init : len;
                     if (m_n > 0 && split_len > 0 && (int)max_len >= split_len &&
-                        max_x2 <= (uint64_t)(int64_t)P.split_width) {
+                        (uint64_t)max_x2 <= (uint64_t)(int64_t)P.split_width) {
                         // re-seed from the middle of the longest SMEM (software/bwamem.c:272-278)
-                        x = (int)(((uint64_t)(uint32_t)max_info + (max_info >> 32)) >> 1);
+                        x = (int)max_mid;
                         min_intv = (int)(max_x2 + 1);
                         middle = 1;
                         phase = P_SMEM_BEGIN;
@@ -393,9 +463,17 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 continue;
             }
             if (phase == P_NEXT2) {  // software/bwamem.c:247-261
-                if (start < len && start >= 0)
-                    while (start < len && qget(P.codes, o0, start, qv, qb) > 3) ++start;  // skip ambiguous bases
-                if (start >= len || start < 0) {                                         // iterator exhausted
+                bool wait_q = false;
+                if (start < len && start >= 0) {
+                    for (;;) {  // skip ambiguous bases
+                        if (start >= len) break;
+                        if (QBLK(start) != qb) { wait_q = true; break; }
+                        if (qsel(o0, start, qv) <= 3) break;
+                        ++start;
+                    }
+                }
+                if (wait_q) YIELD_FOR(start);
+                if (start >= len || start < 0) {  // iterator exhausted
                     P.n_intv[item] = raw_n;
                     P.n_calls[item] = calls_n;
                     phase = P_FETCH;
@@ -410,17 +488,20 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 continue;
             }
             if (phase == P_SMEM_BEGIN) {  // software/bwt.c:782-789
+                if (QBLK(x) != qb) YIELD_FOR(x);
                 mem_n = 0;
-                const int qx = qget(P.codes, o0, x, qv, qb);
+                const int qx = qsel(o0, x, qv);
                 if (qx > 3) {
                     ret = x + 1;
                     phase = P_SMEM_END;
                     continue;
                 }
                 if (min_intv < 1) min_intv = 1;
-                ik0 = P.L2[qx] + 1;
-                ik2 = P.L2[qx + 1] - P.L2[qx];
-                ik1 = P.L2[3 - qx] + 1;
+                const uint64_t lq = sel4(qx, P.L2[0], P.L2[1], P.L2[2], P.L2[3]);
+                const uint64_t lq1 = sel4(qx, P.L2[1], P.L2[2], P.L2[3], P.L2[4]);
+                ik0 = lq + 1;
+                ik2 = lq1 - lq;
+                ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
                 ikend = (uint32_t)(x + 1);
                 fwd_n = 0;
                 i = x + 1;
@@ -428,14 +509,17 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                 continue;
             }
             if (phase == P_FETCH) {
-                item = atomicAdd(P.head, 1);
+                // claiming the next read and loading its offsets happen in the
+                // uniform section; yield until both are done
+                if (nlen < 0) break;
+                item = nitem;
                 if (item >= P.n_items) {
                     phase = P_EXIT;
                     break;
                 }
-                const int rid = P.read_ids ? P.read_ids[item] : item;
-                o0 = P.offs[rid];
-                len = (int)(P.offs[rid + 1] - o0);
+                o0 = no0;
+                len = nlen;
+                nlen = -2;
                 raw_n = 0;
                 calls_n = 0;
                 start = 0;
@@ -444,22 +528,71 @@ __global__ __launch_bounds__(256, 4) void seed_kernel(SeedParams P) {
                     P.n_calls[item] = 0;
                     continue;
                 }
-                split_len = P.split_len_init < len ? P.split_len_init : len;  // software/bwamem.c:456-458
                 phase = P_NEXT2;
+                continue;
+            }
+            break;  // unreachable
+        }
+#undef YIELD_FOR
+#undef QBLK
+        // ---- uniform section: every lane takes part in the cooperative
+        // bucket fetch; the loads for the next iteration are issued here ----
+        const bool live = phase != P_EXIT;
+        const bool want = phase == P_BWD_RES || phase == P_FWD_RES;  // an extend request
+        uint64_t tb = 0;
+        if constexpr (STAMP) {
+            tb = stamp();
+            st_adv += tb - ta;
+            st_iter += 1;
+            st_active += __popcll(__ballot(want));
+        }
+        if (!__any(live)) break;
+        if (phase == P_FETCH) {
+            if (nlen == -2) {  // claim the next read
+                nitem = atomicAdd(P.head, 1);
+                nlen = -1;
+            } else if (nlen == -1) {  // its offsets (the claim returned last iteration)
+                next_offsets(P, nitem, no0, nlen);
             }
         }
-        // ---- one bwt_extend per live lane; the loop exit is wave-uniform so
-        // every lane takes part in the cooperative bucket fetch ----
-        const bool want = phase != P_EXIT;
-        if (!__any(want)) break;
+        // prev[j+1] and the query window land in LDS slots (no VGPR-destination
+        // load the compiler would wait on right away); read back after the wait
+        const bool ld_pn = phase == P_BWD_RES && (uint32_t)j + 1 < prev_n;
+        const bool ld_q = qwant != qb && qwant != ~0u;
+        if (ld_pn)
+            __builtin_amdgcn_global_load_lds(bp + prev_off + j + 1, (__attribute__((address_space(3))) void*)&W->pn[0],
+                                             16, 0, 0);
+        if (ld_q)
+            __builtin_amdgcn_global_load_lds(P.codes + qwant, (__attribute__((address_space(3))) void*)&W->q[0], 16, 0, 0);
         // the interval to extend: ik forward (a = x[1]), prev[j] backward (a = x[0])
         const bool fwd = phase == P_FWD_RES;
-        const uint64_t ra = fwd ? ik1 : p_x0(pc), rb = fwd ? ik0 : p_x1(pc), rs = fwd ? ik2 : p_x2(pc);
+        const uint64_t ra = fwd ? ik1 : ik0, rb = fwd ? ik0 : ik1, rs = ik2;
         const uint64_t k = ra - 1, l = k + rs;
         const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
         Bucket vk, vl;
-        fetch_buckets<COOP>(P.bwt, W, lane, want, kk, ll, vk, vl);
+        fetch_buckets<COOP, AUX>(P.bwt, W, lane, want, kk, ll, vk, vl);  // ends with vmcnt(0)
+        if (ld_pn) pn = W->pn[vlane()];
+        if (ld_q) {
+            qv = W->q[vlane()];
+            qb = qwant;
+        }
+        uint64_t tc = 0;
+        if constexpr (STAMP) {
+            tc = stamp();
+            st_fetch += tc - tb;
+        }
         if (want) extend_counts(P, ra, rb, rs, cur_c, kk, ll, vk, vl, na, nb, ns);
+        if constexpr (STAMP) {
+            asm volatile("" ::"v"(na), "v"(nb), "v"(ns));
+            st_comp += stamp() - tc;
+        }
+    }
+    if constexpr (STAMP) {
+        st_t1 = rtstamp();
+        if (lane == 0 && P.dbg_buf) {
+            uint64_t* o = P.dbg_buf + (lane_g >> 6) * 8;
+            o[0] = st_adv; o[1] = st_fetch; o[2] = st_comp; o[3] = st_iter; o[4] = st_active; o[5] = st_t0; o[6] = st_t1;
+        }
     }
 }
 
@@ -543,10 +676,14 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 
 // ------------------------------------------------------------ host launchers
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
-    if (variant == 1)
-        hipLaunchKernelGGL(smem::seed_kernel<false>, dim3(grid), dim3(block), 0, st, *P);
-    else
-        hipLaunchKernelGGL(smem::seed_kernel<true>, dim3(grid), dim3(block), 0, st, *P);
+    switch (variant) {
+        // 1: per-lane bucket loads; 3: cooperative fetch at 4 waves/SIMD without the fused
+        // fast paths (fits 128 VGPRs); 9: the default build with cycle stamps
+        case 1: hipLaunchKernelGGL((smem::seed_kernel<false, 0, false, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 3: hipLaunchKernelGGL((smem::seed_kernel<true, 0, false, 4, false>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<true, 0, true, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        default: hipLaunchKernelGGL((smem::seed_kernel<true, 0, false, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
+    }
     return hipGetLastError();
 }
 

@@ -13,7 +13,7 @@ from dataclasses import dataclass
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libsmemgpu.so")
+LIB_PATH = os.environ.get("SMEMGPU_LIB") or os.path.join(PKG_DIR, "lib", "libsmemgpu.so")  # override: A/B builds
 
 SMEM_OK = 0
 ERRORS = {-1: "SMEM_E_ARG", -2: "SMEM_E_NOMEM", -3: "SMEM_E_IO", -4: "SMEM_E_DEVICE",
@@ -25,7 +25,7 @@ EXPORTED = [
     "smem_gpu_device_count", "smem_gpu_init", "smem_gpu_shutdown", "smem_gpu_collect",
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
-    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_strerror",
+    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_batch_debug", "smem_strerror",
 ]
 
 
@@ -89,6 +89,8 @@ def load() -> C.CDLL:
     lib.smem_gpu_set_lanes_per_cu.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_set_intv_cap.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_set_kernel_variant.argtypes = [C.c_void_p, C.c_int]
+    if hasattr(lib, "smem_batch_debug"):  # absent from older A/B builds
+        lib.smem_batch_debug.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     lib.smem_strerror.argtypes = [C.c_int]
     lib.smem_strerror.restype = C.c_char_p
     _lib = lib
@@ -262,6 +264,13 @@ class Batch:
         s = BatchStats()
         _check(load().smem_batch_stats(self._h, C.byref(s)), "smem_batch_stats")
         return {k: getattr(s, k) for k, _ in BatchStats._fields_}
+
+    def debug_words(self, n_words: int) -> np.ndarray:
+        out = np.zeros(n_words, dtype=np.uint64)
+        rc = load().smem_batch_debug(self._h, out.ctypes.data, n_words)
+        if rc < 0:
+            _check(rc, "smem_batch_debug")
+        return out[:rc]
 
     def fetch(self) -> Results:
         lib = load()

@@ -87,7 +87,8 @@ int  smem_gpu_device_count(void);
 /* Upload the index to `device` and keep it resident in HBM.  Replaces the
  * FPGA index upload in bwa_idx_load_bwt (software/bwa.c:286-307) and the
  * AAL buffer setup (software/HelloALINLB.cpp:344-451).  The words are copied;
- * the caller's arrays may be freed afterwards. */
+ * the caller's arrays may be freed afterwards.  Limits: seq_len < 2^34 and
+ * an index below 4 GiB (both strands of ~8.5 Gbp); SMEM_E_ARG otherwise. */
 int  smem_gpu_init(smem_gpu_t **gpu, int device, const uint32_t *bwt, uint64_t bwt_size,
                    uint64_t primary, const uint64_t L2[5]);
 void smem_gpu_shutdown(smem_gpu_t *gpu);
@@ -136,9 +137,15 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
 /* per-read output capacity (intervals) of batches created afterwards;
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
-/* seeding-kernel variant: 2 (default) cooperative LDS-DMA Occ-bucket fetch,
- * 1 per-lane fetch; both bit-exact, kept for A/B measurement */
+/* seeding-kernel variant, all bit-exact, kept for A/B measurement:
+ * 2 (default) cooperative LDS-DMA Occ-bucket fetch, 3 waves/SIMD;
+ * 1 per-lane bucket loads; 3 cooperative at 4 waves/SIMD without the fused
+ * fast paths; 9 the default with per-wave cycle stamps (smem_batch_debug) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
+/* variant 9 (stamped diagnostic build): copy the per-wave cycle split
+ * {advance, fetch, compute, iterations, active lanes, t0, t1, 0} of the last
+ * run; returns the number of words copied or a negative code */
+int  smem_batch_debug(const smem_batch_t *b, uint64_t *out, uint64_t n_words);
 const char *smem_strerror(int code);
 
 #ifdef __cplusplus

@@ -13,9 +13,9 @@ PASSES=(
   "TCP_UTCL1_REQUEST TCP_UTCL1_TRANSLATION_MISS TCP_TCC_READ_REQ_LATENCY TD_TD_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES"
   "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU"
 )
-i=0
-for P in "${PASSES[@]}"; do
+SEL=${PMC_PASSES:-$(seq 0 $((${#PASSES[@]} - 1)))}  # e.g. PMC_PASSES="0 1 2"
+for i in $SEL; do
+  P=${PASSES[$i]}
   timeout -k 10 240 rocprofv3 --pmc $P --kernel-include-regex seed_kernel --output-format csv -d "$OUT" -o pass$i -- python tools/prof_run.py "$@" > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
-  i=$((i+1))
 done
 echo "all passes ok"
