@@ -146,6 +146,20 @@ def test_few_lanes_many_reads_per_lane(world, gpu_device):
         gpu.close()
 
 
+@pytest.mark.parametrize("variant", [1, 3, 9])
+def test_kernel_variants(world, gpu_device, variant):
+    """The A/B builds (per-lane fetch, 4 waves/SIMD, stamped) are bit-exact too."""
+    import smemgpu
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant)
+    try:
+        reads = _reads(world["genome"], "mixed", seed=11)
+        for opt in (OPTS["default"], OPTS["reseed"]):
+            want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4, **opt)
+            assert smemgpu.seed(gpu, reads.codes, reads.offs, smemgpu.Options(**opt)).to_smgo() == want
+    finally:
+        gpu.close()
+
+
 def test_batch_reuse(world):
     """One batch object, several runs with different reads (no stale state)."""
     from smemgpu import synth
