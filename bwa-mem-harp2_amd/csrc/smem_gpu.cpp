@@ -214,7 +214,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || variant < 0 || (variant > 3 && variant != 9)) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || variant == 2 || variant == 3 || variant == 9)) return SMEM_E_ARG;
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }
@@ -403,8 +403,8 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
     if (g->variant == 9) {
-        HIP_TRY(b->d_dbg.ensure((size_t)grid * 4 * 8));
-        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, (size_t)grid * 4 * 8 * sizeof(uint64_t), b->st));
+        HIP_TRY(b->d_dbg.ensure((size_t)grid * 4 * 32));
+        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, (size_t)grid * 4 * 32 * sizeof(uint64_t), b->st));
         P.dbg_buf = b->d_dbg.p;
     }
     if (n > 0) HIP_TRY(smem_launch_seed(&P, grid, 256, g->variant, b->st));

@@ -17,8 +17,8 @@
 //    (64-B bucket = 4 x u64 checkpoint + 8 x u32 of 2-bit symbols per 128
 //    BWT symbols, software/bwt.h:72-73); rank inside a bucket is computed
 //    with bit-plane popcounts (v_bcnt) instead of the 1 KB byte LUT;
-//  * Occ buckets are fetched cooperatively: every wave-instruction moves 16
-//    whole 64-B buckets (4 lanes x 16 B) into the wave's LDS image by LDS-DMA;
+//  * Occ buckets are fetched cooperatively by LDS-DMA: every wave-instruction
+//    moves 16 whole 64-B buckets (4 lanes x 16 B) into the wave's LDS image;
 //  * the forward / prev / curr lists live in a per-lane scratch arena as
 //    16-B packed entries, prev[j+1] prefetched while prev[j] is extended;
 //  * matches are appended to the read's output region as bwt_smem1 emits
@@ -34,11 +34,6 @@ namespace smem {
 struct Bucket {
     uint4 c01, c23, w03, w47;
 };
-
-__device__ __forceinline__ Bucket load_bucket(const uint32_t* __restrict__ bwt, uint64_t kk) {
-    const uint4* p = reinterpret_cast<const uint4*>(bwt + ((kk >> 7) << 4));
-    return Bucket{p[0], p[1], p[2], p[3]};
-}
 
 // Counts of C, G, T among the first pos+1 symbols of the bucket's 8 words
 // (MSB-first 2-bit symbols). A = pos+1 - C - G - T, which is what
@@ -114,20 +109,17 @@ enum Phase : int {
 
 constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
 
-// Wave-private LDS: the Occ bucket images [k|l][lane][4 x 16 B] and one
-// 16-B landing slot per lane for prev[j+1] and for the query window, all
-// filled by LDS-DMA (10 KB per wave, 40 KB per 256-thread block).
+// Wave-private LDS: the Occ bucket image (8 KB) and one 16-B landing slot per
+// lane for prev[j+1] and for the query window, all filled by LDS-DMA
+// (10 KB per wave, 40 KB per 256-thread block).  The bucket image is laid
+// out per fetch mode: FETCH_LANE as 8 planes [k0..k3, l0..l3][lane] of 16-B
+// chunks, FETCH_COOP as [k|l][lane][4 chunks].
 struct WaveLds {
-    uint4 k[64][4];
-    uint4 l[64][4];
+    uint4 img[8][64];
     uint4 pn[64];
     uint4 q[64];
 };
 
-// Fetch the 64-B Occ buckets of every live lane.  COOP: each wave-instruction
-// moves 16 whole buckets (4 lanes x 16 B per bucket, one L1 access each)
-// straight into the wave's LDS image with LDS-DMA; the owner lane then reads
-// its bucket from LDS.  !COOP: each lane loads its own bucket (4 x 16 B).
 // The lane id, recomputed where it is used: the register allocator would
 // otherwise keep it (and addresses derived from it) live across the whole
 // state machine, or spill them.
@@ -143,14 +135,47 @@ __device__ __forceinline__ const uint32_t* boff(const uint32_t* __restrict__ bwt
     return reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(bwt) + (b * 64u + chunk * 4u));
 }
 
-template <bool COOP, int AUX>
-__device__ __forceinline__ void fetch_buckets(const uint32_t* __restrict__ bwt, WaveLds* W, int lane, bool want,
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+enum FetchMode { FETCH_LANE = 0, FETCH_COOP = 1 };
+
+// Fetch the 64-B Occ buckets of k and l (l only when it is another bucket,
+// bwt_2occ4's same-bucket case) for every lane that has an extend request,
+// by LDS-DMA, and return them in registers.
+//  FETCH_COOP (default): each instruction moves 16 whole buckets (4 lanes x
+//    16 B, bucket indices exchanged by ds_bpermute).
+//  FETCH_LANE: every lane DMAs its own bucket, one 16-B chunk per
+//    instruction (8 instructions: 4 chunks x k, l), into chunk planes.
+//  On uniformly random buckets of a 1 GB table (tools/gather_ceiling.hip)
+//  FETCH_LANE reads 3.1x faster (43.6 vs 13.9 G buckets/s), but in the
+//  seeding kernel, whose accesses share upper FM-index levels, FETCH_COOP
+//  is 14 % faster (51.8 vs 60.5 ms per 1M reads, 1 Gbp): kept both for A/B.
+template <int FETCH>
+__device__ __forceinline__ void fetch_buckets(const uint32_t* __restrict__ bwt, WaveLds* W, bool want,
                                               uint64_t kk, uint64_t ll, Bucket& vk, Bucket& vl) {
     const bool needl = want && (kk >> 7) != (ll >> 7);
-    if constexpr (COOP) {
+    if constexpr (FETCH == FETCH_LANE) {
+        const uint32_t bk = (uint32_t)(kk >> 7), bl = (uint32_t)(ll >> 7);
+        if (want) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_global_load_lds(boff(bwt, bk, 4 * q), LDS_PTR(&W->img[q][0]), 16, 0, 0);
+        }
+        if (needl) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_global_load_lds(boff(bwt, bl, 4 * q), LDS_PTR(&W->img[4 + q][0]), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int lane = vlane();
+        vk = Bucket{W->img[0][lane], W->img[1][lane], W->img[2][lane], W->img[3][lane]};
+        const int o = needl ? 4 : 0;  // read the l planes only where they were fetched
+        vl = Bucket{W->img[o][lane], W->img[o + 1][lane], W->img[o + 2][lane], W->img[o + 3][lane]};
+    } else {
+        uint4(*img)[4] = reinterpret_cast<uint4(*)[4]>(&W->img[0][0]);  // [k 64 | l 64][4 chunks]
         const uint32_t bk = want ? (uint32_t)(kk >> 7) : NO_BUCKET;
         const uint32_t bl = needl ? (uint32_t)(ll >> 7) : NO_BUCKET;
-        lane = vlane();
+        const int lane = vlane();
         const uint32_t chunk = (uint32_t)(lane & 3) * 4;
         // all 8 source lookups first (one LDS wait), then the 8 DMAs
         uint32_t sk[4], sl[4];
@@ -162,23 +187,15 @@ __device__ __forceinline__ void fetch_buckets(const uint32_t* __restrict__ bwt, 
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if (sk[r] != NO_BUCKET)
-                __builtin_amdgcn_global_load_lds(boff(bwt, sk[r], chunk),
-                                                 (__attribute__((address_space(3))) void*)&W->k[16 * r][0], 16, 0, AUX);
+            if (sk[r] != NO_BUCKET) __builtin_amdgcn_global_load_lds(boff(bwt, sk[r], chunk), LDS_PTR(&img[16 * r][0]), 16, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (sl[r] != NO_BUCKET)
-                __builtin_amdgcn_global_load_lds(boff(bwt, sl[r], chunk),
-                                                 (__attribute__((address_space(3))) void*)&W->l[16 * r][0], 16, 0, AUX);
+                __builtin_amdgcn_global_load_lds(boff(bwt, sl[r], chunk), LDS_PTR(&img[64 + 16 * r][0]), 16, 0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        vk = Bucket{W->k[lane][0], W->k[lane][1], W->k[lane][2], W->k[lane][3]};
-        const int ls = needl ? 1 : 0;  // read the l image only where it was fetched
-        const uint4* src = ls ? &W->l[lane][0] : &W->k[lane][0];
+        vk = Bucket{img[lane][0], img[lane][1], img[lane][2], img[lane][3]};
+        const uint4* src = needl ? &img[64 + lane][0] : &img[lane][0];
         vl = Bucket{src[0], src[1], src[2], src[3]};
-    } else if (want) {
-        // per-lane: the l bucket is loaded again even when it equals k (an L1 hit)
-        vk = load_bucket(bwt, kk);
-        vl = load_bucket(bwt, needl ? ll : kk);
     }
 }
 
@@ -222,7 +239,6 @@ __device__ __forceinline__ void next_offsets(const SeedParams& P, int it, uint32
     len = (int)(b - a);
 }
 
-// AUX: cache-policy bits of the LDS-DMA loads (0 default, 2 nt, 16 sc1, 17 sc0|sc1)
 // chip-wide 100 MHz clock: wave start / end times comparable across XCDs
 __device__ __forceinline__ uint64_t rtstamp() {
     uint64_t t;
@@ -237,9 +253,13 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 // STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
-template <bool COOP, int AUX, bool STAMP, int WPE, bool FAST>
+template <int FETCH, bool STAMP, int WPE>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
+    __shared__ uint32_t scnt[STAMP ? 4 : 1][16];  // STAMP: per-wave block-execution counts
+    if constexpr (STAMP) {
+        if ((threadIdx.x & 63) < 16) scnt[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+    }
     const int lane = threadIdx.x & 63;
     WaveLds* W = &lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const uint64_t lane_g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -286,11 +306,185 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         uint64_t ta = 0;
         if constexpr (STAMP) ta = stamp();
         // ---- advance the state machine until the lane needs an extend ----
-        // one transition per pass (every block ends in continue/break: this
-        // keeps the register allocation at 4 waves/SIMD); blocks are ordered
-        // by frequency
+        // Blocks are laid out in the order the common transitions take, and a
+        // block hands over to a LATER block by setting `phase` and falling
+        // through: result -> next forward base, forward stop -> list reversal
+        // -> first backward step, end of a backward step -> next step all
+        // complete in one pass of the wave.  Going back to an earlier block
+        // (end of a bwt_smem1 call, next read) takes another pass.  A lane sets
+        // `out` when it has an extend request (or yields); the pass has a
+        // single exit at the bottom, which keeps the exec-mask bookkeeping of
+        // the structurized loop (and so the register count) small.
         while (phase != P_EXIT) {
-            if (phase == P_BWD_RES) {  // na = x[0], nb = x[1]
+            if constexpr (STAMP) {  // which blocks this pass of the wave executes
+                const uint64_t act = __ballot(1);
+                if (lane == __ffsll((unsigned long long)act) - 1) {
+                    scnt[threadIdx.x >> 6][15] += 1;
+                    for (int ph = 0; ph < P_EXIT; ++ph)
+                        if (__ballot(phase == ph)) scnt[threadIdx.x >> 6][ph] += 1;
+                }
+            }
+            bool out = false;
+            if (phase == P_SMEM_END) {
+                if (!middle) {  // software/bwamem.c:261-272
+                    start = ret;
+                    m_n = mem_n;
+                    // split_len = min(k * split_factor + .499, len) (software/bwamem.c:456-458)
+                    const int split_len = P.split_len_init < len ? P.split_len_init : len;
+                    if (m_n > 0 && split_len > 0 && (int)max_len >= split_len &&
+                        (uint64_t)max_x2 <= (uint64_t)(int64_t)P.split_width) {
+                        // re-seed from the middle of the longest SMEM (software/bwamem.c:272-278)
+                        x = (int)max_mid;
+                        min_intv = (int)(max_x2 + 1);
+                        middle = 1;
+                        phase = P_SMEM_BEGIN;
+                    }
+                }
+                if (phase == P_SMEM_END) {
+                    // log the list: matches (+ sub-matches) for the finalize pass
+                    if (calls_n >= P.cap_calls) {
+                        phase = P_OVF;
+                    } else {
+                        P.out_call[(uint64_t)item * P.cap_calls + calls_n++] =
+                            CallRec{m_n, middle ? mem_n : 0u, (uint32_t)ori_start, max_len};
+                        phase = P_NEXT2;
+                    }
+                }
+            }
+            if (phase == P_OVF) {  // the read does not fit: hand it to the overflow pass
+                P.n_intv[item] = SMEM_OVERFLOW;
+                P.n_calls[item] = 0;
+                const int slot = atomicAdd(P.ovf_count, 1);
+                P.ovf_items[slot] = item;
+                phase = P_FETCH;
+            }
+            if (phase == P_FETCH) {
+                // claiming the next read and loading its offsets happen in the
+                // uniform section; yield until both are done
+                if (nlen < 0) {
+                    out = true;
+                } else if (nitem >= P.n_items) {
+                    phase = P_EXIT;
+                    out = true;
+                } else {
+                    item = nitem;
+                    o0 = no0;
+                    len = nlen;
+                    nlen = -2;
+                    raw_n = 0;
+                    calls_n = 0;
+                    start = 0;
+                    if (len < P.min_seed_len) {  // mem_chain's guard (software/bwamem.c:600)
+                        P.n_intv[item] = 0;
+                        P.n_calls[item] = 0;
+                        out = true;  // stays in P_FETCH: the next claim is issued below
+                    } else {
+                        phase = P_NEXT2;
+                    }
+                }
+            }
+            if (phase == P_NEXT2) {  // software/bwamem.c:247-261
+                bool wait_q = false;
+                if (start < len && start >= 0) {
+                    for (;;) {  // skip ambiguous bases
+                        if (start >= len) break;
+                        if (QBLK(start) != qb) { wait_q = true; break; }
+                        if (qsel(o0, start, qv) <= 3) break;
+                        ++start;
+                    }
+                }
+                if (wait_q) {
+                    qwant = QBLK(start);
+                    out = true;
+                } else if (start >= len || start < 0) {  // iterator exhausted
+                    P.n_intv[item] = raw_n;
+                    P.n_calls[item] = calls_n;
+                    phase = P_FETCH;
+                } else {
+                    ori_start = start;
+                    x = ori_start;
+                    min_intv = P.start_width;
+                    middle = 0;
+                    max_len = 0;
+                    phase = P_SMEM_BEGIN;
+                }
+            }
+            if (phase == P_SMEM_BEGIN) {  // software/bwt.c:782-789
+                if (QBLK(x) != qb) {
+                    qwant = QBLK(x);
+                    out = true;
+                } else {
+                    mem_n = 0;
+                    const int qx = qsel(o0, x, qv);
+                    if (qx > 3) {
+                        ret = x + 1;
+                        phase = P_SMEM_END;
+                    } else {
+                        if (min_intv < 1) min_intv = 1;
+                        const uint64_t lq = sel4(qx, P.L2[0], P.L2[1], P.L2[2], P.L2[3]);
+                        const uint64_t lq1 = sel4(qx, P.L2[1], P.L2[2], P.L2[3], P.L2[4]);
+                        ik0 = lq + 1;
+                        ik2 = lq1 - lq;
+                        ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
+                        ikend = (uint32_t)(x + 1);
+                        fwd_n = 0;
+                        i = x + 1;
+                        phase = P_FWD;
+                    }
+                }
+            }
+            if (phase == P_FWD_RES) {  // software/bwt.c:795-799; na = x[1], nb = x[0]
+                bool stop = false;
+                if (ns != ik2) {
+                    *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = pack_p(ik0, ik1, ik2, ikend);
+                    ++fwd_n;
+                    stop = ns < (uint64_t)min_intv;
+                }
+                if (stop) {
+                    phase = P_FWD_DONE;
+                } else {
+                    ik0 = nb; ik1 = na; ik2 = ns;
+                    ikend = (uint32_t)(i + 1);
+                    ++i;
+                    phase = P_FWD;
+                }
+            }
+            if (phase == P_FWD) {  // software/bwt.c:791-803
+                bool push = true;
+                if (i < len) {
+                    if (QBLK(i) != qb) {
+                        qwant = QBLK(i);
+                        out = true;
+                        push = false;
+                    } else {
+                        const int qi = qsel(o0, i, qv);
+                        if (qi < 4) {
+                            cur_c = 3 - qi;
+                            if (i + 1 < len) qwant = QBLK(i + 1);
+                            phase = P_FWD_RES;  // -> extend (forward)
+                            out = true;
+                            push = false;
+                        }
+                    }
+                }
+                if (push) {  // ambiguous base, or end of query: push ik and stop
+                    *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = pack_p(ik0, ik1, ik2, ikend);
+                    ++fwd_n;
+                    phase = P_FWD_DONE;
+                }
+            }
+            if (phase == P_FWD_DONE) {  // software/bwt.c:805-808
+                // the last push becomes prev[0] after the reversal; it is always the
+                // current ik (the stop path pushes ik without advancing it)
+                pn = pack_p(ik0, ik1, ik2, ikend);
+                ret = (int)ikend;
+                prev_off = cap - fwd_n;  // pushed downward: ascending = reversed
+                prev_n = fwd_n;
+                curr_off = cap;
+                i = x - 1;
+                phase = P_BWD_STEP;
+            }
+            if (phase == P_BWD_RES) {  // software/bwt.c:815-825; na = x[0], nb = x[1]
                 if (ns < (uint64_t)min_intv) {
                     // only prev[0] can be kept, when nothing longer survived
                     if (curr_n == 0 && (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start)) {
@@ -315,223 +509,60 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     ++curr_n;
                     curr_last_x2 = ns;
                 }
-                ++j;
-                if (phase == P_OVF) continue;
-                if (FAST && (uint32_t)j < prev_n) {  // fast path: extend prev[j] right away (P_BWD_J, j > 0)
-                    ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
-                    break;
+                if (phase == P_BWD_RES) {
+                    ++j;
+                    if ((uint32_t)j < prev_n) {  // extend prev[j] (already in pn) right away
+                        ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
+                        out = true;
+                    } else if (curr_n == 0) {  // software/bwt.c:827
+                        phase = P_SMEM_END;
+                    } else {
+                        prev_off = curr_off;  // software/bwt.c:828: swap, next position
+                        prev_n = curr_n;
+                        pn = head;
+                        curr_off = curr_off == cap ? 0 : cap;
+                        --i;
+                        phase = P_BWD_STEP;
+                    }
                 }
-                phase = P_BWD_J;
-                continue;
             }
-            if (phase == P_BWD_J) {
-                if ((uint32_t)j < prev_n) {
-                    // prev[j] (loaded by the previous iteration) into the ik registers
-                    ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
-                    if (j == 0 && i > 0) qwant = QBLK(i - 1);  // next step's base
-                    phase = P_BWD_RES;
-                    break;  // -> extend (backward); prev[j+1] is fetched meanwhile
-                }
-                if (curr_n == 0) {
-                    phase = P_SMEM_END;  // software/bwt.c:827
+            if (phase == P_BWD_STEP) {  // software/bwt.c:810-812; prev[0] is in pn
+                if (i >= 0 && QBLK(i) != qb) {
+                    qwant = QBLK(i);
+                    out = true;
                 } else {
-                    prev_off = curr_off;
-                    prev_n = curr_n;
-                    pn = head;  // curr[0], kept in registers
-                    curr_off = curr_off == cap ? 0 : cap;
-                    --i;
-                    phase = P_BWD_STEP;
-                }
-                continue;
-            }
-            if (phase == P_FWD_RES) {  // na = x[1], nb = x[0]
-                bool stop = false;
-                if (ns != ik2) {
-                    *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = pack_p(ik0, ik1, ik2, ikend);
-                    ++fwd_n;
-                    stop = ns < (uint64_t)min_intv;
-                }
-                if (stop) {
-                    phase = P_FWD_DONE;
-                    continue;
-                }
-                ik0 = nb; ik1 = na; ik2 = ns;
-                ikend = (uint32_t)(i + 1);
-                ++i;
-                if (FAST && i < len && QBLK(i) == qb) {  // fast path: the next forward extend (P_FWD)
-                    const int qi = qsel(o0, i, qv);
-                    if (qi < 4) {
-                        cur_c = 3 - qi;
-                        if (i + 1 < len) qwant = QBLK(i + 1);
-                        break;
-                    }
-                }
-                phase = P_FWD;
-                continue;
-            }
-            if (phase == P_FWD) {
-                if (i < len) {
-                    if (QBLK(i) != qb) YIELD_FOR(i);
-                    const int qi = qsel(o0, i, qv);
-                    if (qi < 4) {
-                        cur_c = 3 - qi;
-                        if (i + 1 < len) qwant = QBLK(i + 1);
-                        phase = P_FWD_RES;
-                        break;  // -> extend (forward)
-                    }
-                }
-                // ambiguous base, or end of query: push ik and stop
-                *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = pack_p(ik0, ik1, ik2, ikend);
-                ++fwd_n;
-                phase = P_FWD_DONE;
-                continue;
-            }
-            if (phase == P_FWD_DONE) {
-                // the last push becomes prev[0] after the reversal; it is always the
-                // current ik (the stop path pushes ik without advancing it).  From
-                // here on ik holds the backward interval being extended (prev[j]).
-                pn = pack_p(ik0, ik1, ik2, ikend);
-                ret = (int)ikend;
-                prev_off = cap - fwd_n;  // pushed downward: ascending = reversed
-                prev_n = fwd_n;
-                curr_off = cap;
-                i = x - 1;
-                phase = P_BWD_STEP;
-                continue;
-            }
-            if (phase == P_BWD_STEP) {
-                if (i >= 0 && QBLK(i) != qb) YIELD_FOR(i);
-                cur_c = i < 0 ? -1 : qsel(o0, i, qv);
-                if (cur_c > 3) cur_c = -1;
-                curr_n = 0;
-                if (cur_c < 0) {
-                    // nothing extends: prev[0] (= pn) is the only candidate
-                    if (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start) {
-                        if (raw_n >= P.cap_intv) {
-                            phase = P_OVF;
-                        } else {
-                            const uint64_t info = (uint64_t)p_end(pn) | ((uint64_t)(i + 1) << 32);
-                            P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{p_x0(pn), p_x1(pn), p_x2(pn), info};
-                            ++mem_n;
-                            mem_last_start = (uint32_t)(i + 1);
-                            if (!middle && p_end(pn) - (uint32_t)(i + 1) >= max_len) {
-                                max_len = p_end(pn) - (uint32_t)(i + 1);
-                                max_x2 = p_x2(pn) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)p_x2(pn);
-                                max_mid = (p_end(pn) + (uint32_t)(i + 1)) >> 1;
+                    cur_c = i < 0 ? -1 : qsel(o0, i, qv);
+                    if (cur_c > 3) cur_c = -1;
+                    curr_n = 0;
+                    if (cur_c >= 0) {
+                        j = 0;
+                        ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
+                        if (i > 0) qwant = QBLK(i - 1);  // the next step's base
+                        phase = P_BWD_RES;  // -> extend prev[0]; prev[1] is fetched meanwhile
+                        out = true;
+                    } else {
+                        // nothing extends: prev[0] is the only candidate
+                        phase = P_SMEM_END;
+                        if (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start) {
+                            if (raw_n >= P.cap_intv) {
+                                phase = P_OVF;
+                            } else {
+                                const uint64_t info = (uint64_t)p_end(pn) | ((uint64_t)(i + 1) << 32);
+                                P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] =
+                                    Intv{p_x0(pn), p_x1(pn), p_x2(pn), info};
+                                ++mem_n;
+                                mem_last_start = (uint32_t)(i + 1);
+                                if (!middle && p_end(pn) - (uint32_t)(i + 1) >= max_len) {
+                                    max_len = p_end(pn) - (uint32_t)(i + 1);
+                                    max_x2 = p_x2(pn) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)p_x2(pn);
+                                    max_mid = (p_end(pn) + (uint32_t)(i + 1)) >> 1;
+                                }
                             }
                         }
                     }
-                    if (phase != P_OVF) phase = P_SMEM_END;
-                } else {
-                    j = 0;
-                    phase = P_BWD_J;
                 }
-                continue;
             }
-            if (phase == P_SMEM_END) {
-                if (!middle) {  // software/bwamem.c:261-272
-                    start = ret;
-                    m_n = mem_n;
-                    // split_len = min(k * split_factor + .499, len) (software/bwamem.c:456-458)
-                    const int split_len = P.split_len_init < len ? P.split_len_init : len;
-                    if (m_n > 0 && split_len > 0 && (int)max_len >= split_len &&
-                        (uint64_t)max_x2 <= (uint64_t)(int64_t)P.split_width) {
-                        // re-seed from the middle of the longest SMEM (software/bwamem.c:272-278)
-                        x = (int)max_mid;
-                        min_intv = (int)(max_x2 + 1);
-                        middle = 1;
-                        phase = P_SMEM_BEGIN;
-                        continue;
-                    }
-                }
-                // log the list: matches (+ sub-matches) for the finalize pass
-                if (calls_n >= P.cap_calls) {
-                    phase = P_OVF;
-                } else {
-                    P.out_call[(uint64_t)item * P.cap_calls + calls_n++] =
-                        CallRec{m_n, middle ? mem_n : 0u, (uint32_t)ori_start, max_len};
-                    phase = P_NEXT2;
-                }
-                continue;
-            }
-            if (phase == P_OVF) {  // the read does not fit: hand it to the overflow pass
-                P.n_intv[item] = SMEM_OVERFLOW;
-                P.n_calls[item] = 0;
-                const int slot = atomicAdd(P.ovf_count, 1);
-                P.ovf_items[slot] = item;
-                phase = P_FETCH;
-                continue;
-            }
-            if (phase == P_NEXT2) {  // software/bwamem.c:247-261
-                bool wait_q = false;
-                if (start < len && start >= 0) {
-                    for (;;) {  // skip ambiguous bases
-                        if (start >= len) break;
-                        if (QBLK(start) != qb) { wait_q = true; break; }
-                        if (qsel(o0, start, qv) <= 3) break;
-                        ++start;
-                    }
-                }
-                if (wait_q) YIELD_FOR(start);
-                if (start >= len || start < 0) {  // iterator exhausted
-                    P.n_intv[item] = raw_n;
-                    P.n_calls[item] = calls_n;
-                    phase = P_FETCH;
-                } else {
-                    ori_start = start;
-                    x = ori_start;
-                    min_intv = P.start_width;
-                    middle = 0;
-                    max_len = 0;
-                    phase = P_SMEM_BEGIN;
-                }
-                continue;
-            }
-            if (phase == P_SMEM_BEGIN) {  // software/bwt.c:782-789
-                if (QBLK(x) != qb) YIELD_FOR(x);
-                mem_n = 0;
-                const int qx = qsel(o0, x, qv);
-                if (qx > 3) {
-                    ret = x + 1;
-                    phase = P_SMEM_END;
-                    continue;
-                }
-                if (min_intv < 1) min_intv = 1;
-                const uint64_t lq = sel4(qx, P.L2[0], P.L2[1], P.L2[2], P.L2[3]);
-                const uint64_t lq1 = sel4(qx, P.L2[1], P.L2[2], P.L2[3], P.L2[4]);
-                ik0 = lq + 1;
-                ik2 = lq1 - lq;
-                ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
-                ikend = (uint32_t)(x + 1);
-                fwd_n = 0;
-                i = x + 1;
-                phase = P_FWD;
-                continue;
-            }
-            if (phase == P_FETCH) {
-                // claiming the next read and loading its offsets happen in the
-                // uniform section; yield until both are done
-                if (nlen < 0) break;
-                item = nitem;
-                if (item >= P.n_items) {
-                    phase = P_EXIT;
-                    break;
-                }
-                o0 = no0;
-                len = nlen;
-                nlen = -2;
-                raw_n = 0;
-                calls_n = 0;
-                start = 0;
-                if (len < P.min_seed_len) {  // mem_chain's guard (software/bwamem.c:600)
-                    P.n_intv[item] = 0;
-                    P.n_calls[item] = 0;
-                    continue;
-                }
-                phase = P_NEXT2;
-                continue;
-            }
-            break;  // unreachable
+            if (out) break;
         }
 #undef YIELD_FOR
 #undef QBLK
@@ -560,17 +591,17 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         const bool ld_pn = phase == P_BWD_RES && (uint32_t)j + 1 < prev_n;
         const bool ld_q = qwant != qb && qwant != ~0u;
         if (ld_pn)
-            __builtin_amdgcn_global_load_lds(bp + prev_off + j + 1, (__attribute__((address_space(3))) void*)&W->pn[0],
+            __builtin_amdgcn_global_load_lds(bp + prev_off + j + 1, LDS_PTR(&W->pn[0]),
                                              16, 0, 0);
         if (ld_q)
-            __builtin_amdgcn_global_load_lds(P.codes + qwant, (__attribute__((address_space(3))) void*)&W->q[0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&W->q[0]), 16, 0, 0);
         // the interval to extend: ik forward (a = x[1]), prev[j] backward (a = x[0])
         const bool fwd = phase == P_FWD_RES;
         const uint64_t ra = fwd ? ik1 : ik0, rb = fwd ? ik0 : ik1, rs = ik2;
         const uint64_t k = ra - 1, l = k + rs;
         const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
         Bucket vk, vl;
-        fetch_buckets<COOP, AUX>(P.bwt, W, lane, want, kk, ll, vk, vl);  // ends with vmcnt(0)
+        fetch_buckets<FETCH>(P.bwt, W, want, kk, ll, vk, vl);  // ends with vmcnt(0)
         if (ld_pn) pn = W->pn[vlane()];
         if (ld_q) {
             qv = W->q[vlane()];
@@ -590,8 +621,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     if constexpr (STAMP) {
         st_t1 = rtstamp();
         if (lane == 0 && P.dbg_buf) {
-            uint64_t* o = P.dbg_buf + (lane_g >> 6) * 8;
+            uint64_t* o = P.dbg_buf + (lane_g >> 6) * 32;
             o[0] = st_adv; o[1] = st_fetch; o[2] = st_comp; o[3] = st_iter; o[4] = st_active; o[5] = st_t0; o[6] = st_t1;
+            for (int k = 0; k < 16; ++k) o[8 + k] = scnt[threadIdx.x >> 6][k];
         }
     }
 }
@@ -677,12 +709,10 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // ------------------------------------------------------------ host launchers
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
     switch (variant) {
-        // 1: per-lane bucket loads; 3: cooperative fetch at 4 waves/SIMD without the fused
-        // fast paths (fits 128 VGPRs); 9: the default build with cycle stamps
-        case 1: hipLaunchKernelGGL((smem::seed_kernel<false, 0, false, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 3: hipLaunchKernelGGL((smem::seed_kernel<true, 0, false, 4, false>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<true, 0, true, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        default: hipLaunchKernelGGL((smem::seed_kernel<true, 0, false, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 3: per-lane bucket fetch (A/B); 9: the default with cycle stamps
+        case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, true, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }

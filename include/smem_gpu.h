@@ -138,9 +138,9 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement:
- * 2 (default) cooperative LDS-DMA Occ-bucket fetch, 3 waves/SIMD;
- * 1 per-lane bucket loads; 3 cooperative at 4 waves/SIMD without the fused
- * fast paths; 9 the default with per-wave cycle stamps (smem_batch_debug) */
+ * 2 (default, also 0) cooperative LDS-DMA Occ-bucket fetch (16 buckets per
+ * wave-instruction); 3 per-lane LDS-DMA fetch; 9 the default with per-wave
+ * cycle stamps (smem_batch_debug) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
 /* variant 9 (stamped diagnostic build): copy the per-wave cycle split
  * {advance, fetch, compute, iterations, active lanes, t0, t1, 0} of the last

@@ -23,6 +23,7 @@ def main():
     p.add_argument("--sub", type=float, default=0.02)
     p.add_argument("--lanes-per-cu", type=int, default=0)
     p.add_argument("--launches", type=int, default=1)
+    p.add_argument("--variant", type=int, default=0)
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
     a = p.parse_args()
     import smemgpu
@@ -35,7 +36,7 @@ def main():
         smemgpu.Index.build_gpu(g.codes).write(key)
     idx = smemgpu.Index.read(key)
     reads = synth.make_reads(g.codes, a.reads, a.read_len, seed=1000 + a.seed * 7919, sub_rate=a.sub, n_rate=0.001)
-    gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu)
+    gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu, variant=a.variant)
     b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
     b.set_reads(reads.codes, reads.offs)
     for _ in range(a.launches):

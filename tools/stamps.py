@@ -13,6 +13,10 @@ sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
 sys.path.insert(0, ROOT)
 
 
+PHASES = ["BWD_RES", "BWD_J", "FWD_RES", "FWD", "FWD_DONE", "BWD_STEP", "SMEM_END", "OVF", "NEXT2", "SMEM_BEGIN",
+          "FETCH"]
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--genome-mbp", type=float, default=1000)
@@ -40,7 +44,7 @@ def main():
         st = b.stats()
         print(f"variant {variant}: kernel {st['kernel_ms']:.2f} ms", flush=True)
         if variant == 9:
-            w = b.debug_words(st["grid"] * 4 * 8).reshape(-1, 8).astype(np.float64)
+            w = b.debug_words(st["grid"] * 4 * 32).reshape(-1, 32).astype(np.float64)
             adv, fet, comp, it, act, t0, t1 = (w[:, k] for k in range(7))
             tot = adv.sum() + fet.sum() + comp.sum()
             out = {
@@ -55,6 +59,8 @@ def main():
                 "wave_end_ms_p10_p50_p90_max": [float(np.percentile(t1 - t0.min(), q) * 1e-5) for q in (10, 50, 90, 100)],
                 "waves_alive_at_ms": {f"{m:g}": int(((t1 - t0.min()) * 1e-5 > m).sum())
                                       for m in np.linspace(0, float((t1 - t0.min()).max() * 1e-5), 11)},
+                "passes_per_iter": float(w[:, 23].sum() / it.sum()),
+                "block_execs_per_iter": {n: round(float(w[:, 8 + k].sum() / it.sum()), 3) for k, n in enumerate(PHASES)},
                 "share_adv_fetch_comp": [float(adv.sum() / tot), float(fet.sum() / tot), float(comp.sum() / tot)],
             }
             print(json.dumps(out, indent=1), flush=True)
