@@ -92,10 +92,11 @@ struct HostBuf {
 struct smem_gpu {
     int device = 0;
     int n_cu = 0;
-    int lanes_per_cu = 768;  // 3 blocks of 256 per CU: the default kernel runs 3 waves/SIMD
+    int lanes_per_cu = 512;  // 2 blocks of 256 per CU (fastest of 512/768/1024 for the Occ64 kernel)
     int intv_cap = 0;
     int variant = 2;  // see smem_gpu_set_kernel_variant
-    uint32_t* d_bwt = nullptr;
+    uint32_t* d_bwt = nullptr;      // reference layout (variants 3, 4)
+    uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
     std::mutex mu;
     std::unordered_map<std::thread::id, smem_batch_t*> per_thread;
@@ -203,18 +204,30 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
     e = hipMemcpy(g->d_bwt, bwt, bwt_size * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(g->d_bwt + bwt_size, 0, 16 * sizeof(uint32_t));
     if (e != hipSuccess) { (void)hipFree(g->d_bwt); delete g; return fail(SMEM_E_DEVICE, "smem_gpu_init: upload", e); }
+    // the Occ64 re-layout of the same index, built on the device
+    const uint64_t n_ref = (bwt_size + 15) / 16;
+    e = hipMalloc(&g->d_occ64, (n_ref * 16 + 16) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(g->d_occ64 + n_ref * 16, 0, 16 * sizeof(uint32_t));
+    if (e == hipSuccess) e = smem_launch_occ64(g->d_bwt, n_ref, g->d_occ64, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(g->d_bwt);
+        if (g->d_occ64) (void)hipFree(g->d_occ64);
+        delete g;
+        return fail(SMEM_E_DEVICE, "smem_gpu_init: Occ64 layout", e);
+    }
     *out = g;
     return SMEM_OK;
 }
 
 int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
     if (!g) return SMEM_E_ARG;
-    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 768;
+    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 512;
     return SMEM_OK;
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || variant == 2 || variant == 3 || variant == 9)) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || variant == 2 || variant == 3 || variant == 4 || variant == 9)) return SMEM_E_ARG;
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }
@@ -249,6 +262,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
     g->per_thread.clear();
     if (g->d_bwt) (void)hipFree(g->d_bwt);
+    if (g->d_occ64) (void)hipFree(g->d_occ64);
     delete g;
 }
 
@@ -359,6 +373,7 @@ int smem_batch_set_reads_packed(smem_batch_t* b, int n_reads, const uint8_t* cod
 static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& P) {
     std::memset(&P, 0, sizeof(P));
     P.bwt = b->g->d_bwt;
+    P.occ64 = b->g->d_occ64;
     P.primary = b->g->primary;
     std::memcpy(P.L2, b->g->L2, sizeof(P.L2));
     P.codes = b->d_codes.p;

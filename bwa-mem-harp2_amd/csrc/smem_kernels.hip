@@ -137,7 +137,7 @@ __device__ __forceinline__ const uint32_t* boff(const uint32_t* __restrict__ bwt
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-enum FetchMode { FETCH_LANE = 0, FETCH_COOP = 1 };
+enum FetchMode { FETCH_LANE = 0, FETCH_COOP = 1, FETCH_OCC64 = 2 };
 
 // Fetch the 64-B Occ buckets of k and l (l only when it is another bucket,
 // bwt_2occ4's same-bucket case) for every lane that has an extend request,
@@ -227,6 +227,98 @@ __device__ __forceinline__ void extend_counts(const SeedParams& P, uint64_t a, u
     nb = b + (uint64_t)(a <= P.primary && a + s - 1 >= P.primary) + gt;
 }
 
+// ---- Occ64: the index re-laid for the GPU as one 32-B bucket per 64 BWT
+// symbols (same 0.5 B/symbol as the reference's 64 B per 128).  Words 0-2:
+// Occ(C), Occ(G), Occ(T) before the bucket, low 32 bits; word 3: their bits
+// 32-33 (C | G << 2 | T << 4); words 4-7: the 64 symbols, 16 per word,
+// MSB-first as in the reference (software/bwt.h:71-78).  Occ(A) is implied:
+// the $ row is not in the BWT, so A + C + G + T = position.  A rank then reads
+// one 32-B bucket and popcounts at most 4 words.
+struct Bucket32 {
+    uint4 cnt, sym;
+};
+
+__device__ __forceinline__ uint64_t occ_cgt(const uint4& c, int i) {
+    const uint32_t lo = i == 0 ? c.x : (i == 1 ? c.y : c.z);
+    return (uint64_t)((c.w >> (2 * i)) & 3) << 32 | lo;
+}
+
+// C, G, T among the first pos+1 (pos < 64) symbols of the bucket
+__device__ __forceinline__ void count_cgt4(const uint4& v, uint32_t pos, uint32_t& C, uint32_t& G, uint32_t& T) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t nfull = pos >> 4;
+    const uint32_t tail = ~((1u << ((15u - (pos & 15u)) << 1)) - 1u);
+    uint32_t sT = 0, sLo = 0, sHi = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t m = i < nfull ? 0xFFFFFFFFu : (i == nfull ? tail : 0u);
+        const uint32_t x = w[i] & m;
+        const uint32_t lo = x & 0x55555555u;
+        const uint32_t hi = (x >> 1) & 0x55555555u;
+        sT += __popc(lo & hi);
+        sLo += __popc(lo);
+        sHi += __popc(hi);
+    }
+    T = sT;
+    C = sLo - sT;
+    G = sHi - sT;
+}
+
+// bwt_extend for the child c only (as extend_counts) on Occ64 buckets
+__device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a, uint64_t b, uint64_t s, int c,
+                                                uint64_t kk, uint64_t ll, const Bucket32& vk, const Bucket32& vl,
+                                                uint64_t& na, uint64_t& nb, uint64_t& ns) {
+    uint32_t Ck, Gk, Tk, Cl, Gl, Tl;
+    count_cgt4(vk.sym, (uint32_t)(kk & 63), Ck, Gk, Tk);
+    count_cgt4(vl.sym, (uint32_t)(ll & 63), Cl, Gl, Tl);
+    const uint64_t tk1 = occ_cgt(vk.cnt, 0) + Ck, tk2 = occ_cgt(vk.cnt, 1) + Gk, tk3 = occ_cgt(vk.cnt, 2) + Tk;
+    const uint64_t tl1 = occ_cgt(vl.cnt, 0) + Cl, tl2 = occ_cgt(vl.cnt, 1) + Gl, tl3 = occ_cgt(vl.cnt, 2) + Tl;
+    const uint64_t tk0 = kk + 1 - tk1 - tk2 - tk3, tl0 = ll + 1 - tl1 - tl2 - tl3;
+    const uint64_t d0 = tl0 - tk0, d1 = tl1 - tk1, d2 = tl2 - tk2, d3 = tl3 - tk3;
+    const uint64_t L2c = sel4(c, P.L2[0], P.L2[1], P.L2[2], P.L2[3]);
+    na = L2c + 1 + sel4(c, tk0, tk1, tk2, tk3);
+    ns = sel4(c, d0, d1, d2, d3);
+    const uint64_t gt = (c < 1 ? d1 : 0) + (c < 2 ? d2 : 0) + (c < 3 ? d3 : 0);
+    nb = b + (uint64_t)(a <= P.primary && a + s - 1 >= P.primary) + gt;
+}
+
+// Fetch the Occ64 buckets of k and l.  Each lane keeps the two buckets it
+// fetched last in two LDS slots (planes [2*slot + chunk][lane]) with their
+// indices in t0 / t1: consecutive extends of one lane often need the same
+// bucket again (nested intervals of one backward step: 30 % of the buckets
+// on the bench workload), and those are not fetched again.  Every lane DMAs
+// its own buckets, one 16-B chunk per instruction (at most 4 instructions).
+__device__ __forceinline__ void fetch_occ64(const uint32_t* __restrict__ occ, WaveLds* W, bool want, uint64_t kk,
+                                            uint64_t ll, uint32_t& t0, uint32_t& t1, Bucket32& vk, Bucket32& vl) {
+    const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
+    const bool needl = want && bk != bl;
+    int ks = bk == t0 ? 0 : (bk == t1 ? 1 : -1);
+    int ls = !needl ? ks : (bl == t0 ? 0 : (bl == t1 ? 1 : -1));
+    const bool kmiss = want && ks < 0, lmiss = needl && ls < 0;
+    if (kmiss) ks = (needl && ls == 0) ? 1 : 0;  // keep the slot l hits
+    if (!needl) ls = ks;
+    else if (lmiss) ls = ks ^ 1;
+    const bool f0 = (kmiss && ks == 0) || (lmiss && ls == 0);
+    const bool f1 = (kmiss && ks == 1) || (lmiss && ls == 1);
+    const uint32_t b0 = (kmiss && ks == 0) ? bk : bl, b1 = (kmiss && ks == 1) ? bk : bl;
+    if (f0) {
+        __builtin_amdgcn_global_load_lds(boff(occ, b0 >> 1, (b0 & 1) * 8), LDS_PTR(&W->img[0][0]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(boff(occ, b0 >> 1, (b0 & 1) * 8 + 4), LDS_PTR(&W->img[1][0]), 16, 0, 0);
+        t0 = b0;
+    }
+    if (f1) {
+        __builtin_amdgcn_global_load_lds(boff(occ, b1 >> 1, (b1 & 1) * 8), LDS_PTR(&W->img[2][0]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(boff(occ, b1 >> 1, (b1 & 1) * 8 + 4), LDS_PTR(&W->img[3][0]), 16, 0, 0);
+        t1 = b1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int lane = vlane();
+    ks = ks < 0 ? 0 : ks;  // lanes without a request read a slot and ignore it
+    ls = ls < 0 ? 0 : ls;
+    vk = Bucket32{W->img[2 * ks][lane], W->img[2 * ks + 1][lane]};
+    vl = Bucket32{W->img[2 * ls][lane], W->img[2 * ls + 1][lane]};
+}
+
 // offsets of work item `it` (read_ids maps overflow-pass items to reads)
 __device__ __forceinline__ void next_offsets(const SeedParams& P, int it, uint32_t& o0, int& len) {
     if (it >= P.n_items) {
@@ -292,6 +384,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     uint32_t max_len = 0, max_x2 = 0, max_mid = 0;  // x2 saturated to 32 bits
     uint4 pn = {0, 0, 0, 0}, head = {0, 0, 0, 0};  // prev[j+1] in flight, curr[0]
     uint64_t na = 0, nb = 0, ns = 0;
+    uint32_t tag0 = ~0u, tag1 = ~0u;  // FETCH_OCC64: buckets held in the lane's two LDS slots
     uint64_t st_adv = 0, st_fetch = 0, st_comp = 0, st_iter = 0, st_active = 0, st_t0 = 0, st_t1 = 0;
     if constexpr (STAMP) st_t0 = rtstamp();
 
@@ -601,7 +694,11 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         const uint64_t k = ra - 1, l = k + rs;
         const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
         Bucket vk, vl;
-        fetch_buckets<FETCH>(P.bwt, W, want, kk, ll, vk, vl);  // ends with vmcnt(0)
+        Bucket32 wk, wl;
+        if constexpr (FETCH == FETCH_OCC64)
+            fetch_occ64(P.occ64, W, want, kk, ll, tag0, tag1, wk, wl);  // ends with vmcnt(0)
+        else
+            fetch_buckets<FETCH>(P.bwt, W, want, kk, ll, vk, vl);  // ends with vmcnt(0)
         if (ld_pn) pn = W->pn[vlane()];
         if (ld_q) {
             qv = W->q[vlane()];
@@ -612,7 +709,12 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             tc = stamp();
             st_fetch += tc - tb;
         }
-        if (want) extend_counts(P, ra, rb, rs, cur_c, kk, ll, vk, vl, na, nb, ns);
+        if (want) {
+            if constexpr (FETCH == FETCH_OCC64)
+                extend_counts64(P, ra, rb, rs, cur_c, kk, ll, wk, wl, na, nb, ns);
+            else
+                extend_counts(P, ra, rb, rs, cur_c, kk, ll, vk, vl, na, nb, ns);
+        }
         if constexpr (STAMP) {
             asm volatile("" ::"v"(na), "v"(nb), "v"(ns));
             st_comp += stamp() - tc;
@@ -709,10 +811,12 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // ------------------------------------------------------------ host launchers
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
     switch (variant) {
-        // 3: per-lane bucket fetch (A/B); 9: the default with cycle stamps
-        case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, true, 3>), dim3(grid), dim3(block), 0, st, *P); break;
-        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 3: reference-layout buckets, cooperative fetch; 4: reference layout,
+        // per-lane fetch; 9: the default with cycle stamps
+        case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 4: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }
@@ -750,4 +854,38 @@ extern "C" hipError_t smem_launch_offsets(const uint64_t* in, uint64_t* out, int
     hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
     if (e != hipSuccess || n <= 0) return e;
     return hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, in, out + 1, n, st);
+}
+
+namespace smem {
+// reference interleaved buckets (software/bwtindex.c:128-150: 4 x u64 Occ +
+// 8 x u32 symbols per 128) -> Occ64 (see Bucket32); one thread per 64 symbols
+__global__ __launch_bounds__(256) void occ64_kernel(const uint32_t* __restrict__ bwt, uint64_t n_ref,
+                                                     uint32_t* __restrict__ out) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= 2 * n_ref) return;
+    const uint32_t* r = bwt + (b >> 1) * 16;
+    uint64_t c1 = (uint64_t)r[3] << 32 | r[2], c2 = (uint64_t)r[5] << 32 | r[4], c3 = (uint64_t)r[7] << 32 | r[6];
+    const uint32_t* sw = r + 8 + (b & 1) * 4;
+    if (b & 1) {  // add the first 64 symbols of the 128-block
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t lo = r[8 + i] & 0x55555555u, hi = (r[8 + i] >> 1) & 0x55555555u;
+            const uint32_t t = __popc(lo & hi);
+            c1 += __popc(lo) - t;
+            c2 += __popc(hi) - t;
+            c3 += t;
+        }
+    }
+    uint4* o = reinterpret_cast<uint4*>(out + b * 8);
+    o[0] = make_uint4((uint32_t)c1, (uint32_t)c2, (uint32_t)c3,
+                      (uint32_t)(c1 >> 32) | (uint32_t)(c2 >> 32) << 2 | (uint32_t)(c3 >> 32) << 4);
+    o[1] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+}
+}  // namespace smem
+
+extern "C" hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32_t* out, hipStream_t st) {
+    const uint64_t n = 2 * n_ref_buckets;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::occ64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, bwt, n_ref_buckets, out);
+    return hipGetLastError();
 }

@@ -138,9 +138,11 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement:
- * 2 (default, also 0) cooperative LDS-DMA Occ-bucket fetch (16 buckets per
- * wave-instruction); 3 per-lane LDS-DMA fetch; 9 the default with per-wave
- * cycle stamps (smem_batch_debug) */
+ * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
+ * device at init) with per-lane LDS-DMA fetch and bucket reuse;
+ * 3 reference-layout buckets, cooperative fetch (16 per wave-instruction);
+ * 4 reference layout, per-lane fetch; 9 the default with per-wave cycle
+ * stamps (smem_batch_debug) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
 /* variant 9 (stamped diagnostic build): copy the per-wave cycle split
  * {advance, fetch, compute, iterations, active lanes, t0, t1, 0} of the last

@@ -146,9 +146,9 @@ def test_few_lanes_many_reads_per_lane(world, gpu_device):
         gpu.close()
 
 
-@pytest.mark.parametrize("variant", [3, 9])
+@pytest.mark.parametrize("variant", [3, 4, 9])
 def test_kernel_variants(world, gpu_device, variant):
-    """The A/B builds (per-lane fetch, stamped) are bit-exact too."""
+    """The A/B builds (reference-layout fetches, stamped) are bit-exact too."""
     import smemgpu
     gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant)
     try:
