@@ -92,7 +92,7 @@ struct HostBuf {
 struct smem_gpu {
     int device = 0;
     int n_cu = 0;
-    int lanes_per_cu = 512;  // 2 blocks of 256 per CU (fastest of 512/768/1024 for the Occ64 kernel)
+    int lanes_per_cu = 768;  // 3 blocks of 256 per CU: what the default kernel's LDS allows
     int intv_cap = 0;
     int variant = 2;  // see smem_gpu_set_kernel_variant
     uint32_t* d_bwt = nullptr;      // reference layout (variants 3, 4)
@@ -222,12 +222,12 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
 
 int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
     if (!g) return SMEM_E_ARG;
-    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 512;
+    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 768;
     return SMEM_OK;
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || variant == 2 || variant == 3 || variant == 4 || variant == 9)) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 6) || variant == 9)) return SMEM_E_ARG;
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }

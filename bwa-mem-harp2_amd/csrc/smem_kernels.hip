@@ -108,16 +108,26 @@ enum Phase : int {
 };
 
 constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
+// backward-list entries per lane kept in LDS.  On the bench workload 86 % of
+// curr pushes and 80 % of prev reads fall below 7 (99 % below 12); 7 entries
+// keep the wave at 13 KB of LDS, so 3 blocks of 4 waves fit a CU, which
+// measured faster than 12 entries at 2 blocks (39.5 vs 42.1 ms per 1M reads).
+// The forward list itself stays in global memory.
+constexpr int LIST_LDS = 7;
 
-// Wave-private LDS: the Occ bucket image (8 KB) and one 16-B landing slot per
-// lane for prev[j+1] and for the query window, all filled by LDS-DMA
-// (10 KB per wave, 40 KB per 256-thread block).  The bucket image is laid
-// out per fetch mode: FETCH_LANE as 8 planes [k0..k3, l0..l3][lane] of 16-B
-// chunks, FETCH_COOP as [k|l][lane][4 chunks].
-struct WaveLds {
-    uint4 img[8][64];
+// Wave-private LDS.  img: the Occ bucket image (FETCH_OCC64: 4 planes
+// [slot*2 + chunk][lane]; FETCH_LANE: 8 planes [k0..k3, l0..l3][lane];
+// FETCH_COOP: [k|l][lane][4 chunks]).  pn / q: one 16-B landing slot per lane
+// for prev[j+1] and for the query window, filled by LDS-DMA.  list: the
+// first NLIST entries of the lane's backward interval list (curr, which
+// becomes prev), entry-major so that a wave's accesses are bank-conflict
+// free whatever entry each lane is at.
+template <int NIMG, int NLIST>
+struct WaveLdsT {
+    uint4 img[NIMG][64];
     uint4 pn[64];
     uint4 q[64];
+    uint4 list[NLIST > 0 ? NLIST : 1][64];
 };
 
 // The lane id, recomputed where it is used: the register allocator would
@@ -150,8 +160,8 @@ enum FetchMode { FETCH_LANE = 0, FETCH_COOP = 1, FETCH_OCC64 = 2 };
 //  FETCH_LANE reads 3.1x faster (43.6 vs 13.9 G buckets/s), but in the
 //  seeding kernel, whose accesses share upper FM-index levels, FETCH_COOP
 //  is 14 % faster (51.8 vs 60.5 ms per 1M reads, 1 Gbp): kept both for A/B.
-template <int FETCH>
-__device__ __forceinline__ void fetch_buckets(const uint32_t* __restrict__ bwt, WaveLds* W, bool want,
+template <int FETCH, class WL>
+__device__ __forceinline__ void fetch_buckets(const uint32_t* __restrict__ bwt, WL* W, bool want,
                                               uint64_t kk, uint64_t ll, Bucket& vk, Bucket& vl) {
     const bool needl = want && (kk >> 7) != (ll >> 7);
     if constexpr (FETCH == FETCH_LANE) {
@@ -288,7 +298,8 @@ __device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a,
 // bucket again (nested intervals of one backward step: 30 % of the buckets
 // on the bench workload), and those are not fetched again.  Every lane DMAs
 // its own buckets, one 16-B chunk per instruction (at most 4 instructions).
-__device__ __forceinline__ void fetch_occ64(const uint32_t* __restrict__ occ, WaveLds* W, bool want, uint64_t kk,
+template <class WL>
+__device__ __forceinline__ void fetch_occ64(const uint32_t* __restrict__ occ, WL* W, bool want, uint64_t kk,
                                             uint64_t ll, uint32_t& t0, uint32_t& t1, Bucket32& vk, Bucket32& vl) {
     const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
     const bool needl = want && bk != bl;
@@ -345,8 +356,11 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 // STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
-template <int FETCH, bool STAMP, int WPE>
+template <int FETCH, bool STAMP, int WPE, int NLIST>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
+    // backward lists: the first NLIST entries live in LDS
+    constexpr int NL = NLIST;
+    using WaveLds = WaveLdsT<FETCH == FETCH_OCC64 ? 4 : 8, NL>;
     __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
     __shared__ uint32_t scnt[STAMP ? 4 : 1][16];  // STAMP: per-wave block-execution counts
     if constexpr (STAMP) {
@@ -375,7 +389,12 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     int x = 0, min_intv = 1, middle = 0, i = 0, j = 0, ret = 0, cur_c = 0;
     uint64_t ik0 = 0, ik1 = 0, ik2 = 0;
     uint32_t ikend = 0;
-    uint32_t fwd_n = 0, prev_off = 0, prev_n = 0, curr_off = 0, curr_n = 0;
+    // per-lane arena: [0, cap) the forward list (pushed downward, so ascending
+    // order is the reversed list bwt_smem1 iterates), [cap, 2 cap) the backward
+    // list beyond its first NL entries (which live in LDS).  curr is written in
+    // place over prev: curr[k] is pushed after prev[j >= k] has been read.
+    uint32_t fwd_n = 0, prev_off = 0, prev_n = 0, curr_n = 0;
+    bool prev_lds = false;  // prev is the backward list (LDS + region 2), not the forward list
     uint32_t mem_n = 0, mem_last_start = 0, m_n = 0;
     uint64_t curr_last_x2 = 0;
     // longest match of the first bwt_smem1 (software/bwamem.c:266-270), tracked
@@ -573,7 +592,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 ret = (int)ikend;
                 prev_off = cap - fwd_n;  // pushed downward: ascending = reversed
                 prev_n = fwd_n;
-                curr_off = cap;
+                prev_lds = false;
                 i = x - 1;
                 phase = P_BWD_STEP;
             }
@@ -597,23 +616,26 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     }
                 } else if (curr_n == 0 || ns != curr_last_x2) {
                     const uint4 e = pack_p(na, nb, ns, ikend);
-                    *reinterpret_cast<uint4*>(bp + curr_off + curr_n) = e;
+                    if (NL > 0 && curr_n < (uint32_t)NL)
+                        W->list[curr_n][vlane()] = e;
+                    else
+                        *reinterpret_cast<uint4*>(bp + cap + curr_n) = e;
                     if (curr_n == 0) head = e;  // prev[0] of the next step
                     ++curr_n;
                     curr_last_x2 = ns;
                 }
                 if (phase == P_BWD_RES) {
                     ++j;
-                    if ((uint32_t)j < prev_n) {  // extend prev[j] (already in pn) right away
+                    if ((uint32_t)j < prev_n) {  // extend prev[j] (read into pn last iteration) right away
                         ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
                         out = true;
                     } else if (curr_n == 0) {  // software/bwt.c:827
                         phase = P_SMEM_END;
                     } else {
-                        prev_off = curr_off;  // software/bwt.c:828: swap, next position
+                        prev_off = cap;  // software/bwt.c:828: swap, next position
                         prev_n = curr_n;
+                        prev_lds = true;
                         pn = head;
-                        curr_off = curr_off == cap ? 0 : cap;
                         --i;
                         phase = P_BWD_STEP;
                     }
@@ -681,7 +703,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         }
         // prev[j+1] and the query window land in LDS slots (no VGPR-destination
         // load the compiler would wait on right away); read back after the wait
-        const bool ld_pn = phase == P_BWD_RES && (uint32_t)j + 1 < prev_n;
+        const bool ld_pn = phase == P_BWD_RES && (uint32_t)j + 1 < prev_n && !(NL > 0 && prev_lds && j + 1 < NL);
         const bool ld_q = qwant != qb && qwant != ~0u;
         if (ld_pn)
             __builtin_amdgcn_global_load_lds(bp + prev_off + j + 1, LDS_PTR(&W->pn[0]),
@@ -700,6 +722,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         else
             fetch_buckets<FETCH>(P.bwt, W, want, kk, ll, vk, vl);  // ends with vmcnt(0)
         if (ld_pn) pn = W->pn[vlane()];
+        if constexpr (NL > 0) {  // prev[j+1] from the LDS list: read here, off the advance's critical path
+            if (phase == P_BWD_RES && prev_lds && (uint32_t)j + 1 < prev_n && j + 1 < NL) pn = W->list[j + 1][vlane()];
+        }
         if (ld_q) {
             qv = W->q[vlane()];
             qb = qwant;
@@ -811,12 +836,16 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // ------------------------------------------------------------ host launchers
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
     switch (variant) {
-        // 3: reference-layout buckets, cooperative fetch; 4: reference layout,
-        // per-lane fetch; 9: the default with cycle stamps
-        case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 4: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3>), dim3(grid), dim3(block), 0, st, *P); break;
-        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 3: reference-layout buckets, cooperative fetch, lists in global memory;
+        // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
+        // LDS at 2 blocks per CU; 6: Occ64, lists in global memory; 9: the
+        // default with cycle stamps
+        case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 4: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 5: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }

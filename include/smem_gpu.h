@@ -139,10 +139,12 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement:
  * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
- * device at init) with per-lane LDS-DMA fetch and bucket reuse;
- * 3 reference-layout buckets, cooperative fetch (16 per wave-instruction);
- * 4 reference layout, per-lane fetch; 9 the default with per-wave cycle
- * stamps (smem_batch_debug) */
+ * device at init), per-lane LDS-DMA fetch with bucket reuse, the first 7
+ * backward-list entries per lane in LDS; 3 reference-layout buckets,
+ * cooperative fetch, lists in global memory; 4 reference layout, per-lane
+ * fetch; 5 as 2 with 12 list entries in LDS (2 blocks per CU); 6 as 2 with
+ * lists in global memory; 9 the default with per-wave cycle stamps
+ * (smem_batch_debug) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
 /* variant 9 (stamped diagnostic build): copy the per-wave cycle split
  * {advance, fetch, compute, iterations, active lanes, t0, t1, 0} of the last

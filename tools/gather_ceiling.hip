@@ -12,7 +12,8 @@
 // mode 1: per-lane, 4 x global_load_dwordx4 per bucket, 2 buckets per lane;
 // mode 2: mode 0 with 32-B buckets (2 lanes x 16 B);
 // mode 3: the cooperative layout through registers (global_load_dwordx4 + ds_write_b128);
-// mode 4: per-lane buckets (2 per lane) by LDS-DMA, 4 chunk-planes per bucket.
+// mode 4: per-lane buckets (2 per lane) by LDS-DMA, 4 chunk-planes per bucket;
+// mode 5: mode 4 plus argv[8] lane-private cache-hit loads per round.
 // Every round waits for its data (vmcnt(0)) before the next, like the
 // kernel; addresses are independent so only bandwidth/queueing limit it.
 #include <hip/hip_runtime.h>
@@ -36,8 +37,8 @@ __device__ __forceinline__ uint32_t mix(uint32_t x) {
 
 template <int MODE>
 __global__ __launch_bounds__(256) void gather(const uint4* __restrict__ tab, uint32_t n_buckets, int iters,
-                                              uint32_t* __restrict__ sink, int active) {
-    __shared__ uint4 img[4][128][4];
+                                              uint32_t* __restrict__ sink, int active, int extra) {
+    __shared__ uint4 img[4][256][4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t seed = (blockIdx.x * 4 + w) * 0x9E3779B9u + lane * 0x85EBCA6Bu;
     uint32_t acc = 0;
@@ -65,6 +66,26 @@ __global__ __launch_bounds__(256) void gather(const uint4* __restrict__ tab, uin
                                                      (__attribute__((address_space(3))) void*)&img[w][(b * 4 + q) * 16][0],
                                                      16, 0, 0);
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint4* pl = &img[w][0][0];
+            const uint4 v = pl[lane], u = pl[7 * 64 + lane];
+            acc ^= v.x ^ u.w;
+        } else if (MODE == 5) {
+            // mode 4 plus `extra` per-lane 16-B LDS-DMA loads from a lane-private
+            // 4 KB arena (cache hits), like the list traffic of the seeding kernel
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const uint32_t bk = mix(seed + it * 2 + b) % n_buckets;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    __builtin_amdgcn_global_load_lds(tab + (uint64_t)bk * 4 + q,
+                                                     (__attribute__((address_space(3))) void*)&img[w][(b * 4 + q) * 16][0],
+                                                     16, 0, 0);
+            }
+            const uint4* arena = tab + ((uint64_t)(blockIdx.x * 256 + threadIdx.x) << 8);
+            for (int e = 0; e < extra; ++e)
+                __builtin_amdgcn_global_load_lds(arena + ((it * 7 + e) & 255),
+                                                 (__attribute__((address_space(3))) void*)&img[w][(8 + (e & 7)) * 16][0], 16, 0, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint4* pl = &img[w][0][0];
             const uint4 v = pl[lane], u = pl[7 * 64 + lane];
@@ -110,7 +131,11 @@ int main(int argc, char** argv) {
     CHECK(hipGetDeviceProperties(&prop, 0));
     uint4* tab;
     uint32_t* sink;
-    CHECK(hipMalloc(&tab, bytes));
+    // argv[7]: 1 = physically contiguous allocation (hipDeviceMallocContiguous: large TLB fragments)
+    if (argc > 7 && atoi(argv[7]) == 1)
+        CHECK(hipExtMallocWithFlags((void**)&tab, bytes, hipDeviceMallocContiguous));
+    else
+        CHECK(hipMalloc(&tab, bytes));
     CHECK(hipMalloc(&sink, 4));
     CHECK(hipMemset(tab, 1, bytes));
     const int bsz = mode == 2 ? 32 : 64;
@@ -120,21 +145,23 @@ int main(int argc, char** argv) {
     const int grid = prop.multiProcessorCount * wpc / 4;
     int active = argc > 6 ? atoi(argv[6]) : 64;  // mode 4: lanes that fetch
     if (active < 1 || active > 64) active = 64;
+    const int extra = argc > 8 ? atoi(argv[8]) : 0;  // mode 5: extra lane-private loads per round
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
     for (int rep = 0; rep < 3; ++rep) {
         CHECK(hipEventRecord(e0));
-        if (mode == 0) hipLaunchKernelGGL(gather<0>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active);
-        if (mode == 1) hipLaunchKernelGGL(gather<1>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active);
-        if (mode == 2) hipLaunchKernelGGL(gather<2>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active);
-        if (mode == 3) hipLaunchKernelGGL(gather<3>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active);
-        if (mode == 4) hipLaunchKernelGGL(gather<4>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active);
+        if (mode == 0) hipLaunchKernelGGL(gather<0>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 1) hipLaunchKernelGGL(gather<1>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 2) hipLaunchKernelGGL(gather<2>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 3) hipLaunchKernelGGL(gather<3>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 4) hipLaunchKernelGGL(gather<4>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 5) hipLaunchKernelGGL(gather<5>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
-        const double nbk = (double)grid * 4 * iters * (mode == 4 ? 2 * active : 128);  // buckets fetched
+        const double nbk = (double)grid * 4 * iters * (mode == 4 ? 2 * active : 128);  // buckets fetched (mode 5: 128)
         printf("{\"table_MB\": %zu, \"waves_per_cu\": %d, \"mode\": %d, \"bucket_B\": %d, \"ms\": %.3f, "
                "\"Gbuckets_per_s\": %.2f, \"TB_per_s\": %.3f, \"active\": %d, \"us_per_round\": %.3f}\n",
                mb, wpc, mode, bsz, ms, nbk / ms * 1e-6, nbk * bsz / ms * 1e-9, active, ms * 1e3 / iters);
