@@ -404,6 +404,11 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     uint4 pn = {0, 0, 0, 0}, head = {0, 0, 0, 0};  // prev[j+1] in flight, curr[0]
     uint64_t na = 0, nb = 0, ns = 0;
     uint32_t tag0 = ~0u, tag1 = ~0u;  // FETCH_OCC64: buckets held in the lane's two LDS slots
+    // wave-cooperative backward step (tail of the batch): idle lanes extend
+    // entries of one owner lane's prev list; wave-uniform descriptor of the
+    // batch handed to the owner's next BWD_RES
+    int bat_o = -1, bat_m = 0;
+    uint64_t bat_h = 0;
     uint64_t st_adv = 0, st_fetch = 0, st_comp = 0, st_iter = 0, st_active = 0, st_t0 = 0, st_t1 = 0;
     if constexpr (STAMP) st_t0 = rtstamp();
 
@@ -597,12 +602,25 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 phase = P_BWD_STEP;
             }
             if (phase == P_BWD_RES) {  // software/bwt.c:815-825; na = x[0], nb = x[1]
-                if (ns < (uint64_t)min_intv) {
-                    // only prev[0] can be kept, when nothing longer survived
-                    if (curr_n == 0 && (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start)) {
-                        if (raw_n >= P.cap_intv) {
-                            phase = P_OVF;
-                        } else {
+                // the lane's own result for prev[j], then (helped owner only) the
+                // results idle lanes computed for prev[j+1 .. j+bat_m], in order
+                const int nres = 1 + (lane == bat_o ? bat_m : 0);
+                uint64_t hm = bat_h;
+                for (int r = 0; r < nres; ++r) {
+                    if (r > 0) {
+                        const int h = __builtin_ctzll(hm);
+                        hm &= hm - 1;
+                        const uint4 ent = W->pn[h], res = W->q[h];
+                        ik0 = p_x0(ent); ik1 = p_x1(ent); ik2 = p_x2(ent); ikend = p_end(ent);
+                        na = p_x0(res); nb = p_x1(res); ns = p_x2(res);
+                    }
+                    if (ns < (uint64_t)min_intv) {
+                        // only prev[0] can be kept, when nothing longer survived
+                        if (curr_n == 0 && (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start)) {
+                            if (raw_n >= P.cap_intv) {
+                                phase = P_OVF;
+                                break;
+                            }
                             const uint64_t info = (uint64_t)ikend | ((uint64_t)(i + 1) << 32);
                             P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{ik0, ik1, ik2, info};
                             ++mem_n;
@@ -613,19 +631,19 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                                 max_mid = (ikend + (uint32_t)(i + 1)) >> 1;
                             }
                         }
+                    } else if (curr_n == 0 || ns != curr_last_x2) {
+                        const uint4 e = pack_p(na, nb, ns, ikend);
+                        if (NL > 0 && curr_n < (uint32_t)NL)
+                            W->list[curr_n][vlane()] = e;
+                        else
+                            *reinterpret_cast<uint4*>(bp + cap + curr_n) = e;
+                        if (curr_n == 0) head = e;  // prev[0] of the next step
+                        ++curr_n;
+                        curr_last_x2 = ns;
                     }
-                } else if (curr_n == 0 || ns != curr_last_x2) {
-                    const uint4 e = pack_p(na, nb, ns, ikend);
-                    if (NL > 0 && curr_n < (uint32_t)NL)
-                        W->list[curr_n][vlane()] = e;
-                    else
-                        *reinterpret_cast<uint4*>(bp + cap + curr_n) = e;
-                    if (curr_n == 0) head = e;  // prev[0] of the next step
-                    ++curr_n;
-                    curr_last_x2 = ns;
+                    ++j;
                 }
                 if (phase == P_BWD_RES) {
-                    ++j;
                     if ((uint32_t)j < prev_n) {  // extend prev[j] (read into pn last iteration) right away
                         ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
                         out = true;
@@ -684,7 +702,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         // ---- uniform section: every lane takes part in the cooperative
         // bucket fetch; the loads for the next iteration are issued here ----
         const bool live = phase != P_EXIT;
-        const bool want = phase == P_BWD_RES || phase == P_FWD_RES;  // an extend request
+        bool want = phase == P_BWD_RES || phase == P_FWD_RES;  // an extend request
         uint64_t tb = 0;
         if constexpr (STAMP) {
             tb = stamp();
@@ -701,18 +719,65 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 next_offsets(P, nitem, no0, nlen);
             }
         }
-        // prev[j+1] and the query window land in LDS slots (no VGPR-destination
-        // load the compiler would wait on right away); read back after the wait
-        const bool ld_pn = phase == P_BWD_RES && (uint32_t)j + 1 < prev_n && !(NL > 0 && prev_lds && j + 1 < NL);
+        // Lanes that found the work queue empty help: when the wave has idle
+        // lanes and a lane in a backward step with more entries left, each idle
+        // lane extends one of those entries (same base, independent of each
+        // other, software/bwt.c:812-826) and leaves entry + result in its pn / q
+        // slots; the owner consumes them in order next iteration.  This cuts the
+        // dependent chain of the few repeat-rich reads left at the end.
+        bat_o = -1;
+        bat_m = 0;
+        bat_h = 0;
+        bool helper = false;
+        uint4 hent = {0, 0, 0, 0};
+        int hc = 0;
+        if constexpr (FETCH == FETCH_OCC64) {
+            const uint64_t idle = __ballot(phase == P_EXIT);
+            if (idle) {
+                const uint64_t elig = __ballot(phase == P_BWD_RES && (uint32_t)j + 1 < prev_n);
+                if (elig) {
+                    const int o = __builtin_ctzll(elig);
+                    const uint32_t jo = __builtin_amdgcn_readlane((int)j, o);
+                    const uint32_t pno = __builtin_amdgcn_readlane((int)prev_n, o);
+                    const uint32_t poff = __builtin_amdgcn_readlane((int)prev_off, o);
+                    const int plds = __builtin_amdgcn_readlane((int)prev_lds, o);
+                    const int co = __builtin_amdgcn_readlane(cur_c, o);
+                    const uint32_t m = min((uint32_t)__popcll(idle), pno - jo - 1);
+                    const int me = vlane();
+                    const uint32_t r = (uint32_t)__popcll(idle & ((1ull << me) - 1));
+                    helper = phase == P_EXIT && r < m;
+                    if (helper) {
+                        const uint32_t e = jo + 1 + r;
+                        const PIntv* obp = reinterpret_cast<const PIntv*>(
+                            P.scratch + ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + o) * 2ull * cap);
+                        hent = (NL > 0 && plds && e < (uint32_t)NL) ? W->list[e][o] : load_p(obp + poff + e);
+                        hc = co;
+                    }
+                    bat_o = o;
+                    bat_m = (int)m;
+                    bat_h = __ballot(helper);
+                }
+            }
+        }
+        // prev[j+1] (the owner of a helped batch: prev[j+1+bat_m]) and the query
+        // window land in LDS slots (no VGPR-destination load the compiler would
+        // wait on right away); read back after the wait
+        const uint32_t pidx = (uint32_t)j + 1 + (lane == bat_o ? (uint32_t)bat_m : 0u);
+        const bool ld_pn = phase == P_BWD_RES && pidx < prev_n && !(NL > 0 && prev_lds && pidx < (uint32_t)NL);
         const bool ld_q = qwant != qb && qwant != ~0u;
         if (ld_pn)
-            __builtin_amdgcn_global_load_lds(bp + prev_off + j + 1, LDS_PTR(&W->pn[0]),
+            __builtin_amdgcn_global_load_lds(bp + prev_off + pidx, LDS_PTR(&W->pn[0]),
                                              16, 0, 0);
         if (ld_q)
             __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&W->q[0]), 16, 0, 0);
-        // the interval to extend: ik forward (a = x[1]), prev[j] backward (a = x[0])
+        // the interval to extend: ik forward (a = x[1]), prev[j] backward (a = x[0]),
+        // a helper's entry backward
+        want = want || helper;
         const bool fwd = phase == P_FWD_RES;
-        const uint64_t ra = fwd ? ik1 : ik0, rb = fwd ? ik0 : ik1, rs = ik2;
+        const uint64_t hx0 = p_x0(hent), hx1 = p_x1(hent), hx2 = p_x2(hent);
+        const uint64_t ra = helper ? hx0 : (fwd ? ik1 : ik0), rb = helper ? hx1 : (fwd ? ik0 : ik1),
+                       rs = helper ? hx2 : ik2;
+        const int rc = helper ? hc : cur_c;
         const uint64_t k = ra - 1, l = k + rs;
         const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
         Bucket vk, vl;
@@ -722,8 +787,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         else
             fetch_buckets<FETCH>(P.bwt, W, want, kk, ll, vk, vl);  // ends with vmcnt(0)
         if (ld_pn) pn = W->pn[vlane()];
-        if constexpr (NL > 0) {  // prev[j+1] from the LDS list: read here, off the advance's critical path
-            if (phase == P_BWD_RES && prev_lds && (uint32_t)j + 1 < prev_n && j + 1 < NL) pn = W->list[j + 1][vlane()];
+        if constexpr (NL > 0) {  // prev[pidx] from the LDS list: read here, off the advance's critical path
+            if (phase == P_BWD_RES && prev_lds && pidx < prev_n && pidx < (uint32_t)NL) pn = W->list[pidx][vlane()];
         }
         if (ld_q) {
             qv = W->q[vlane()];
@@ -736,9 +801,13 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         }
         if (want) {
             if constexpr (FETCH == FETCH_OCC64)
-                extend_counts64(P, ra, rb, rs, cur_c, kk, ll, wk, wl, na, nb, ns);
+                extend_counts64(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
             else
-                extend_counts(P, ra, rb, rs, cur_c, kk, ll, vk, vl, na, nb, ns);
+                extend_counts(P, ra, rb, rs, rc, kk, ll, vk, vl, na, nb, ns);
+        }
+        if (helper) {  // entry + result for the owner's next BWD_RES
+            W->pn[vlane()] = hent;
+            W->q[vlane()] = pack_p(na, nb, ns, 0);
         }
         if constexpr (STAMP) {
             asm volatile("" ::"v"(na), "v"(nb), "v"(ns));
