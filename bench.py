@@ -19,7 +19,9 @@ with no collective in the data path (index replicated): scaling "weak".
 roofline: dominant kernel = seed_kernel; achieved = algorithmic bytes per
 launch (64 B x distinct Occ buckets per extend + read length
 + 32 B x intervals out, counted by the CPU oracle on a sample of the same
-reads) / the kernel's HIP-event duration measured here.
+reads) / the kernel's HIP-event duration measured here; achieved_occ64 is the
+same with the 32-B buckets of this build's index layout; traffic is the
+per-launch FETCH_SIZE recorded by tools/pmc_passes.sh for this workload.
 
 cpu_baseline: the reference's own C (oracle/_ref/ref_harness, compiled from
 the reference sources) when present, else the C restatement, timed on this
@@ -63,7 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--stats-sample", type=int, default=20000, help="reads counted by the oracle for bytes/read")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
-    p.add_argument("--traffic-json", default="", help="per-launch HBM bytes measured by rocprofv3 --pmc")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="per-launch FETCH_SIZE bytes measured by rocprofv3 --pmc for this workload")
     return p.parse_args()
 
 
@@ -121,14 +124,31 @@ def cpu_baseline(args, idx, idx_path, reads, cores):
 
 
 def algorithmic_bytes(args, idx, reads):
-    """SURVEY.md §8(d) bytes/read, counted by the oracle on a sample."""
+    """SURVEY.md §8(d) bytes/read (64 B per distinct reference-layout Occ bucket
+    of each bwt_extend + read + 32 B per interval), and the same with the
+    32-B Occ64 buckets this build reads, counted by the oracle on a sample."""
     from oracle import oracle
     oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
     n = min(reads.n, args.stats_sample)
     s = reads.subset(np.arange(n))
     per, st = oracle.seed_stats(oi, s.codes, s.offs, threads=min(16, os.cpu_count() or 1))
     oi.close()
-    return float(per["bytes"].mean()), st, n
+    b64 = (32.0 * st["n_bkt64"] + st["n_bases"] + 32.0 * st["n_intv"]) / max(n, 1)
+    return float(per["bytes"].mean()), b64, st, n
+
+
+def traffic_for(args, path: str):
+    """Per-launch L2 fabric read bytes (rocprofv3 FETCH_SIZE) recorded for this
+    exact workload by tools/pmc_passes.sh, or None."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        t = json.load(fh)
+    w = t.get("workload", {})
+    if (w.get("genome_mbp"), w.get("reads"), w.get("read_len"), w.get("seed")) != (
+            args.genome_mbp, args.reads, args.read_len, args.seed):
+        return None
+    return t.get("bytes_per_launch")
 
 
 class Dist:
@@ -229,13 +249,10 @@ def main():
     pcie = pcie_inclusive(batch, reads, opt) if rank == 0 else None
 
     if rank == 0:
-        bpr, ostats, n_counted = algorithmic_bytes(args, idx, reads)
+        bpr, bpr64, ostats, n_counted = algorithmic_bytes(args, idx, reads)
         k_ms = float(np.mean(kernel_ms))
         achieved = bpr * reads.n / (k_ms * 1e-3) / 1e9
-        traffic = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as fh:
-                traffic = json.load(fh).get("bytes_per_launch")
+        traffic = traffic_for(args, args.traffic_json)
         cores = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
         cpu = None
         if args.cpu_seconds > 0:
@@ -274,6 +291,8 @@ def main():
                 "kernel": "seed_kernel",
                 "kernel_ms": round(k_ms, 3),
                 "bytes_per_read": round(bpr, 1),
+                "bytes_per_read_occ64": round(bpr64, 1),
+                "achieved_occ64": round(bpr64 * reads.n / (k_ms * 1e-3) / 1e9, 2),
                 "bytes_per_read_sample": n_counted,
                 "extends_per_read": round(ostats["n_ext"] / max(n_counted, 1), 1),
             },

@@ -35,7 +35,7 @@ class OptT(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("n_calls", "n_intv", "n_smem1", "n_ext", "n_ext_ref", "n_bkt",
-                                          "n_bkt_ref", "n_bases")]
+                                          "n_bkt_ref", "n_bases", "n_bkt64")]
 
     def as_dict(self) -> dict:
         return {k: int(getattr(self, k)) for k, _ in self._fields_}

@@ -162,7 +162,11 @@ static void count_extend(const orc_bwt_t *b, const orc_intv_t *ik, int is_back, 
 	uint64_t nb = (k == (uint64_t)-1) ? 1 : 1 + ((kk >> 7) != (ll >> 7));
 	st->n_ext_ref++;
 	st->n_bkt_ref += nb;
-	if (used) { st->n_ext++; st->n_bkt += nb; }
+	if (used) {
+		st->n_ext++;
+		st->n_bkt += nb;
+		st->n_bkt64 += (k == (uint64_t)-1) ? 1 : 1 + ((kk >> 6) != (ll >> 6));
+	}
 }
 
 /* ------------------------------------------------------------ bwt_smem1 */
@@ -361,7 +365,7 @@ static void add_stats(orc_stats_t *d, const orc_stats_t *s)
 {
 	d->n_calls += s->n_calls; d->n_intv += s->n_intv; d->n_smem1 += s->n_smem1;
 	d->n_ext += s->n_ext; d->n_ext_ref += s->n_ext_ref; d->n_bkt += s->n_bkt;
-	d->n_bkt_ref += s->n_bkt_ref; d->n_bases += s->n_bases;
+	d->n_bkt_ref += s->n_bkt_ref; d->n_bases += s->n_bases; d->n_bkt64 += s->n_bkt64;
 }
 
 int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,

@@ -51,6 +51,7 @@ typedef struct {
 	uint64_t n_bkt;         /* distinct 64-B Occ buckets over n_ext (1 or 2 each) */
 	uint64_t n_bkt_ref;     /* same over n_ext_ref */
 	uint64_t n_bases;       /* query bases of reads that entered the loop */
+	uint64_t n_bkt64;       /* distinct 32-B Occ64 buckets (64 symbols) over n_ext: the GPU layout */
 } orc_stats_t;
 
 orc_bwt_t *orc_bwt_load(const char *fn);
