@@ -227,7 +227,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 6) || variant == 9)) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 7) || variant == 9)) return SMEM_E_ARG;
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }

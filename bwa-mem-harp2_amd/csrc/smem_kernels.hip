@@ -356,7 +356,7 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 // STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
-template <int FETCH, bool STAMP, int WPE, int NLIST>
+template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -432,16 +432,22 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         // `out` when it has an extend request (or yields); the pass has a
         // single exit at the bottom, which keeps the exec-mask bookkeeping of
         // the structurized loop (and so the register count) small.
-        while (phase != P_EXIT) {
-            if constexpr (STAMP) {  // which blocks this pass of the wave executes
+        // ONE pass per iteration (SINGLE): a lane that still needs an earlier
+        // block after this pass (end of a bwt_smem1 call: ~1 % of lane-
+        // iterations) continues next iteration without an extend, instead of
+        // the whole wave running a second pass.
+        bool out = false;
+        for (int pass = 0; phase != P_EXIT && (pass == 0 || !SINGLE); ++pass) {
+            if constexpr (STAMP) {  // which blocks this pass of the wave starts in (any lane)
                 const uint64_t act = __ballot(1);
+                uint32_t any = 0;
+                for (int ph = 0; ph < P_EXIT; ++ph) any |= (__ballot(phase == ph) ? 1u : 0u) << ph;
                 if (lane == __ffsll((unsigned long long)act) - 1) {
                     scnt[threadIdx.x >> 6][15] += 1;
-                    for (int ph = 0; ph < P_EXIT; ++ph)
-                        if (__ballot(phase == ph)) scnt[threadIdx.x >> 6][ph] += 1;
+                    for (int ph = 0; ph < P_EXIT; ++ph) scnt[threadIdx.x >> 6][ph] += (any >> ph) & 1;
                 }
             }
-            bool out = false;
+            out = false;
             if (phase == P_SMEM_END) {
                 if (!middle) {  // software/bwamem.c:261-272
                     start = ret;
@@ -702,7 +708,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         // ---- uniform section: every lane takes part in the cooperative
         // bucket fetch; the loads for the next iteration are issued here ----
         const bool live = phase != P_EXIT;
-        bool want = phase == P_BWD_RES || phase == P_FWD_RES;  // an extend request
+        bool want = out && (phase == P_BWD_RES || phase == P_FWD_RES);  // an extend request
         uint64_t tb = 0;
         if constexpr (STAMP) {
             tb = stamp();
@@ -907,12 +913,14 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
     switch (variant) {
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
-        // LDS at 2 blocks per CU; 6: Occ64, lists in global memory; 9: the
-        // default with cycle stamps
+        // LDS at 2 blocks per CU; 6: Occ64, lists in global memory; 7: the
+        // default with several advance passes per iteration; 9: the default
+        // with cycle stamps
         case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 4: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 5: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12>), dim3(grid), dim3(block), 0, st, *P); break;
         case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, false>), dim3(grid), dim3(block), 0, st, *P); break;
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
         default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
     }
