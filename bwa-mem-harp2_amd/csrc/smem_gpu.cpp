@@ -227,7 +227,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 7) || variant == 9)) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 8) || variant == 9)) return SMEM_E_ARG;
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }
@@ -372,6 +372,8 @@ int smem_batch_set_reads_packed(smem_batch_t* b, int n_reads, const uint8_t* cod
 
 static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& P) {
     std::memset(&P, 0, sizeof(P));
+    P.s_intv = b->d_sz_intv.p;   // per-read output sizes, written by the seeding kernel
+    P.s_calls = b->d_sz_calls.p;
     P.bwt = b->g->d_bwt;
     P.occ64 = b->g->d_occ64;
     P.primary = b->g->primary;
@@ -463,7 +465,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
         b->ovf_cap_calls = cap_c;
         HIP_TRY(smem_launch_ovf_slot(b->d_ovf_items.p, n_ovf, b->d_ovf_slot.p, b->st));
     }
-    // finalize: raw lists -> smem_next2 lists (count, scan, write)
+    // finalize: raw lists -> smem_next2 lists (scan of the sizes, write)
     HIP_TRY(hipEventRecord(b->ev[2], b->st));
     smem::FinalizeParams F;
     std::memset(&F, 0, sizeof(F));
@@ -485,7 +487,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     F.s_calls = b->d_sz_calls.p;
     F.intv_off = b->d_intv_off.p;
     F.call_off = b->d_call_off.p;
-    HIP_TRY(smem_launch_finalize(&F, 0, b->st));
+    // (the sizes were written by the seeding kernel as each read completed)
     size_t tmp = b->d_scan_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_sz_intv.p, b->d_intv_off.p, n, b->d_scan_tmp.p, &tmp, b->st));
     HIP_TRY(smem_launch_offsets(b->d_sz_calls.p, b->d_call_off.p, n, b->d_scan_tmp.p, &tmp, b->st));

@@ -36,6 +36,8 @@ struct SeedParams {
     uint32_t cap_calls;
     uint32_t* n_intv;          // [item] raw intervals, or SMEM_OVERFLOW
     uint32_t* n_calls;         // [item]
+    uint64_t* s_intv;          // [read] intervals smem_next2 returns for the read (compaction sizes)
+    uint64_t* s_calls;         // [read] smem_next2 lists of the read
     int32_t* ovf_count;
     int32_t* ovf_items;
     int32_t* head;             // work counter, zeroed before each launch

@@ -331,12 +331,12 @@ __device__ __forceinline__ void fetch_occ64(const uint32_t* __restrict__ occ, WL
 }
 
 // offsets of work item `it` (read_ids maps overflow-pass items to reads)
-__device__ __forceinline__ void next_offsets(const SeedParams& P, int it, uint32_t& o0, int& len) {
+__device__ __forceinline__ void next_offsets(const SeedParams& P, int it, uint32_t& o0, int& len, int& rid) {
     if (it >= P.n_items) {
         len = 0;
         return;
     }
-    const int rid = P.read_ids ? P.read_ids[it] : it;
+    rid = P.read_ids ? P.read_ids[it] : it;
     const uint64_t a = P.offs[rid], b = P.offs[rid + 1];
     o0 = (uint32_t)a;
     len = (int)(b - a);
@@ -381,6 +381,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     int phase = P_FETCH;
     int item = -1, len = 0;
     int nitem = 0, nlen = -2;  // next read: -2 nothing claimed, -1 claimed, >= 0 offsets loaded
+    int rid = 0, nrid = 0;     // read index of the item (overflow pass: through read_ids)
+    uint32_t keep_n = 0;       // intervals of the read that smem_next2 returns (matches + kept sub-matches)
     uint32_t o0 = 0, no0 = 0;
     uint32_t qb = ~0u, qwant = ~0u;      // 16-B query window held / wanted (offsets into codes)
     uint4 qv = {0, 0, 0, 0};
@@ -491,6 +493,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     out = true;
                 } else {
                     item = nitem;
+                    rid = nrid;
+                    keep_n = 0;
                     o0 = no0;
                     len = nlen;
                     nlen = -2;
@@ -500,6 +504,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     if (len < P.min_seed_len) {  // mem_chain's guard (software/bwamem.c:600)
                         P.n_intv[item] = 0;
                         P.n_calls[item] = 0;
+                        P.s_intv[rid] = 0;
+                        P.s_calls[rid] = 0;
                         out = true;  // stays in P_FETCH: the next claim is issued below
                     } else {
                         phase = P_NEXT2;
@@ -522,6 +528,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 } else if (start >= len || start < 0) {  // iterator exhausted
                     P.n_intv[item] = raw_n;
                     P.n_calls[item] = calls_n;
+                    P.s_intv[rid] = keep_n;  // sizes for the compaction scan (no count pass)
+                    P.s_calls[rid] = calls_n;
                     phase = P_FETCH;
                 } else {
                     ori_start = start;
@@ -629,6 +637,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                             }
                             const uint64_t info = (uint64_t)ikend | ((uint64_t)(i + 1) << 32);
                             P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{ik0, ik1, ik2, info};
+                            // the merge keeps a sub-match if it is at least half the longest
+                            // match and ends after the call's start (software/bwamem.c:284-292)
+                            keep_n += !middle || (ikend - (uint32_t)(i + 1) >= (max_len >> 1) && ikend > (uint32_t)ori_start);
                             ++mem_n;
                             mem_last_start = (uint32_t)(i + 1);
                             if (!middle && ikend - (uint32_t)(i + 1) >= max_len) {
@@ -689,6 +700,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                                 const uint64_t info = (uint64_t)p_end(pn) | ((uint64_t)(i + 1) << 32);
                                 P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] =
                                     Intv{p_x0(pn), p_x1(pn), p_x2(pn), info};
+                                keep_n += !middle || (p_end(pn) - (uint32_t)(i + 1) >= (max_len >> 1) &&
+                                                      p_end(pn) > (uint32_t)ori_start);
                                 ++mem_n;
                                 mem_last_start = (uint32_t)(i + 1);
                                 if (!middle && p_end(pn) - (uint32_t)(i + 1) >= max_len) {
@@ -722,7 +735,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 nitem = atomicAdd(P.head, 1);
                 nlen = -1;
             } else if (nlen == -1) {  // its offsets (the claim returned last iteration)
-                next_offsets(P, nitem, no0, nlen);
+                next_offsets(P, nitem, no0, nlen, nrid);
             }
         }
         // Lanes that found the work queue empty help: when the wave has idle
@@ -834,10 +847,13 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
 // (software/bwt.c:830) and merge matches with sub-matches keyed by
 // (start, len - end), keeping a sub-match only if it is at least half the
 // longest match and ends after the call's start (software/bwamem.c:280-301).
-// One thread per read; WRITE=false computes the sizes, WRITE=true writes them.
-template <bool WRITE>
+// Four threads per read, one per 8-B word of bwtintv_t: all four walk the
+// same merge (on the info words) and each moves its own word, so a wave's
+// loads and stores touch 16 intervals' lines instead of 64.  The per-read
+// sizes come from the seeding kernel.
 __global__ __launch_bounds__(256) void finalize_kernel(FinalizeParams F) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = (int)(t >> 2), w = (int)(t & 3);
     if (r >= F.n) return;
     const Intv* raw = F.main_intv + (uint64_t)r * F.cap_intv;
     const CallRec* rec = F.main_call + (uint64_t)r * F.cap_calls;
@@ -849,50 +865,48 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeParams F) {
         nc = F.ovf_n_calls[s];
     }
     const uint32_t len = (uint32_t)(F.offs[r + 1] - F.offs[r]);
-    uint64_t out = WRITE ? F.intv_off[r] : 0, total = 0;
-    const uint64_t cout = WRITE ? F.call_off[r] : 0;
-    uint32_t pos = 0;
+    const uint64_t* rw = reinterpret_cast<const uint64_t*>(raw);
+    uint64_t* ow = reinterpret_cast<uint64_t*>(F.flat_intv + F.intv_off[r]);
+    const uint64_t cout = F.call_off[r];
+    uint32_t pos = 0, out = 0;
     for (uint32_t c = 0; c < nc; ++c) {
         const CallRec cr = rec[c];
-        const Intv* M = raw + pos;           // M[m_n-1-a] is the a-th match in final order
-        const Intv* S = raw + pos + cr.m_n;  // likewise for sub-matches
+        // M[m_n-1-a] is the a-th match in final order; likewise S for sub-matches
+        const uint64_t* M = rw + (uint64_t)pos * 4;
+        const uint64_t* S = rw + (uint64_t)(pos + cr.m_n) * 4;
         const uint64_t half = (uint64_t)(cr.max_len >> 1);
         uint32_t a = 0, b = 0, n = 0;
-        while (a < cr.m_n && b < cr.s_n) {
-            const Intv ma = M[cr.m_n - 1 - a], sb = S[cr.s_n - 1 - b];
-            const uint64_t xi = (ma.info >> 32 << 32) | (uint64_t)(uint32_t)(len - (uint32_t)ma.info);
-            const uint64_t xj = (sb.info >> 32 << 32) | (uint64_t)(uint32_t)(len - (uint32_t)sb.info);
-            if ((int64_t)xi < (int64_t)xj) {
-                if (WRITE) F.flat_intv[out + n] = ma;
+        while (a < cr.m_n || b < cr.s_n) {
+            bool take_m;
+            uint64_t si = 0;
+            if (b >= cr.s_n) {
+                take_m = true;
+            } else {
+                si = S[(uint64_t)(cr.s_n - 1 - b) * 4 + 3];
+                if (a >= cr.m_n) {
+                    take_m = false;
+                } else {
+                    const uint64_t mi = M[(uint64_t)(cr.m_n - 1 - a) * 4 + 3];
+                    const uint64_t xi = (mi >> 32 << 32) | (uint64_t)(uint32_t)(len - (uint32_t)mi);
+                    const uint64_t xj = (si >> 32 << 32) | (uint64_t)(uint32_t)(len - (uint32_t)si);
+                    take_m = (int64_t)xi < (int64_t)xj;
+                }
+            }
+            if (take_m) {
+                ow[(uint64_t)(out + n) * 4 + w] = M[(uint64_t)(cr.m_n - 1 - a) * 4 + w];
                 ++n;
                 ++a;
             } else {
-                if ((uint64_t)(uint32_t)sb.info - (sb.info >> 32) >= half && (uint32_t)sb.info > cr.ori_start) {
-                    if (WRITE) F.flat_intv[out + n] = sb;
+                if ((uint64_t)(uint32_t)si - (si >> 32) >= half && (uint32_t)si > cr.ori_start) {
+                    ow[(uint64_t)(out + n) * 4 + w] = S[(uint64_t)(cr.s_n - 1 - b) * 4 + w];
                     ++n;
                 }
                 ++b;
             }
         }
-        for (; a < cr.m_n; ++a) {
-            if (WRITE) F.flat_intv[out + n] = M[cr.m_n - 1 - a];
-            ++n;
-        }
-        for (; b < cr.s_n; ++b) {
-            const Intv sb = S[cr.s_n - 1 - b];
-            if ((uint64_t)(uint32_t)sb.info - (sb.info >> 32) >= half && (uint32_t)sb.info > cr.ori_start) {
-                if (WRITE) F.flat_intv[out + n] = sb;
-                ++n;
-            }
-        }
-        if (WRITE) F.flat_calls[cout + c] = n;
+        if (w == 0) F.flat_calls[cout + c] = n;
         out += n;
-        total += n;
         pos += cr.m_n + cr.s_n;
-    }
-    if (!WRITE) {
-        F.s_intv[r] = total;
-        F.s_calls[r] = nc;
     }
 }
 
@@ -921,6 +935,7 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 5: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12>), dim3(grid), dim3(block), 0, st, *P); break;
         case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, false>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 8: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
         default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
     }
@@ -928,12 +943,9 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
 }
 
 extern "C" hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int write, hipStream_t st) {
-    if (F->n <= 0) return hipSuccess;
-    const unsigned g = (unsigned)((F->n + 255) / 256);
-    if (write)
-        hipLaunchKernelGGL(smem::finalize_kernel<true>, dim3(g), dim3(256), 0, st, *F);
-    else
-        hipLaunchKernelGGL(smem::finalize_kernel<false>, dim3(g), dim3(256), 0, st, *F);
+    if (F->n <= 0 || !write) return hipSuccess;  // sizes come from the seeding kernel: no count pass
+    const unsigned g = (unsigned)((4ull * F->n + 255) / 256);
+    hipLaunchKernelGGL(smem::finalize_kernel, dim3(g), dim3(256), 0, st, *F);
     return hipGetLastError();
 }
 
