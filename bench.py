@@ -13,8 +13,12 @@ builder; its size is reported in `config`.
 A step = one pass of the seeding hot path (mem_insert_seed's smem_next2 loop
 for every read, software/bwamem.c:453-460) over the resident batch: the
 seeding kernel plus result compaction, outputs left in HBM (host transfers
-excluded; DESIGN.md gives the PCIe-inclusive rate).  Reads shard across ranks
-with no collective in the data path (index replicated): scaling "weak".
+excluded; DESIGN.md gives the PCIe-inclusive rate).  As the reference's
+kt_for_batch workers do, --streams host workers (default 2) each own a batch
+(all the reads) and a HIP stream and run whole steps dealt round-robin, so
+one step's tail overlaps the next step's start; K steps are timed in total.
+Reads shard across ranks with no collective in the data path (index
+replicated): scaling "weak".
 
 roofline: dominant kernel = seed_kernel; achieved = algorithmic bytes per
 launch (64 B x distinct Occ buckets per extend + read length
@@ -62,6 +66,7 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu", help="index construction (same bytes)")
     p.add_argument("--lanes-per-cu", type=int, default=0)
+    p.add_argument("--streams", type=int, default=2, help="host workers, each with its own batch and HIP stream")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--stats-sample", type=int, default=20000, help="reads counted by the oracle for bytes/read")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
@@ -70,7 +75,7 @@ def parse():
     return p.parse_args()
 
 
-def get_index(args, rank, world, barrier):
+def get_index(args, rank, world, barrier, device=0):
     import smemgpu
     from smemgpu import synth
     os.makedirs(args.cache, exist_ok=True)
@@ -79,7 +84,7 @@ def get_index(args, rank, world, barrier):
     if rank == 0 and not os.path.exists(key):
         t = time.time()
         g = synth.make_genome(n_bp, seed=args.seed, n_chrom=24)
-        idx = smemgpu.Index.build_gpu(g.codes, device=0) if args.builder == "gpu" else smemgpu.Index.build(g.codes)
+        idx = smemgpu.Index.build_gpu(g.codes, device=device) if args.builder == "gpu" else smemgpu.Index.build(g.codes)
         idx.write(key + ".tmp")
         os.replace(key + ".tmp", key)
         del g
@@ -164,10 +169,14 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", 1))
         self.local = int(os.environ.get("LOCAL_RANK", 0))
         self.device = "cpu"
+        # the GPU this rank drives (local rank, wrapped when a rehearsal runs
+        # more ranks than the node has GPUs)
+        n_dev = torch.cuda.device_count()
+        self.gpu = self.local % n_dev if n_dev > 0 else 0
         if self.world > 1:
-            backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            backend = backend or os.environ.get("SMEM_DIST_BACKEND") or ("nccl" if n_dev > 0 else "gloo")
             if backend == "nccl":
-                torch.cuda.set_device(self.local)
+                torch.cuda.set_device(self.gpu)
                 self.device = "cuda"
             dist.init_process_group(backend)
 
@@ -224,23 +233,57 @@ def main():
     rank, world, local = d.rank, d.world, d.local
     barrier = d.barrier
 
-    idx, idx_path = get_index(args, rank, world, barrier)
+    idx, idx_path = get_index(args, rank, world, barrier, d.gpu)
     reads = make_reads(args, rank)
-    gpu = smemgpu.Gpu(idx, device=local, lanes_per_cu=args.lanes_per_cu)
-    batch = gpu.batch(reads.n, int(reads.codes.size), int(reads.lens.max()))
-    batch.set_reads(reads.codes, reads.offs)  # inputs resident in HBM before timing
+    gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu)
+    # one batch object (own HIP stream, own buffers) per host worker, each
+    # holding the whole read set: a step is one full pass over the reads
+    batches = []
+    for _ in range(max(1, args.streams)):
+        b = gpu.batch(reads.n, int(reads.codes.size), int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)  # inputs resident in HBM before timing
+        batches.append(b)
+    batch = batches[0]
     torch.cuda.synchronize()
 
     opt = smemgpu.Options()
-    for _ in range(args.warmup):
-        batch.run(opt)
+    # warmup; the seeding kernel's duration for the roofline is taken from
+    # launches that run alone on the GPU (no other stream's kernels beside them)
     kernel_ms = []
+    for w in range(max(args.warmup, 2)):
+        batch.run(opt)
+        if w > 0:
+            kernel_ms.append(batch.stats()["kernel_ms"])
+    for b in batches[1:]:
+        b.run(opt)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        batch.run(opt)
-        kernel_ms.append(batch.stats()["kernel_ms"])
+    if len(batches) == 1:
+        for _ in range(args.steps):
+            batch.run(opt)
+    else:
+        # kt_for_batch-style workers (the reference's own host model,
+        # software/kthread_batch.c:29-59): steps are dealt round-robin, each
+        # worker runs whole steps on its own stream, so one step's tail and
+        # compaction overlap the next step's seeding
+        import threading
+        errs = []
+
+        def worker(wi):
+            try:
+                for k in range(wi, args.steps, len(batches)):
+                    batches[wi].run(opt)
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(wi,)) for wi in range(len(batches))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -278,7 +321,8 @@ def main():
                 "read_len": args.read_len,
                 "genome_bp": int(args.genome_mbp * 1e6),
                 "index_bytes": int(idx.words.nbytes),
-                "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collectives",
+                "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collectives; "
+                               f"{len(batches)} host workers per GPU, each running whole steps on its own stream",
                 "grid": st["grid"], "block": st["block"],
             },
             "roofline": {
@@ -290,6 +334,7 @@ def main():
                 "traffic": traffic,
                 "kernel": "seed_kernel",
                 "kernel_ms": round(k_ms, 3),
+                "kernel_ms_source": "HIP events around seed_kernel launches running alone (warmup)",
                 "bytes_per_read": round(bpr, 1),
                 "bytes_per_read_occ64": round(bpr64, 1),
                 "achieved_occ64": round(bpr64 * reads.n / (k_ms * 1e-3) / 1e9, 2),
@@ -302,7 +347,8 @@ def main():
             "overflow_reads": st["n_overflow"],
         }
         print(json.dumps(out), flush=True)
-    batch.close()
+    for b in batches:
+        b.close()
     gpu.close()
     d.close()
 
