@@ -118,16 +118,23 @@ constexpr int LIST_LDS = 7;
 // Wave-private LDS.  img: the Occ bucket image (FETCH_OCC64: 4 planes
 // [slot*2 + chunk][lane]; FETCH_LANE: 8 planes [k0..k3, l0..l3][lane];
 // FETCH_COOP: [k|l][lane][4 chunks]).  pn / q: one 16-B landing slot per lane
-// for prev[j+1] and for the query window, filled by LDS-DMA.  list: the
-// first NLIST entries of the lane's backward interval list (curr, which
-// becomes prev), entry-major so that a wave's accesses are bank-conflict
-// free whatever entry each lane is at.
-template <int NIMG, int NLIST>
+// for prev[j+1] and for the query window, filled by LDS-DMA.  The first
+// NLIST entries of the lane's backward interval list (curr, which becomes
+// prev) live in WaveListT, entry-major so that a wave's accesses are
+// bank-conflict free whatever entry each lane is at.
+template <int NIMG>
 struct WaveLdsT {
     uint4 img[NIMG][64];
     uint4 pn[64];
     uint4 q[64];
-    uint4 list[NLIST > 0 ? NLIST : 1][64];
+};
+
+// the backward-list entries kept in LDS, per wave [entry][lane].  A separate
+// __shared__ object from the LDS-DMA targets above, so the compiler can see
+// that reading a list entry does not wait for bucket DMAs in flight.
+template <int NLIST>
+struct WaveListT {
+    uint4 e[NLIST > 0 ? NLIST : 1][64];
 };
 
 // The lane id, recomputed where it is used: the register allocator would
@@ -292,20 +299,21 @@ __device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a,
     nb = b + (uint64_t)(a <= P.primary && a + s - 1 >= P.primary) + gt;
 }
 
-// Fetch the Occ64 buckets of k and l.  Each lane keeps the two buckets it
+// Fetch the Occ64 buckets of k and l (issue: DMAs, tags; read: after the
+// wave's vmcnt wait).  Each lane keeps the two buckets it
 // fetched last in two LDS slots (planes [2*slot + chunk][lane]) with their
 // indices in t0 / t1: consecutive extends of one lane often need the same
 // bucket again (nested intervals of one backward step: 30 % of the buckets
 // on the bench workload), and those are not fetched again.  Every lane DMAs
 // its own buckets, one 16-B chunk per instruction (at most 4 instructions).
 template <class WL>
-__device__ __forceinline__ void fetch_occ64(const uint32_t* __restrict__ occ, WL* W, bool want, uint64_t kk,
-                                            uint64_t ll, uint32_t& t0, uint32_t& t1, Bucket32& vk, Bucket32& vl) {
+__device__ __forceinline__ void fetch_occ64_issue(const uint32_t* __restrict__ occ, WL* W, uint64_t kk, uint64_t ll,
+                                                  uint32_t& t0, uint32_t& t1, int& ks, int& ls) {
     const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
-    const bool needl = want && bk != bl;
-    int ks = bk == t0 ? 0 : (bk == t1 ? 1 : -1);
-    int ls = !needl ? ks : (bl == t0 ? 0 : (bl == t1 ? 1 : -1));
-    const bool kmiss = want && ks < 0, lmiss = needl && ls < 0;
+    const bool needl = bk != bl;
+    ks = bk == t0 ? 0 : (bk == t1 ? 1 : -1);
+    ls = !needl ? ks : (bl == t0 ? 0 : (bl == t1 ? 1 : -1));
+    const bool kmiss = ks < 0, lmiss = needl && ls < 0;
     if (kmiss) ks = (needl && ls == 0) ? 1 : 0;  // keep the slot l hits
     if (!needl) ls = ks;
     else if (lmiss) ls = ks ^ 1;
@@ -322,7 +330,11 @@ __device__ __forceinline__ void fetch_occ64(const uint32_t* __restrict__ occ, WL
         __builtin_amdgcn_global_load_lds(boff(occ, b1 >> 1, (b1 & 1) * 8 + 4), LDS_PTR(&W->img[3][0]), 16, 0, 0);
         t1 = b1;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// after the wait: the lane's k and l buckets from its slots
+template <class WL>
+__device__ __forceinline__ void fetch_occ64_read(WL* W, int ks, int ls, Bucket32& vk, Bucket32& vl) {
     const int lane = vlane();
     ks = ks < 0 ? 0 : ks;  // lanes without a request read a slot and ignore it
     ls = ls < 0 ? 0 : ls;
@@ -356,18 +368,20 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 // STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
-template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true>
+template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
-    using WaveLds = WaveLdsT<FETCH == FETCH_OCC64 ? 4 : 8, NL>;
+    using WaveLds = WaveLdsT<FETCH == FETCH_OCC64 ? 4 : 8>;
     __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
+    __shared__ WaveListT<NL> lists[4];
     __shared__ uint32_t scnt[STAMP ? 4 : 1][16];  // STAMP: per-wave block-execution counts
     if constexpr (STAMP) {
         if ((threadIdx.x & 63) < 16) scnt[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     }
     const int lane = threadIdx.x & 63;
     WaveLds* W = &lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    WaveListT<NL>* WLs = &lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const uint64_t lane_g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t cap = P.cap_list;
     // per-lane scratch: two packed lists (B0 | B1) used as forward / prev / curr
@@ -424,6 +438,16 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     for (;;) {
         uint64_t ta = 0;
         if constexpr (STAMP) ta = stamp();
+        // claiming the next read and loading its offsets: here, at the top of the
+        // iteration, where no bucket DMA is in flight yet for their waits to cover
+        if (phase == P_FETCH) {
+            if (nlen == -2) {  // claim the next read
+                nitem = atomicAdd(P.head, 1);
+                nlen = -1;
+            } else if (nlen == -1) {  // its offsets (the claim returned last iteration)
+                next_offsets(P, nitem, no0, nlen, nrid);
+            }
+        }
         // ---- advance the state machine until the lane needs an extend ----
         // Blocks are laid out in the order the common transitions take, and a
         // block hands over to a LATER block by setting `phase` and falling
@@ -439,6 +463,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         // iterations) continues next iteration without an extend, instead of
         // the whole wave running a second pass.
         bool out = false;
+        bool early = false;  // FETCH_OCC64: this lane's bucket fetch was issued in BWD_RES
+        int fks = -1, fls = -1;  // its bucket slots
         for (int pass = 0; phase != P_EXIT && (pass == 0 || !SINGLE); ++pass) {
             if constexpr (STAMP) {  // which blocks this pass of the wave starts in (any lane)
                 const uint64_t act = __ballot(1);
@@ -564,6 +590,74 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     }
                 }
             }
+            if (phase == P_BWD_RES) {  // software/bwt.c:815-825; na = x[0], nb = x[1]
+                // the lane's own result for prev[j], then (helped owner only) the
+                // results idle lanes computed for prev[j+1 .. j+bat_m], in order
+                const int nres = 1 + (lane == bat_o ? bat_m : 0);
+                uint64_t hm = bat_h;
+                for (int r = 0; r < nres; ++r) {
+                    if (r > 0) {
+                        const int h = __builtin_ctzll(hm);
+                        hm &= hm - 1;
+                        const uint4 ent = W->pn[h], res = W->q[h];
+                        ik0 = p_x0(ent); ik1 = p_x1(ent); ik2 = p_x2(ent); ikend = p_end(ent);
+                        na = p_x0(res); nb = p_x1(res); ns = p_x2(res);
+                    }
+                    if (ns < (uint64_t)min_intv) {
+                        // only prev[0] can be kept, when nothing longer survived
+                        if (curr_n == 0 && (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start)) {
+                            if (raw_n >= P.cap_intv) {
+                                phase = P_OVF;
+                                break;
+                            }
+                            const uint64_t info = (uint64_t)ikend | ((uint64_t)(i + 1) << 32);
+                            P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{ik0, ik1, ik2, info};
+                            // the merge keeps a sub-match if it is at least half the longest
+                            // match and ends after the call's start (software/bwamem.c:284-292)
+                            keep_n += !middle || (ikend - (uint32_t)(i + 1) >= (max_len >> 1) && ikend > (uint32_t)ori_start);
+                            ++mem_n;
+                            mem_last_start = (uint32_t)(i + 1);
+                            if (!middle && ikend - (uint32_t)(i + 1) >= max_len) {
+                                max_len = ikend - (uint32_t)(i + 1);
+                                max_x2 = ik2 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ik2;
+                                max_mid = (ikend + (uint32_t)(i + 1)) >> 1;
+                            }
+                        }
+                    } else if (curr_n == 0 || ns != curr_last_x2) {
+                        const uint4 e = pack_p(na, nb, ns, ikend);
+                        if (NL > 0 && curr_n < (uint32_t)NL)
+                            WLs->e[curr_n][vlane()] = e;
+                        else
+                            *reinterpret_cast<uint4*>(bp + cap + curr_n) = e;
+                        if (curr_n == 0) head = e;  // prev[0] of the next step
+                        ++curr_n;
+                        curr_last_x2 = ns;
+                    }
+                    ++j;
+                }
+                if (phase == P_BWD_RES) {
+                    if ((uint32_t)j < prev_n) {  // extend prev[j] (read into pn last iteration) right away
+                        ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
+                        out = true;
+                        if constexpr (FETCH == FETCH_OCC64 && EARLY) {
+                            // issue its bucket fetch now: it overlaps the rest of the pass
+                            const uint64_t k = ik0 - 1, l = k + ik2;
+                            fetch_occ64_issue(P.occ64, W, k - (k >= P.primary), l - (l >= P.primary), tag0, tag1,
+                                              fks, fls);
+                            early = true;
+                        }
+                    } else if (curr_n == 0) {  // software/bwt.c:827
+                        phase = P_SMEM_END;
+                    } else {
+                        prev_off = cap;  // software/bwt.c:828: swap, next position
+                        prev_n = curr_n;
+                        prev_lds = true;
+                        pn = head;
+                        --i;
+                        phase = P_BWD_STEP;
+                    }
+                }
+            }
             if (phase == P_FWD_RES) {  // software/bwt.c:795-799; na = x[1], nb = x[0]
                 bool stop = false;
                 if (ns != ik2) {
@@ -614,67 +708,6 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 prev_lds = false;
                 i = x - 1;
                 phase = P_BWD_STEP;
-            }
-            if (phase == P_BWD_RES) {  // software/bwt.c:815-825; na = x[0], nb = x[1]
-                // the lane's own result for prev[j], then (helped owner only) the
-                // results idle lanes computed for prev[j+1 .. j+bat_m], in order
-                const int nres = 1 + (lane == bat_o ? bat_m : 0);
-                uint64_t hm = bat_h;
-                for (int r = 0; r < nres; ++r) {
-                    if (r > 0) {
-                        const int h = __builtin_ctzll(hm);
-                        hm &= hm - 1;
-                        const uint4 ent = W->pn[h], res = W->q[h];
-                        ik0 = p_x0(ent); ik1 = p_x1(ent); ik2 = p_x2(ent); ikend = p_end(ent);
-                        na = p_x0(res); nb = p_x1(res); ns = p_x2(res);
-                    }
-                    if (ns < (uint64_t)min_intv) {
-                        // only prev[0] can be kept, when nothing longer survived
-                        if (curr_n == 0 && (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start)) {
-                            if (raw_n >= P.cap_intv) {
-                                phase = P_OVF;
-                                break;
-                            }
-                            const uint64_t info = (uint64_t)ikend | ((uint64_t)(i + 1) << 32);
-                            P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{ik0, ik1, ik2, info};
-                            // the merge keeps a sub-match if it is at least half the longest
-                            // match and ends after the call's start (software/bwamem.c:284-292)
-                            keep_n += !middle || (ikend - (uint32_t)(i + 1) >= (max_len >> 1) && ikend > (uint32_t)ori_start);
-                            ++mem_n;
-                            mem_last_start = (uint32_t)(i + 1);
-                            if (!middle && ikend - (uint32_t)(i + 1) >= max_len) {
-                                max_len = ikend - (uint32_t)(i + 1);
-                                max_x2 = ik2 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ik2;
-                                max_mid = (ikend + (uint32_t)(i + 1)) >> 1;
-                            }
-                        }
-                    } else if (curr_n == 0 || ns != curr_last_x2) {
-                        const uint4 e = pack_p(na, nb, ns, ikend);
-                        if (NL > 0 && curr_n < (uint32_t)NL)
-                            W->list[curr_n][vlane()] = e;
-                        else
-                            *reinterpret_cast<uint4*>(bp + cap + curr_n) = e;
-                        if (curr_n == 0) head = e;  // prev[0] of the next step
-                        ++curr_n;
-                        curr_last_x2 = ns;
-                    }
-                    ++j;
-                }
-                if (phase == P_BWD_RES) {
-                    if ((uint32_t)j < prev_n) {  // extend prev[j] (read into pn last iteration) right away
-                        ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
-                        out = true;
-                    } else if (curr_n == 0) {  // software/bwt.c:827
-                        phase = P_SMEM_END;
-                    } else {
-                        prev_off = cap;  // software/bwt.c:828: swap, next position
-                        prev_n = curr_n;
-                        prev_lds = true;
-                        pn = head;
-                        --i;
-                        phase = P_BWD_STEP;
-                    }
-                }
             }
             if (phase == P_BWD_STEP) {  // software/bwt.c:810-812; prev[0] is in pn
                 if (i >= 0 && QBLK(i) != qb) {
@@ -730,14 +763,6 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             st_active += __popcll(__ballot(want));
         }
         if (!__any(live)) break;
-        if (phase == P_FETCH) {
-            if (nlen == -2) {  // claim the next read
-                nitem = atomicAdd(P.head, 1);
-                nlen = -1;
-            } else if (nlen == -1) {  // its offsets (the claim returned last iteration)
-                next_offsets(P, nitem, no0, nlen, nrid);
-            }
-        }
         // Lanes that found the work queue empty help: when the wave has idle
         // lanes and a lane in a backward step with more entries left, each idle
         // lane extends one of those entries (same base, independent of each
@@ -769,7 +794,16 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         const uint32_t e = jo + 1 + r;
                         const PIntv* obp = reinterpret_cast<const PIntv*>(
                             P.scratch + ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + o) * 2ull * cap);
-                        hent = (NL > 0 && plds && e < (uint32_t)NL) ? W->list[e][o] : load_p(obp + poff + e);
+                        if (NL > 0 && plds && e < (uint32_t)NL) {
+                            hent = WLs->e[e][o];
+                        } else {
+                            // the entry into this (idle) lane's pn slot by LDS-DMA: no
+                            // VGPR-destination load whose wait would also cover the
+                            // bucket DMAs issued early in BWD_RES on the main path
+                            __builtin_amdgcn_global_load_lds(obp + poff + e, LDS_PTR(&W->pn[0]), 16, 0, 0);
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            hent = W->pn[me];
+                        }
                         hc = co;
                     }
                     bat_o = o;
@@ -801,13 +835,17 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
         Bucket vk, vl;
         Bucket32 wk, wl;
-        if constexpr (FETCH == FETCH_OCC64)
-            fetch_occ64(P.occ64, W, want, kk, ll, tag0, tag1, wk, wl);  // ends with vmcnt(0)
-        else
+        if constexpr (FETCH == FETCH_OCC64) {
+            // lanes whose fetch was not issued early in BWD_RES issue it now
+            if (want && !early) fetch_occ64_issue(P.occ64, W, kk, ll, tag0, tag1, fks, fls);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            fetch_occ64_read(W, fks, fls, wk, wl);
+        } else {
             fetch_buckets<FETCH>(P.bwt, W, want, kk, ll, vk, vl);  // ends with vmcnt(0)
+        }
         if (ld_pn) pn = W->pn[vlane()];
         if constexpr (NL > 0) {  // prev[pidx] from the LDS list: read here, off the advance's critical path
-            if (phase == P_BWD_RES && prev_lds && pidx < prev_n && pidx < (uint32_t)NL) pn = W->list[pidx][vlane()];
+            if (phase == P_BWD_RES && prev_lds && pidx < prev_n && pidx < (uint32_t)NL) pn = WLs->e[pidx][vlane()];
         }
         if (ld_q) {
             qv = W->q[vlane()];
@@ -928,13 +966,14 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
         // LDS at 2 blocks per CU; 6: Occ64, lists in global memory; 7: the
-        // default with several advance passes per iteration; 9: the default
-        // with cycle stamps
+        // default with the bucket fetch of BWD_RES lanes issued inside the
+        // advance (no gain measured: the fetch is throughput-bound); 8: 4 blocks per CU
+        // with 4 list entries in LDS; 9: the default with cycle stamps
         case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 4: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 5: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12>), dim3(grid), dim3(block), 0, st, *P); break;
         case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, false>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 8: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
         default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
