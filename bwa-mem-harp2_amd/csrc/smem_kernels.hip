@@ -421,10 +421,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     uint64_t na = 0, nb = 0, ns = 0;
     uint32_t tag0 = ~0u, tag1 = ~0u;  // FETCH_OCC64: buckets held in the lane's two LDS slots
     // wave-cooperative backward step (tail of the batch): idle lanes extend
-    // entries of one owner lane's prev list; wave-uniform descriptor of the
-    // batch handed to the owner's next BWD_RES
-    int bat_o = -1, bat_m = 0;
-    uint64_t bat_h = 0;
+    // entries of owner lanes' prev lists
+    int bat_m = 0;        // this lane's helped entries for its next BWD_RES (owner only)
+    uint64_t bat_h = 0;   // the lanes that computed them, in entry order
     uint64_t st_adv = 0, st_fetch = 0, st_comp = 0, st_iter = 0, st_active = 0, st_t0 = 0, st_t1 = 0;
     if constexpr (STAMP) st_t0 = rtstamp();
 
@@ -593,7 +592,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (phase == P_BWD_RES) {  // software/bwt.c:815-825; na = x[0], nb = x[1]
                 // the lane's own result for prev[j], then (helped owner only) the
                 // results idle lanes computed for prev[j+1 .. j+bat_m], in order
-                const int nres = 1 + (lane == bat_o ? bat_m : 0);
+                const int nres = 1 + bat_m;
                 uint64_t hm = bat_h;
                 for (int r = 0; r < nres; ++r) {
                     if (r > 0) {
@@ -769,7 +768,6 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         // other, software/bwt.c:812-826) and leaves entry + result in its pn / q
         // slots; the owner consumes them in order next iteration.  This cuts the
         // dependent chain of the few repeat-rich reads left at the end.
-        bat_o = -1;
         bat_m = 0;
         bat_h = 0;
         bool helper = false;
@@ -778,44 +776,62 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         if constexpr (FETCH == FETCH_OCC64) {
             const uint64_t idle = __ballot(phase == P_EXIT);
             if (idle) {
-                const uint64_t elig = __ballot(phase == P_BWD_RES && (uint32_t)j + 1 < prev_n);
-                if (elig) {
+                // owners in lane order take the idle lanes in rank order, each as
+                // many as it has entries left in its step
+                uint64_t elig = __ballot(phase == P_BWD_RES && (uint32_t)j + 1 < prev_n);
+                const uint32_t nidle = (uint32_t)__popcll(idle);
+                const int me = vlane();
+                const uint32_t r = (uint32_t)__popcll(idle & ((1ull << me) - 1));
+                uint32_t base = 0, he = 0, hpoff = 0;
+                int ho = -1, hplds = 0;
+                while (elig && base < nidle) {
+                    // o is wave-uniform: its state is read with v_readlane (valid
+                    // whatever the exec mask, unlike a shuffle from an inactive lane)
                     const int o = __builtin_ctzll(elig);
+                    elig &= elig - 1;
                     const uint32_t jo = __builtin_amdgcn_readlane((int)j, o);
                     const uint32_t pno = __builtin_amdgcn_readlane((int)prev_n, o);
-                    const uint32_t poff = __builtin_amdgcn_readlane((int)prev_off, o);
-                    const int plds = __builtin_amdgcn_readlane((int)prev_lds, o);
-                    const int co = __builtin_amdgcn_readlane(cur_c, o);
-                    const uint32_t m = min((uint32_t)__popcll(idle), pno - jo - 1);
-                    const int me = vlane();
-                    const uint32_t r = (uint32_t)__popcll(idle & ((1ull << me) - 1));
-                    helper = phase == P_EXIT && r < m;
-                    if (helper) {
-                        const uint32_t e = jo + 1 + r;
-                        const PIntv* obp = reinterpret_cast<const PIntv*>(
-                            P.scratch + ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + o) * 2ull * cap);
-                        if (NL > 0 && plds && e < (uint32_t)NL) {
-                            hent = WLs->e[e][o];
-                        } else {
-                            // the entry into this (idle) lane's pn slot by LDS-DMA: no
-                            // VGPR-destination load whose wait would also cover the
-                            // bucket DMAs issued early in BWD_RES on the main path
-                            __builtin_amdgcn_global_load_lds(obp + poff + e, LDS_PTR(&W->pn[0]), 16, 0, 0);
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            hent = W->pn[me];
-                        }
-                        hc = co;
+                    const uint32_t poff_o = __builtin_amdgcn_readlane((int)prev_off, o);
+                    const int plds_o = __builtin_amdgcn_readlane((int)prev_lds, o);
+                    const int c_o = __builtin_amdgcn_readlane(cur_c, o);
+                    const uint32_t m = min(nidle - base, pno - jo - 1);
+                    const bool mine = phase == P_EXIT && r >= base && r < base + m;
+                    if (mine) {
+                        ho = o;
+                        he = jo + 1 + (r - base);
+                        hc = c_o;
+                        hpoff = poff_o;
+                        hplds = plds_o;
                     }
-                    bat_o = o;
-                    bat_m = (int)m;
-                    bat_h = __ballot(helper);
+                    const uint64_t hmask = __ballot(mine);
+                    if (me == o) {
+                        bat_m = (int)m;
+                        bat_h = hmask;
+                    }
+                    base += m;
+                }
+                helper = ho >= 0;
+                if (helper) {
+                    // the owner's list: its first NL entries in LDS (after the first
+                    // step), the rest in its arena; prev_off / prev_lds are per owner
+                    if (NL > 0 && hplds && he < (uint32_t)NL) {
+                        hent = WLs->e[he][ho];
+                    } else {
+                        const PIntv* obp = reinterpret_cast<const PIntv*>(
+                            P.scratch + ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + ho) * 2ull * cap);
+                        // the entry into this (idle) lane's pn slot by LDS-DMA: no
+                        // VGPR-destination load on the main path
+                        __builtin_amdgcn_global_load_lds(obp + hpoff + he, LDS_PTR(&W->pn[0]), 16, 0, 0);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        hent = W->pn[me];
+                    }
                 }
             }
         }
         // prev[j+1] (the owner of a helped batch: prev[j+1+bat_m]) and the query
         // window land in LDS slots (no VGPR-destination load the compiler would
         // wait on right away); read back after the wait
-        const uint32_t pidx = (uint32_t)j + 1 + (lane == bat_o ? (uint32_t)bat_m : 0u);
+        const uint32_t pidx = (uint32_t)j + 1 + (uint32_t)bat_m;
         const bool ld_pn = phase == P_BWD_RES && pidx < prev_n && !(NL > 0 && prev_lds && pidx < (uint32_t)NL);
         const bool ld_q = qwant != qb && qwant != ~0u;
         if (ld_pn)
