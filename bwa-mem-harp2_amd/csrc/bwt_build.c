@@ -144,7 +144,7 @@ static int sais_core(const text_t *t, uint32_t *SA, uint32_t n, uint32_t K)
 
 /* --------------------------------------------------------- public API */
 
-int smem_bwt_build(const uint8_t *fwd, uint64_t n_fwd, smem_index_t *idx)
+static int build_core(const uint8_t *fwd, uint64_t n_fwd, int sa_intv, smem_index_t *idx, smem_sa_t *sa_out)
 {
 	uint64_t n, i, j, k, n_occ, c[4];
 	uint8_t *text;
@@ -169,6 +169,20 @@ int smem_bwt_build(const uint8_t *fwd, uint64_t n_fwd, smem_index_t *idx)
 		if (sais_core(&t, SA, (uint32_t)(n + 1), 5)) { free(text); free(SA); return SMEM_E_NOMEM; }
 	}
 	/* SA[0] is the sentinel suffix; rows 0..n of the BWT matrix */
+	if (sa_out) {
+		/* sampled SA as bwt_cal_sa leaves it (software/bwt.c:80-102):
+		 * sa[r] = SA[r * intv], sa[0] = -1 */
+		memset(sa_out, 0, sizeof(*sa_out));
+		sa_out->sa_intv = (uint64_t)sa_intv;
+		sa_out->seq_len = n;
+		sa_out->n_sa = (n + (uint64_t)sa_intv) / (uint64_t)sa_intv;
+		sa_out->sa = (uint64_t*)malloc(8 * (sa_out->n_sa + 1));
+		if (!sa_out->sa) { free(text); free(SA); return SMEM_E_NOMEM; }
+		for (i = 0; i < sa_out->n_sa; ++i) sa_out->sa[i] = SA[i * (uint64_t)sa_intv];
+		sa_out->sa[0] = (uint64_t)-1;
+		sa_out->sa[sa_out->n_sa] = 0;  /* pad: 16-B loads of the last sample stay in bounds */
+		sa_out->owns = 1;
+	}
 	memset(idx->L2, 0, sizeof(idx->L2));
 	for (i = 0; i < n; ++i) idx->L2[text[i]]++;      /* text[i] in 1..4 -> L2[1..4] counts */
 	for (i = 2; i <= 4; ++i) idx->L2[i] += idx->L2[i - 1];
@@ -201,7 +215,71 @@ int smem_bwt_build(const uint8_t *fwd, uint64_t n_fwd, smem_index_t *idx)
 	idx->primary = primary;
 	idx->seq_len = n;
 	idx->owns = 1;
+	if (sa_out) {
+		sa_out->primary = primary;
+		memcpy(sa_out->L2, idx->L2, sizeof(idx->L2));
+	}
 	return SMEM_OK;
+}
+
+int smem_bwt_build(const uint8_t *fwd, uint64_t n_fwd, smem_index_t *idx)
+{
+	return build_core(fwd, n_fwd, 0, idx, 0);
+}
+
+int smem_bwt_build_sa(const uint8_t *fwd, uint64_t n_fwd, int sa_intv, smem_index_t *idx, smem_sa_t *sa)
+{
+	int rc;
+	if (!sa || sa_intv <= 0 || (sa_intv & (sa_intv - 1))) return SMEM_E_ARG;  /* power of 2 (software/bwt.c:87) */
+	rc = build_core(fwd, n_fwd, sa_intv, idx, sa);
+	if (rc != SMEM_OK) smem_sa_free(sa);
+	return rc;
+}
+
+/* .sa file (software/bwt.c:852-863 / 877-897): primary, L2[1..4], sa_intv,
+ * seq_len, then sa[1 .. n_sa-1] */
+int smem_sa_write(const char *fn, const smem_sa_t *sa)
+{
+	FILE *fp;
+	if (!sa || !sa->sa || sa->n_sa == 0) return SMEM_E_ARG;
+	fp = fopen(fn, "wb");
+	if (!fp) return SMEM_E_IO;
+	if (fwrite(&sa->primary, 8, 1, fp) != 1 || fwrite(sa->L2 + 1, 8, 4, fp) != 4 || fwrite(&sa->sa_intv, 8, 1, fp) != 1
+			|| fwrite(&sa->seq_len, 8, 1, fp) != 1 || fwrite(sa->sa + 1, 8, sa->n_sa - 1, fp) != sa->n_sa - 1) {
+		fclose(fp);
+		return SMEM_E_IO;
+	}
+	return fclose(fp) == 0 ? SMEM_OK : SMEM_E_IO;
+}
+
+int smem_sa_read(const char *fn, smem_sa_t *sa)
+{
+	FILE *fp;
+	if (!sa) return SMEM_E_ARG;
+	memset(sa, 0, sizeof(*sa));
+	fp = fopen(fn, "rb");
+	if (!fp) return SMEM_E_IO;
+	if (fread(&sa->primary, 8, 1, fp) != 1 || fread(sa->L2 + 1, 8, 4, fp) != 4 || fread(&sa->sa_intv, 8, 1, fp) != 1
+			|| fread(&sa->seq_len, 8, 1, fp) != 1 || sa->sa_intv == 0) {
+		fclose(fp);
+		return SMEM_E_IO;
+	}
+	sa->n_sa = (sa->seq_len + sa->sa_intv) / sa->sa_intv;
+	sa->sa = (uint64_t*)malloc(8 * (sa->n_sa + 1));
+	if (!sa->sa) { fclose(fp); return SMEM_E_NOMEM; }
+	sa->sa[0] = (uint64_t)-1;
+	sa->sa[sa->n_sa] = 0;
+	if (fread(sa->sa + 1, 8, sa->n_sa - 1, fp) != sa->n_sa - 1) { fclose(fp); free(sa->sa); sa->sa = 0; return SMEM_E_IO; }
+	fclose(fp);
+	sa->owns = 1;
+	return SMEM_OK;
+}
+
+void smem_sa_free(smem_sa_t *sa)
+{
+	if (!sa) return;
+	if (sa->owns) free(sa->sa);
+	memset(sa, 0, sizeof(*sa));
 }
 
 int smem_bwt_write(const char *fn, const smem_index_t *idx)

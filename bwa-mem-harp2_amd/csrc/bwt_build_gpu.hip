@@ -145,7 +145,14 @@ struct Buf {
 
 static inline unsigned blocks(uint64_t n, unsigned t = 256) { return (unsigned)((n + t - 1) / t); }
 
-extern "C" int smem_bwt_build_gpu(int device, const uint8_t* fwd, uint64_t n_fwd, smem_index_t* idx) {
+// sampled SA (software/bwt.c:80-102): row r holds SA = (r == 0 ? n : sa[r-1]);
+// samples at rows i * intv, i >= 1 (sa[0] = -1 is set on the host)
+__global__ void sample_sa(const uint32_t* __restrict__ sa, uint64_t n_sa, uint64_t intv, uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (i < n_sa) out[i] = sa[i * intv - 1];
+}
+
+static int build_gpu(int device, const uint8_t* fwd, uint64_t n_fwd, int sa_intv, smem_index_t* idx, smem_sa_t* sa_out) {
     if (!fwd || !idx || n_fwd == 0) return SMEM_E_ARG;
     const uint64_t n = 2 * n_fwd;
     if (n + 1 >= 0xFFFFFFFEull) return SMEM_E_ARG;
@@ -215,6 +222,23 @@ extern "C" int smem_bwt_build_gpu(int device, const uint8_t* fwd, uint64_t n_fwd
         key_bits = 64;
     }
     const uint32_t* sa = vals.Current();
+    if (sa_out) {
+        const uint64_t intv = (uint64_t)sa_intv, n_sa = (n + intv) / intv;
+        Buf bS;
+        GB_TRY(hipMalloc(&bS.p, 8 * (n_sa + 1)));
+        GB_TRY(hipMemsetAsync(bS.p, 0, 8 * (n_sa + 1), st));
+        if (n_sa > 1) sample_sa<<<blocks(n_sa - 1), 256, 0, st>>>(sa, n_sa, intv, (uint64_t*)bS.p);
+        memset(sa_out, 0, sizeof(*sa_out));
+        sa_out->sa = (uint64_t*)malloc(8 * (n_sa + 1));
+        if (!sa_out->sa) return SMEM_E_NOMEM;
+        sa_out->owns = 1;
+        GB_TRY(hipMemcpyAsync(sa_out->sa, bS.p, 8 * (n_sa + 1), hipMemcpyDeviceToHost, st));
+        GB_TRY(hipStreamSynchronize(st));
+        sa_out->sa[0] = (uint64_t)-1;
+        sa_out->sa_intv = intv;
+        sa_out->n_sa = n_sa;
+        sa_out->seq_len = n;
+    }
     // primary = 1 + position of suffix 0 = rank[0] (rank = position + 1)
     uint32_t r0 = 0;
     GB_TRY(hipMemcpyAsync(&r0, rank, 4, hipMemcpyDeviceToHost, st));
@@ -265,5 +289,24 @@ extern "C" int smem_bwt_build_gpu(int device, const uint8_t* fwd, uint64_t n_fwd
         memset(idx, 0, sizeof(*idx));
         return SMEM_E_INTERNAL;
     }
+    if (sa_out) {
+        sa_out->primary = primary;
+        memcpy(sa_out->L2, idx->L2, sizeof(idx->L2));
+    }
     return SMEM_OK;
+}
+
+extern "C" int smem_bwt_build_gpu(int device, const uint8_t* fwd, uint64_t n_fwd, smem_index_t* idx) {
+    return build_gpu(device, fwd, n_fwd, 0, idx, nullptr);
+}
+
+extern "C" int smem_bwt_build_gpu_sa(int device, const uint8_t* fwd, uint64_t n_fwd, int sa_intv, smem_index_t* idx,
+                                     smem_sa_t* sa) {
+    if (!sa || sa_intv <= 0 || (sa_intv & (sa_intv - 1))) return SMEM_E_ARG;
+    const int rc = build_gpu(device, fwd, n_fwd, sa_intv, idx, sa);
+    if (rc != SMEM_OK) {
+        smem_sa_free(sa);
+        smem_index_free(idx);
+    }
+    return rc;
 }

@@ -97,6 +97,9 @@ struct smem_gpu {
     int variant = 2;  // see smem_gpu_set_kernel_variant
     uint32_t* d_bwt = nullptr;      // reference layout (variants 3, 4)
     uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
+    uint64_t* d_sa = nullptr;       // sampled SA (smem_gpu_load_sa), n_sa + 1 words
+    uint64_t n_sa = 0;
+    uint32_t sa_shift = 0;
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
     std::mutex mu;
     std::unordered_map<std::thread::id, smem_batch_t*> per_thread;
@@ -142,6 +145,12 @@ struct smem_batch {
     HostBuf<uint64_t> h_intv_off, h_call_off;
     bool fetched = false, ran = false;
     uint64_t tot_intv = 0, tot_calls = 0;
+    // bwt_sa of the seed occurrences (smem_batch_sa)
+    DevBuf<uint64_t> d_occ_n, d_occ_off, d_sa_pos;
+    DevBuf<uint8_t> d_sa_tmp;
+    HostBuf<uint64_t> h_occ_off, h_sa_pos;
+    bool sa_ran = false, sa_fetched = false;
+    uint64_t tot_occ = 0;
     smem_batch_stats_t stats{};
 };
 
@@ -248,6 +257,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_scratch.release(); b->d_dbg.release(); b->d_ovf_intv.release(); b->d_ovf_call.release(); b->d_ovf_n_intv.release();
     b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
     b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
+    b->d_occ_n.release(); b->d_occ_off.release(); b->d_sa_pos.release(); b->d_sa_tmp.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
     b->h_intv_off.release(); b->h_call_off.release();
     for (auto& ev : b->ev)
@@ -263,6 +273,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     g->per_thread.clear();
     if (g->d_bwt) (void)hipFree(g->d_bwt);
     if (g->d_occ64) (void)hipFree(g->d_occ64);
+    if (g->d_sa) (void)hipFree(g->d_sa);
     delete g;
 }
 
@@ -398,6 +409,9 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     HIP_TRY(hipSetDevice(g->device));
     const int n = b->n_reads;
     b->fetched = false;
+    b->sa_ran = false;
+    b->sa_fetched = false;
+    b->tot_occ = 0;
     b->stats = smem_batch_stats_t{};
     b->stats.block = 256;
     smem::SeedParams P;
@@ -532,8 +546,99 @@ int smem_batch_fetch(smem_batch_t* b) {
         HIP_TRY(hipMemcpyAsync(b->h_intv.p, b->d_flat_intv.p, sizeof(Intv) * b->tot_intv, hipMemcpyDeviceToHost, b->st));
     if (b->tot_calls)
         HIP_TRY(hipMemcpyAsync(b->h_calls.p, b->d_flat_calls.p, sizeof(uint32_t) * b->tot_calls, hipMemcpyDeviceToHost, b->st));
+    if (b->sa_ran) {
+        HIP_TRY(b->h_occ_off.ensure(b->tot_intv + 1));
+        HIP_TRY(b->h_sa_pos.ensure(std::max<uint64_t>(b->tot_occ, 1)));
+        HIP_TRY(hipMemcpyAsync(b->h_occ_off.p, b->d_occ_off.p, sizeof(uint64_t) * (b->tot_intv + 1),
+                               hipMemcpyDeviceToHost, b->st));
+        if (b->tot_occ)
+            HIP_TRY(hipMemcpyAsync(b->h_sa_pos.p, b->d_sa_pos.p, sizeof(uint64_t) * b->tot_occ, hipMemcpyDeviceToHost,
+                                   b->st));
+    }
     HIP_TRY(hipStreamSynchronize(b->st));
     b->fetched = true;
+    b->sa_fetched = b->sa_ran;
+    return SMEM_OK;
+}
+
+int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
+    g_err[0] = 0;
+    if (!g || !sa || !sa->sa || sa->n_sa == 0 || sa->sa_intv == 0 || (sa->sa_intv & (sa->sa_intv - 1)))
+        return fail(SMEM_E_ARG, "smem_gpu_load_sa: bad SA");
+    if (sa->seq_len != g->L2[4] || sa->n_sa != (sa->seq_len + sa->sa_intv) / sa->sa_intv)
+        return fail(SMEM_E_ARG, "smem_gpu_load_sa: SA does not belong to this index (seq_len)");
+    if (sa->primary != g->primary) return fail(SMEM_E_ARG, "smem_gpu_load_sa: SA does not belong to this index (primary)");
+    HIP_TRY(hipSetDevice(g->device));
+    if (g->d_sa) {
+        (void)hipFree(g->d_sa);
+        g->d_sa = nullptr;
+    }
+    // n_sa + 1 words: the zero pad of smem_sa_t (a 16-B load of the last sample stays in bounds)
+    hipError_t e = hipMalloc(&g->d_sa, (sa->n_sa + 1) * sizeof(uint64_t));
+    if (e != hipSuccess) return fail(SMEM_E_NOMEM, "smem_gpu_load_sa: hipMalloc", e);
+    e = hipMemcpy(g->d_sa, sa->sa, sa->n_sa * sizeof(uint64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(g->d_sa + sa->n_sa, 0, sizeof(uint64_t));
+    if (e != hipSuccess) return fail(SMEM_E_DEVICE, "smem_gpu_load_sa: upload", e);
+    g->n_sa = sa->n_sa;
+    g->sa_shift = (uint32_t)__builtin_ctzll(sa->sa_intv);
+    return SMEM_OK;
+}
+
+int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
+    g_err[0] = 0;
+    if (!b || !b->ran) return fail(SMEM_E_ARG, "smem_batch_sa: batch has not run");
+    smem_gpu_t* g = b->g;
+    if (!g->d_sa) return fail(SMEM_E_ARG, "smem_batch_sa: no SA loaded (smem_gpu_load_sa)");
+    if (max_occ < 0) return fail(SMEM_E_ARG, "smem_batch_sa: max_occ");
+    HIP_TRY(hipSetDevice(g->device));
+    const uint64_t ni = b->tot_intv;
+    if (ni >= (1ull << 31)) return fail(SMEM_E_CAPACITY, "smem_batch_sa: too many intervals");
+    HIP_TRY(b->d_occ_n.ensure(ni));
+    HIP_TRY(b->d_occ_off.ensure(ni + 1));
+    size_t tmp = 0;
+    HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)std::max<uint64_t>(ni, 1), nullptr, &tmp, b->st));
+    HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
+    smem::SaParams S;
+    std::memset(&S, 0, sizeof(S));
+    S.occ64 = g->d_occ64;
+    S.primary = g->primary;
+    std::memcpy(S.L2, g->L2, sizeof(S.L2));
+    S.sa = g->d_sa;
+    S.sa_shift = g->sa_shift;
+    S.intv = b->d_flat_intv.p;
+    S.n_intv = ni;
+    S.min_seed_len = min_seed_len;
+    S.max_occ = (uint64_t)max_occ;
+    S.n_occ_intv = b->d_occ_n.p;
+    S.occ_off = b->d_occ_off.p;
+    HIP_TRY(hipEventRecord(b->ev[0], b->st));
+    HIP_TRY(smem_launch_sa_count(&S, b->st));
+    tmp = b->d_sa_tmp.n;
+    HIP_TRY(smem_launch_offsets(b->d_occ_n.p, b->d_occ_off.p, (int)ni, b->d_sa_tmp.p, &tmp, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_tot.p + 2, b->d_occ_off.p + ni, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    b->tot_occ = b->h_tot.p[2];
+    HIP_TRY(b->d_sa_pos.ensure(std::max<uint64_t>(b->tot_occ, 1)));
+    S.n_occ = b->tot_occ;
+    S.pos = b->d_sa_pos.p;
+    const int grid = std::max(1, (int)std::min<uint64_t>((uint64_t)g->n_cu * 8, (b->tot_occ + 255) / 256));
+    HIP_TRY(smem_launch_sa_walk(&S, grid, b->st));
+    HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
+    b->stats.sa_ms = ms;
+    b->stats.n_occ = b->tot_occ;
+    b->sa_ran = true;
+    b->sa_fetched = false;
+    return SMEM_OK;
+}
+
+int smem_batch_sa_results(const smem_batch_t* b, const uint64_t** pos, const uint64_t** occ_off, uint64_t* n_occ) {
+    if (!b || !b->sa_fetched) return SMEM_E_ARG;
+    if (pos) *pos = b->h_sa_pos.p;
+    if (occ_off) *occ_off = b->h_occ_off.p;
+    if (n_occ) *n_occ = b->tot_occ;
     return SMEM_OK;
 }
 

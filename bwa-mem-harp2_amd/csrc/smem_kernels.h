@@ -47,6 +47,23 @@ struct SeedParams {
     uint64_t* dbg_buf;         // stamped diagnostic variant: 8 x u64 per wave
 };
 
+// bwt_sa over the seeding output (software/bwamem.c:462-474, software/bwt.c:104-114)
+struct SaParams {
+    const uint32_t* occ64;
+    uint64_t primary;
+    uint64_t L2[5];
+    const uint64_t* sa;        // sampled SA, sa[0] = -1
+    uint32_t sa_shift;         // log2(sa_intv)
+    const Intv* intv;          // flat smem_next2 intervals
+    uint64_t n_intv;
+    const uint64_t* occ_off;   // [n_intv + 1] exclusive prefix of occurrences per interval
+    uint64_t n_occ;
+    int min_seed_len;
+    uint64_t max_occ;
+    uint64_t* n_occ_intv;      // [n_intv] occurrences per interval (count kernel output)
+    uint64_t* pos;             // [n_occ] bwt_sa results
+};
+
 // raw logs -> final smem_next2 lists (reverse + ordered merge, software/bwamem.c:280-301)
 struct FinalizeParams {
     int n;
@@ -79,6 +96,8 @@ hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32
 hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int write, hipStream_t st);
 hipError_t smem_launch_fill_i32(int32_t* p, int32_t v, int n, hipStream_t st);
 hipError_t smem_launch_ovf_slot(const int32_t* items, int n_ovf, int32_t* ovf_slot, hipStream_t st);
+hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t st);
+hipError_t smem_launch_sa_walk(const smem::SaParams* S, int grid, hipStream_t st);
 hipError_t smem_launch_offsets(const uint64_t* in, uint64_t* out, int n, void* temp, size_t* temp_bytes,
                                hipStream_t st);
 }

@@ -1062,3 +1062,93 @@ extern "C" hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buck
     hipLaunchKernelGGL(smem::occ64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, bwt, n_ref_buckets, out);
     return hipGetLastError();
 }
+
+// ------------------------------------------------------------------ bwt_sa
+// The SA lookup mem_insert_seed() does for every seed occurrence
+// (software/bwamem.c:462-474): for each interval of the smem_next2 lists
+// with seed length >= k and x2 <= max_occ, bwt_sa(bwt, x0 + j), j < x2
+// (software/bwt.c:104-114): LF steps (bwt_invPsi, software/bwt.c:71-77)
+// until the row is a multiple of sa_intv, then the sampled SA.  Each LF step
+// is one rank in one Occ64 bucket: the symbol at the row and its count are in
+// the same 32 B.
+namespace smem {
+
+
+// occurrences of each interval (software/bwamem.c:467)
+__global__ __launch_bounds__(256) void sa_count_kernel(SaParams S) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= S.n_intv) return;
+    const Intv v = S.intv[t];
+    const int slen = (int)((uint32_t)v.info - (uint32_t)(v.info >> 32));
+    S.n_occ_intv[t] = (slen < S.min_seed_len || v.x2 > S.max_occ) ? 0 : v.x2;
+}
+
+// bwt_invPsi on the Occ64 layout
+__device__ __forceinline__ uint64_t inv_psi64(const SaParams& S, uint64_t k) {
+    if (k == S.primary) return 0;
+    const uint64_t kk = k - (k > S.primary);
+    const uint4* b = reinterpret_cast<const uint4*>(S.occ64) + (kk >> 6) * 2;
+    const uint4 cnt = b[0], sym = b[1];
+    const uint32_t pos = (uint32_t)(kk & 63);
+    const uint32_t sel = pos >> 4;
+    const uint32_t w = sel == 0 ? sym.x : (sel == 1 ? sym.y : (sel == 2 ? sym.z : sym.w));
+    const int c = (int)((w >> ((~pos & 15u) << 1)) & 3u);
+    uint32_t C, G, T;
+    count_cgt4(sym, pos, C, G, T);
+    const uint64_t oc = occ_cgt(cnt, 0) + C, og = occ_cgt(cnt, 1) + G, ot = occ_cgt(cnt, 2) + T;
+    const uint64_t occ = c == 0 ? kk + 1 - oc - og - ot : (c == 1 ? oc : (c == 2 ? og : ot));
+    return sel4(c, S.L2[0], S.L2[1], S.L2[2], S.L2[3]) + occ;
+}
+
+// One lane per occurrence, occurrences dealt lane-strided; the row of
+// occurrence o is x0 + (o - occ_off[t]) of the interval t that holds it
+// (binary search over occ_off, once per occurrence).  Lanes of a wave walk
+// different numbers of LF steps (0 .. sa_intv-1): a lane that finishes takes
+// its next occurrence in the same loop, so the wave stays full.
+__global__ __launch_bounds__(256) void sa_walk_kernel(SaParams S) {
+    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t mask = (1ull << S.sa_shift) - 1;
+    uint64_t k = 0, steps = 0;
+    bool live = false;
+    auto start = [&](uint64_t occ) {
+        uint64_t lo = 0, hi = S.n_intv;  // largest t with occ_off[t] <= occ
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (S.occ_off[mid] <= occ) lo = mid; else hi = mid;
+        }
+        k = S.intv[lo].x0 + (occ - S.occ_off[lo]);
+        steps = 0;
+    };
+    if (o < S.n_occ) {
+        start(o);
+        live = true;
+    }
+    while (__any(live)) {
+        if (live) {
+            if (k & mask) {
+                k = inv_psi64(S, k);
+                ++steps;
+            } else {
+                // sa[0] = -1: unsigned wrap as in software/bwt.c:110-113
+                S.pos[o] = steps + S.sa[k >> S.sa_shift];
+                o += lanes;
+                if (o < S.n_occ) start(o); else live = false;
+            }
+        }
+    }
+}
+
+}  // namespace smem
+
+extern "C" hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t st) {
+    if (S->n_intv == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::sa_count_kernel, dim3((unsigned)((S->n_intv + 255) / 256)), dim3(256), 0, st, *S);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_sa_walk(const smem::SaParams* S, int grid, hipStream_t st) {
+    if (S->n_occ == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::sa_walk_kernel, dim3(grid), dim3(256), 0, st, *S);
+    return hipGetLastError();
+}

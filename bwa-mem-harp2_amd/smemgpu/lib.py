@@ -26,6 +26,8 @@ EXPORTED = [
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
     "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_batch_debug", "smem_strerror",
+    "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
+    "smem_batch_sa", "smem_batch_sa_results",
 ]
 
 
@@ -42,6 +44,11 @@ class IndexT(C.Structure):
                 ("bwt_size", C.c_uint64), ("bwt", C.POINTER(C.c_uint32)), ("owns", C.c_int)]
 
 
+class SaT(C.Structure):
+    _fields_ = [("primary", C.c_uint64), ("L2", C.c_uint64 * 5), ("seq_len", C.c_uint64), ("sa_intv", C.c_uint64),
+                ("n_sa", C.c_uint64), ("sa", C.POINTER(C.c_uint64)), ("owns", C.c_int)]
+
+
 class OptT(C.Structure):
     _fields_ = [("min_seed_len", C.c_int), ("split_factor", C.c_float), ("split_width", C.c_int),
                 ("start_width", C.c_int)]
@@ -49,7 +56,8 @@ class OptT(C.Structure):
 
 class BatchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
-                ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int)]
+                ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int),
+                ("sa_ms", C.c_double), ("n_occ", C.c_uint64)]
 
 
 _lib = None
@@ -71,6 +79,15 @@ def load() -> C.CDLL:
     lib.smem_bwt_write.argtypes = [C.c_char_p, P(IndexT)]
     lib.smem_index_free.argtypes = [P(IndexT)]
     lib.smem_index_free.restype = None
+    lib.smem_bwt_build_sa.argtypes = [C.c_void_p, C.c_uint64, C.c_int, P(IndexT), P(SaT)]
+    lib.smem_bwt_build_gpu_sa.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int, P(IndexT), P(SaT)]
+    lib.smem_sa_read.argtypes = [C.c_char_p, P(SaT)]
+    lib.smem_sa_write.argtypes = [C.c_char_p, P(SaT)]
+    lib.smem_sa_free.argtypes = [P(SaT)]
+    lib.smem_sa_free.restype = None
+    lib.smem_gpu_load_sa.argtypes = [C.c_void_p, P(SaT)]
+    lib.smem_batch_sa.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.smem_batch_sa_results.argtypes = [C.c_void_p, P(P(C.c_uint64)), P(P(C.c_uint64)), P(C.c_uint64)]
     lib.smem_gpu_device_count.argtypes = []
     lib.smem_gpu_init.argtypes = [P(C.c_void_p), C.c_int, C.c_void_p, C.c_uint64, C.c_uint64, P(C.c_uint64)]
     lib.smem_gpu_shutdown.argtypes = [C.c_void_p]
@@ -137,6 +154,19 @@ class Index:
         return cls(raw)
 
     @classmethod
+    def build_sa(cls, fwd_codes: np.ndarray, sa_intv: int = 32, gpu: bool = False, device: int = 0):
+        """(Index, SA): the .bwt and the sampled SA bwa index writes beside it."""
+        fwd = np.ascontiguousarray(fwd_codes, dtype=np.uint8)
+        raw, sraw = IndexT(), SaT()
+        if gpu:
+            _check(load().smem_bwt_build_gpu_sa(device, fwd.ctypes.data, fwd.size, sa_intv, C.byref(raw), C.byref(sraw)),
+                   "smem_bwt_build_gpu_sa")
+        else:
+            _check(load().smem_bwt_build_sa(fwd.ctypes.data, fwd.size, sa_intv, C.byref(raw), C.byref(sraw)),
+                   "smem_bwt_build_sa")
+        return cls(raw), SA(sraw)
+
+    @classmethod
     def read(cls, path: str) -> "Index":
         raw = IndexT()
         _check(load().smem_bwt_read(path.encode(), C.byref(raw)), f"smem_bwt_read({path})")
@@ -174,6 +204,45 @@ class Index:
             pass
 
 
+class SA:
+    """Sampled suffix array (.sa) in host memory (owned by the library)."""
+
+    def __init__(self, raw: SaT):
+        self._raw = raw
+
+    @classmethod
+    def read(cls, path: str) -> "SA":
+        raw = SaT()
+        _check(load().smem_sa_read(path.encode(), C.byref(raw)), f"smem_sa_read({path})")
+        return cls(raw)
+
+    def write(self, path: str) -> None:
+        _check(load().smem_sa_write(path.encode(), C.byref(self._raw)), f"smem_sa_write({path})")
+
+    @property
+    def sa_intv(self) -> int:
+        return int(self._raw.sa_intv)
+
+    @property
+    def seq_len(self) -> int:
+        return int(self._raw.seq_len)
+
+    @property
+    def samples(self) -> np.ndarray:
+        """uint64 view (no copy) of sa[0 .. n_sa-1]; sa[0] = 2^64-1."""
+        return np.ctypeslib.as_array(self._raw.sa, shape=(int(self._raw.n_sa),))
+
+    def close(self) -> None:
+        if self._raw.sa:
+            load().smem_sa_free(C.byref(self._raw))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def device_count() -> int:
     return int(load().smem_gpu_device_count())
 
@@ -184,6 +253,17 @@ class Results:
     intv_off: np.ndarray  # (n_reads + 1,) uint64
     call_n: np.ndarray    # (n_lists,) uint32
     call_off: np.ndarray  # (n_reads + 1,) uint64
+    occ_off: np.ndarray | None = None  # (N + 1,) uint64, when Batch.sa() ran
+    sa_pos: np.ndarray | None = None   # (n_occ,) uint64 bwt_sa positions
+
+    def read_sa(self, i: int) -> np.ndarray:
+        """bwt_sa positions of read i's seed occurrences, in interval order."""
+        a, b = int(self.intv_off[i]), int(self.intv_off[i + 1])
+        return self.sa_pos[int(self.occ_off[a]):int(self.occ_off[b])]
+
+    def to_smsa(self) -> bytes:
+        from . import synth
+        return synth.write_smsa([self.read_sa(i) for i in range(self.intv_off.size - 1)])
 
     def read_calls(self, i: int) -> list:
         """The lists smem_next2 returned for read i, in order."""
@@ -226,6 +306,9 @@ class Gpu:
             _check(lib.smem_gpu_set_kernel_variant(self._h, variant), "smem_gpu_set_kernel_variant")
         self.device = device
 
+    def load_sa(self, sa: "SA") -> None:
+        _check(load().smem_gpu_load_sa(self._h, C.byref(sa._raw)), "smem_gpu_load_sa")
+
     def batch(self, max_reads: int, max_bases: int, max_len: int) -> "Batch":
         return Batch(self, max_reads, max_bases, max_len)
 
@@ -265,6 +348,10 @@ class Batch:
         _check(load().smem_batch_stats(self._h, C.byref(s)), "smem_batch_stats")
         return {k: getattr(s, k) for k, _ in BatchStats._fields_}
 
+    def sa(self, min_seed_len: int = 19, max_occ: int = 10000) -> None:
+        """bwt_sa of every seed occurrence of the last run (smem_batch_sa)."""
+        _check(load().smem_batch_sa(self._h, min_seed_len, max_occ), "smem_batch_sa")
+
     def debug_words(self, n_words: int) -> np.ndarray:
         out = np.zeros(n_words, dtype=np.uint64)
         rc = load().smem_batch_debug(self._h, out.ctypes.data, n_words)
@@ -287,7 +374,15 @@ class Batch:
         intv = (np.ctypeslib.as_array(C.cast(iv, C.POINTER(C.c_uint64)), shape=(max(ni, 1) * 4,))[:ni * 4]
                 .reshape(ni, 4).copy())
         call_n = np.ctypeslib.as_array(cn, shape=(max(nc, 1),))[:nc].copy()
-        return Results(intv, intv_off, call_n, call_off)
+        res = Results(intv, intv_off, call_n, call_off)
+        pos = C.POINTER(C.c_uint64)()
+        oo = C.POINTER(C.c_uint64)()
+        no = C.c_uint64()
+        if lib.smem_batch_sa_results(self._h, C.byref(pos), C.byref(oo), C.byref(no)) == 0:
+            n_occ = int(no.value)
+            res.occ_off = np.ctypeslib.as_array(oo, shape=(ni + 1,)).copy()
+            res.sa_pos = np.ctypeslib.as_array(pos, shape=(max(n_occ, 1),))[:n_occ].copy()
+        return res
 
     def close(self) -> None:
         if self._h:

@@ -231,3 +231,35 @@ def read_smgo(path_or_bytes) -> list:
     if pos != len(data):
         raise ValueError("trailing bytes in SMGO stream")
     return out
+
+
+def read_smsa(path_or_bytes) -> list:
+    """Parse an SMSA stream (include/smem_formats.h) into [read] -> uint64 positions."""
+    if isinstance(path_or_bytes, (bytes, bytearray)):
+        data = bytes(path_or_bytes)
+    else:
+        with open(path_or_bytes, "rb") as fh:
+            data = fh.read()
+    if data[:8] != b"SMSA0001":
+        raise ValueError("not an SMSA stream")
+    (n_reads,) = struct.unpack_from("<Q", data, 8)
+    pos = 16
+    out = []
+    for _ in range(n_reads):
+        (n,) = struct.unpack_from("<I", data, pos)
+        pos += 4
+        out.append(np.frombuffer(data, dtype="<u8", count=n, offset=pos).copy())
+        pos += 8 * n
+    if pos != len(data):
+        raise ValueError("trailing bytes in SMSA stream")
+    return out
+
+
+def write_smsa(per_read) -> bytes:
+    """SMSA stream bytes from [read] -> positions."""
+    parts = [b"SMSA0001", struct.pack("<Q", len(per_read))]
+    for p in per_read:
+        p = np.ascontiguousarray(p, dtype="<u8")
+        parts.append(struct.pack("<I", p.size))
+        parts.append(p.tobytes())
+    return b"".join(parts)

@@ -17,6 +17,14 @@
  *   uint64_t n_reads
  *   per read:  uint32_t n_calls
  *              per call: uint32_t n ; n x { uint64_t x0, x1, x2, info }
+ *
+ * SA positions file ("SMSA0001") — for every interval of an SMGO stream, in
+ * order, that mem_insert_seed() turns into seeds (seed length >= k and
+ * x2 <= max_occ, software/bwamem.c:467), bwt_sa(bwt, x0 + j) for j < x2
+ * (software/bwamem.c:469-474, software/bwt.c:104-114):
+ *   char     magic[8]      = "SMSA0001"
+ *   uint64_t n_reads
+ *   per read:  uint32_t n_occ ; n_occ x uint64_t position (forward-reverse coordinate)
  */
 #ifndef SMEM_FORMATS_H
 #define SMEM_FORMATS_H
@@ -28,6 +36,7 @@
 
 #define SMRD_MAGIC "SMRD0001"
 #define SMGO_MAGIC "SMGO0001"
+#define SMSA_MAGIC "SMSA0001"
 
 typedef struct {
 	uint64_t n_reads, n_bases;
@@ -68,6 +77,13 @@ static inline int smrd_load(const char *fn, smrd_reads_t *r)
 static inline int smgo_write_header(FILE *fp, uint64_t n_reads)
 {
 	if (fwrite(SMGO_MAGIC, 1, 8, fp) != 8) return -1;
+	if (fwrite(&n_reads, 8, 1, fp) != 1) return -1;
+	return 0;
+}
+
+static inline int smsa_write_header(FILE *fp, uint64_t n_reads)
+{
+	if (fwrite(SMSA_MAGIC, 1, 8, fp) != 8) return -1;
 	if (fwrite(&n_reads, 8, 1, fp) != 1) return -1;
 	return 0;
 }

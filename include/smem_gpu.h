@@ -52,6 +52,21 @@ typedef struct {
 	int owns;             /* bwt was allocated by this library */
 } smem_index_t;
 
+/* Sampled suffix array for bwt_sa (software/bwt.c:80-114): sa[r] =
+ * SA[r * sa_intv] for r < n_sa = (seq_len + sa_intv) / sa_intv, sa[0] =
+ * (uint64_t)-1 as bwt_cal_sa leaves it.  primary / L2 / seq_len are those of
+ * the .bwt it belongs to (the .sa header, software/bwt.c:852-863).  sa holds
+ * n_sa + 1 words (one zero pad). */
+typedef struct {
+	uint64_t primary;
+	uint64_t L2[5];
+	uint64_t seq_len;
+	uint64_t sa_intv;
+	uint64_t n_sa;
+	uint64_t *sa;
+	int owns;
+} smem_sa_t;
+
 /* the mem_opt_t fields the seeding loop reads (software/bwamem.h:44-48,
  * software/bwamem.c:456-458) */
 typedef struct {
@@ -79,6 +94,16 @@ int  smem_bwt_build_gpu(int device, const uint8_t *fwd_codes, uint64_t n_fwd, sm
 int  smem_bwt_read(const char *fn, smem_index_t *idx);
 int  smem_bwt_write(const char *fn, const smem_index_t *idx);
 void smem_index_free(smem_index_t *idx);
+/* smem_bwt_build + the sampled SA bwa index writes beside it (`bwa index`
+ * .sa, sa_intv = 32 there, software/bwtindex.c:280); sa_intv a power of 2 */
+int  smem_bwt_build_sa(const uint8_t *fwd_codes, uint64_t n_fwd, int sa_intv, smem_index_t *idx, smem_sa_t *sa);
+/* the same on a HIP device (prefix doubling, as smem_bwt_build_gpu) */
+int  smem_bwt_build_gpu_sa(int device, const uint8_t *fwd_codes, uint64_t n_fwd, int sa_intv, smem_index_t *idx,
+                           smem_sa_t *sa);
+/* .sa file I/O (software/bwt.c:852-897) */
+int  smem_sa_read(const char *fn, smem_sa_t *sa);
+int  smem_sa_write(const char *fn, const smem_sa_t *sa);
+void smem_sa_free(smem_sa_t *sa);
 
 /* --------------------------------------------------------------- device */
 /* Number of visible HIP devices (0 on a machine without a GPU). */
@@ -121,6 +146,21 @@ int  smem_batch_read(const smem_batch_t *b, int i, const smem_intv_t **intv, int
 int  smem_batch_results(const smem_batch_t *b, const smem_intv_t **intv, const uint64_t **intv_off,
                         const uint32_t **call_n, const uint64_t **call_off);
 
+/* ------------------------------------------------------- SA lookup */
+/* Keep the sampled SA of the uploaded index resident in HBM (the index's
+ * .sa, software/bwt.c:877-897; bwa_idx_load's bwt_restore_sa).  SMEM_E_ARG
+ * if it does not belong to the index. */
+int  smem_gpu_load_sa(smem_gpu_t *gpu, const smem_sa_t *sa);
+/* After smem_batch_run: bwt_sa (software/bwt.c:104-114) of every seed
+ * occurrence mem_insert_seed() generates from the lists — each interval with
+ * seed length >= min_seed_len and x2 <= max_occ, rows x0 .. x0+x2-1
+ * (software/bwamem.c:462-474) — on the GPU.  smem_batch_fetch then copies
+ * them; smem_batch_sa_results gives the positions (forward-reverse
+ * coordinates, the mem_seed_t rbeg) in interval order and occ_off[n_intv + 1]
+ * indexed by flat interval (the numbering of smem_batch_results). */
+int  smem_batch_sa(smem_batch_t *b, int min_seed_len, int max_occ);
+int  smem_batch_sa_results(const smem_batch_t *b, const uint64_t **pos, const uint64_t **occ_off, uint64_t *n_occ);
+
 /* ---------------------------------------------------------- telemetry */
 typedef struct {
 	double kernel_ms;        /* seeding kernel(s), HIP events on the batch stream */
@@ -129,6 +169,8 @@ typedef struct {
 	uint64_t n_calls;        /* smem_next2 lists produced */
 	uint32_t n_overflow;     /* reads re-run with a larger output capacity */
 	int grid, block;         /* launch shape of the seeding kernel */
+	double sa_ms;            /* smem_batch_sa kernels */
+	uint64_t n_occ;          /* seed occurrences resolved by smem_batch_sa */
 } smem_batch_stats_t;
 int  smem_batch_stats(const smem_batch_t *b, smem_batch_stats_t *st);
 

@@ -66,6 +66,16 @@ def load() -> C.CDLL:
         lib.orc_free.restype = None
         lib.orc_occ4.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
         lib.orc_occ4.restype = None
+        lib.orc_sa_load.argtypes = [C.c_char_p]
+        lib.orc_sa_load.restype = C.c_void_p
+        lib.orc_sa_wrap.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]
+        lib.orc_sa_wrap.restype = C.c_void_p
+        lib.orc_sa_free.argtypes = [C.c_void_p]
+        lib.orc_sa_free.restype = None
+        lib.orc_sa_lookup.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        lib.orc_sa_lookup.restype = C.c_uint64
+        lib.orc_sa_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int]
+        lib.orc_sa_batch.restype = None
         _lib = lib
     return _lib
 
@@ -99,6 +109,67 @@ class OracleIndex:
             self.close()
         except Exception:
             pass
+
+
+class OracleSA:
+    """Sampled SA (bwa's .sa: sa[i] = SA[i * sa_intv], sa[0] = -1) for bwt_sa."""
+
+    def __init__(self, path: str | None = None, sa=None, sa_intv: int = 32, seq_len: int = 0):
+        lib = load()
+        if path is not None:
+            self._h = lib.orc_sa_load(path.encode())
+            if not self._h:
+                raise IOError(path)
+            self._keep = None
+        else:
+            a = np.ascontiguousarray(sa, dtype=np.uint64)
+            self._keep = a
+            self._h = lib.orc_sa_wrap(a.ctypes.data, a.size, int(sa_intv), int(seq_len))
+
+    def lookup(self, index: OracleIndex, k) -> np.ndarray:
+        """bwt_sa(bwt, k) for every k (software/bwt.c:104-114)."""
+        k = np.ascontiguousarray(k, dtype=np.uint64)
+        out = np.zeros(max(k.size, 1), dtype=np.uint64)
+        if k.size:
+            load().orc_sa_batch(index._h, self._h, k.ctypes.data, k.size, out.ctypes.data, min(8, os.cpu_count() or 1))
+        return out[:k.size]
+
+    def close(self):
+        if self._h:
+            load().orc_sa_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def sa_queries(lists_per_read, min_seed_len: int = 19, max_occ: int = 500):
+    """The bwt_sa arguments mem_insert_seed() generates from smem_next2's lists
+    (software/bwamem.c:462-474): for every interval with seed length >=
+    min_seed_len and x2 <= max_occ, x0 + j for j < x2.  Returns (per-read
+    counts, concatenated k)."""
+    counts, ks = [], []
+    for lists in lists_per_read:
+        n = 0
+        for a in lists:
+            if a.shape[0] == 0:
+                continue
+            x0, x2, info = a[:, 0], a[:, 2], a[:, 3]
+            slen = (info & 0xFFFFFFFF).astype(np.int64) - (info >> 32).astype(np.int64)
+            for i in np.nonzero((slen >= min_seed_len) & (x2 <= max_occ))[0]:
+                ks.append(x0[i] + np.arange(int(x2[i]), dtype=np.uint64))
+                n += int(x2[i])
+        counts.append(n)
+    k = np.concatenate(ks).astype(np.uint64) if ks else np.zeros(0, np.uint64)
+    return np.array(counts, dtype=np.int64), k
+
+
+def ref_sa(bwt: str, sa: str, smgo: str, out: str, min_seed_len: int = 19, max_occ: int = 500) -> None:
+    """bwt_sa of every seed occurrence of an SMGO stream, by the compiled reference."""
+    subprocess.run([REF, "sa", bwt, sa, smgo, out, str(min_seed_len), str(max_occ)], check=True)
 
 
 def _opt(min_seed_len=19, split_factor=1.5, split_width=10, start_width=1) -> OptT:

@@ -17,6 +17,11 @@
  *   bench <in.bwt> <reads.smrd> <n_threads> <max_reads> <k> <split_factor> <split_width> <start_width>
  *       Same loop, timed, pthreads over contiguous read chunks; prints one
  *       line: "reads=<n> seconds=<t> threads=<T> reads_per_s=<r>".
+ *   sa    <in.bwt> <in.sa> <in.smgo> <out.smsa> <k> <max_occ>
+ *       For every interval of the SMGO stream that mem_insert_seed() turns
+ *       into seeds (software/bwamem.c:467), the reference bwt_sa()
+ *       (software/bwt.c:104-114) of each occurrence x0 + j, j < x2
+ *       (software/bwamem.c:469-474), written as SMSA (include/smem_formats.h).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -170,10 +175,63 @@ static int cmd_bench(int argc, char **argv)
 	return 0;
 }
 
+static int cmd_sa(int argc, char **argv)
+{
+	bwt_t *bwt;
+	FILE *in, *out;
+	char magic[8];
+	uint64_t n_reads, r;
+	int k, max_occ;
+	if (argc < 7) { fprintf(stderr, "usage: sa <bwt> <sa> <in.smgo> <out.smsa> <k> <max_occ>\n"); return 1; }
+	k = atoi(argv[5]);
+	max_occ = atoi(argv[6]);
+	bwt = bwt_restore_bwt(argv[1]);
+	bwt_restore_sa(argv[2], bwt);
+	in = fopen(argv[3], "rb");
+	out = fopen(argv[4], "wb");
+	if (!in || !out) return 1;
+	if (fread(magic, 1, 8, in) != 8 || memcmp(magic, SMGO_MAGIC, 8) != 0) return 1;
+	if (fread(&n_reads, 8, 1, in) != 1) return 1;
+	smsa_write_header(out, n_reads);
+	for (r = 0; r < n_reads; ++r) {
+		uint32_t n_calls, c, n_occ = 0;
+		long pos = ftell(out);
+		if (fread(&n_calls, 4, 1, in) != 1) return 1;
+		fwrite(&n_occ, 4, 1, out);
+		for (c = 0; c < n_calls; ++c) {
+			uint32_t n, i;
+			if (fread(&n, 4, 1, in) != 1) return 1;
+			for (i = 0; i < n; ++i) {
+				uint64_t v[4];
+				int slen;
+				bwtint_t j;
+				if (fread(v, 8, 4, in) != 4) return 1;
+				slen = (uint32_t)v[3] - (int)(v[3] >> 32);
+				if (slen < k || v[2] > (uint64_t)max_occ) continue;
+				for (j = 0; j < v[2]; ++j) {
+					uint64_t p = bwt_sa(bwt, v[0] + j);
+					fwrite(&p, 8, 1, out);
+					++n_occ;
+				}
+			}
+		}
+		{
+			long end = ftell(out);
+			fseek(out, pos, SEEK_SET);
+			fwrite(&n_occ, 4, 1, out);
+			fseek(out, end, SEEK_SET);
+		}
+	}
+	fclose(in);
+	fclose(out);
+	bwt_destroy(bwt);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	if (argc < 2) {
-		fprintf(stderr, "usage: ref_harness index|smem|bench ...\n");
+		fprintf(stderr, "usage: ref_harness index|smem|bench|sa ...\n");
 		return 1;
 	}
 	if (strcmp(argv[1], "index") == 0) {
@@ -184,6 +242,7 @@ int main(int argc, char **argv)
 	}
 	if (strcmp(argv[1], "smem") == 0) return cmd_smem(argc - 1, argv + 1);
 	if (strcmp(argv[1], "bench") == 0) return cmd_bench(argc - 1, argv + 1);
+	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

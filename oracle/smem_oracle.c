@@ -420,3 +420,99 @@ double orc_seed_timed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes,
 	gettimeofday(&t1, 0);
 	return (t1.tv_sec - t0.tv_sec) + (t1.tv_usec - t0.tv_usec) * 1e-6;
 }
+
+/* ------------------------------------------------------- SA lookup (bwt_sa) */
+
+orc_sa_t *orc_sa_load(const char *fn)
+{
+	/* .sa: primary, L2[1..4], sa_intv, seq_len, sa[1 .. n_sa-1] (software/bwt.c:852-897) */
+	uint64_t hdr[7];
+	orc_sa_t *s;
+	FILE *fp = fopen(fn, "rb");
+	if (!fp) return 0;
+	if (fread(hdr, 8, 7, fp) != 7) { fclose(fp); return 0; }
+	s = (orc_sa_t*)calloc(1, sizeof(orc_sa_t));
+	s->sa_intv = hdr[5];
+	s->seq_len = hdr[6];
+	s->n_sa = (s->seq_len + s->sa_intv) / s->sa_intv;
+	s->sa = (uint64_t*)malloc(8 * s->n_sa);
+	s->sa[0] = (uint64_t)-1;
+	if (fread(s->sa + 1, 8, s->n_sa - 1, fp) != s->n_sa - 1) { fclose(fp); free(s->sa); free(s); return 0; }
+	fclose(fp);
+	s->owns = 1;
+	return s;
+}
+
+orc_sa_t *orc_sa_wrap(const uint64_t *sa, uint64_t n_sa, uint64_t sa_intv, uint64_t seq_len)
+{
+	orc_sa_t *s = (orc_sa_t*)calloc(1, sizeof(orc_sa_t));
+	s->sa = (uint64_t*)sa;
+	s->n_sa = n_sa;
+	s->sa_intv = sa_intv;
+	s->seq_len = seq_len;
+	return s;
+}
+
+void orc_sa_free(orc_sa_t *s)
+{
+	if (!s) return;
+	if (s->owns) free(s->sa);
+	free(s);
+}
+
+/* bwt_invPsi (software/bwt.c:71-77): the LF step.  x = k with the $ row
+ * removed, c = BWT symbol at x (bwt_B0, software/bwt.h:78), result =
+ * L2[c] + Occ(c, k) (bwt_occ, software/bwt.c:125-146); row primary maps to 0 */
+static uint64_t inv_psi(const orc_bwt_t *b, uint64_t k)
+{
+	uint64_t x = k - (k > b->primary), cnt[4];
+	uint32_t w = b->bwt[((x >> 7) << 4) + 8 + ((x & 127) >> 4)];
+	int c = (int)(w >> ((~x & 15) << 1) & 3);
+	if (k == b->primary) return 0;
+	orc_occ4(b, k, cnt);  /* == bwt_occ(k, c) for c; k == seq_len gives the totals */
+	return b->L2[c] + cnt[c];
+}
+
+uint64_t orc_sa_lookup(const orc_bwt_t *b, const orc_sa_t *s, uint64_t k)
+{
+	uint64_t sa = 0, mask = s->sa_intv - 1;
+	while (k & mask) {
+		++sa;
+		k = inv_psi(b, k);
+	}
+	return sa + s->sa[k / s->sa_intv];  /* sa[0] = -1 (software/bwt.c:110-113) */
+}
+
+typedef struct {
+	const orc_bwt_t *b;
+	const orc_sa_t *s;
+	const uint64_t *k;
+	uint64_t *out;
+	uint64_t beg, end;
+} sa_job_t;
+
+static void *sa_job(void *data)
+{
+	sa_job_t *j = (sa_job_t*)data;
+	uint64_t i;
+	for (i = j->beg; i < j->end; ++i) j->out[i] = orc_sa_lookup(j->b, j->s, j->k[i]);
+	return 0;
+}
+
+void orc_sa_batch(const orc_bwt_t *b, const orc_sa_t *s, const uint64_t *k, uint64_t n, uint64_t *out, int n_threads)
+{
+	int t;
+	sa_job_t *jobs;
+	pthread_t *tid;
+	if (n_threads < 1) n_threads = 1;
+	jobs = (sa_job_t*)calloc(n_threads, sizeof(sa_job_t));
+	tid = (pthread_t*)calloc(n_threads, sizeof(pthread_t));
+	for (t = 0; t < n_threads; ++t) {
+		jobs[t].b = b; jobs[t].s = s; jobs[t].k = k; jobs[t].out = out;
+		jobs[t].beg = n * t / n_threads; jobs[t].end = n * (t + 1) / n_threads;
+		pthread_create(&tid[t], 0, sa_job, &jobs[t]);
+	}
+	for (t = 0; t < n_threads; ++t) pthread_join(tid[t], 0);
+	free(jobs); free(tid);
+}
+

@@ -83,6 +83,23 @@ double orc_seed_timed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes,
 
 void orc_free(void *p);
 
+/* ------------------------------------------------------- SA lookup (bwt_sa) */
+/* sampled suffix array as bwa keeps it (software/bwt.c:80-102, .sa file
+ * software/bwt.c:852-897): sa[i] = SA[i * sa_intv], sa[0] = (uint64_t)-1 */
+typedef struct {
+	uint64_t sa_intv, n_sa, seq_len;
+	uint64_t *sa;
+	int owns;
+} orc_sa_t;
+
+orc_sa_t *orc_sa_load(const char *fn);
+orc_sa_t *orc_sa_wrap(const uint64_t *sa, uint64_t n_sa, uint64_t sa_intv, uint64_t seq_len);
+void orc_sa_free(orc_sa_t *s);
+/* bwt_sa(bwt, k) (software/bwt.c:104-114) */
+uint64_t orc_sa_lookup(const orc_bwt_t *b, const orc_sa_t *s, uint64_t k);
+/* out[i] = bwt_sa(bwt, k[i]) for n positions, n_threads pthreads */
+void orc_sa_batch(const orc_bwt_t *b, const orc_sa_t *s, const uint64_t *k, uint64_t n, uint64_t *out, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,6 +12,9 @@ reference code itself:
   r1.smrd.gz          1500 reads (SMRD, include/smem_formats.h), mixed shapes
   g1_<case>.smgo.gz   reference smem_next2 streams under mem_insert_seed
                       (software/bwamem.c:453-460) for each option set
+  g1.sa.gz            the `bwa index` sampled suffix array (.sa, software/bwt.c:852)
+  g1_<case>.smsa.gz   reference bwt_sa() of every seed occurrence of that stream
+                      (software/bwamem.c:467-474, max_occ 10000)
   manifest.json       cases, options, sha256 of the uncompressed streams
 """
 import gzip
@@ -31,6 +34,8 @@ sys.path.insert(0, ROOT)
 
 from smemgpu import synth  # noqa: E402
 from oracle import oracle  # noqa: E402
+
+MAX_OCC = 10000  # mem_opt_t.max_occ default of this reference (software/bwamem.c:60)
 
 CASES = [
     dict(name="default", n_reads=1500, opt=dict(min_seed_len=19, split_factor=1.5, split_width=10, start_width=1)),
@@ -77,6 +82,8 @@ def main():
             gz_write(os.path.join(HERE, "g1.fa.gz"), fh.read())
         with open(os.path.join(tmp, "g1.bwt"), "rb") as fh:
             gz_write(os.path.join(HERE, "g1.bwt.gz"), fh.read())
+        with open(os.path.join(tmp, "g1.sa"), "rb") as fh:
+            gz_write(os.path.join(HERE, "g1.sa.gz"), fh.read())
         with open(smrd, "rb") as fh:
             gz_write(os.path.join(HERE, "r1.smrd.gz"), fh.read())
         manifest = {"genome": dict(n_bp=300_000, seed=11), "cases": []}
@@ -90,9 +97,17 @@ def main():
                 data = fh.read()
             gz_write(os.path.join(HERE, f"g1_{case['name']}.smgo.gz"), data)
             parsed = synth.read_smgo(data)
+            sa_out = os.path.join(tmp, case["name"] + ".smsa")
+            oracle.ref_sa(os.path.join(tmp, "g1.bwt"), os.path.join(tmp, "g1.sa"), out, sa_out,
+                          min_seed_len=case["opt"]["min_seed_len"], max_occ=MAX_OCC)
+            with open(sa_out, "rb") as fh:
+                sa_data = fh.read()
+            gz_write(os.path.join(HERE, f"g1_{case['name']}.smsa.gz"), sa_data)
             manifest["cases"].append(dict(case, sha256=hashlib.sha256(data).hexdigest(),
                                           n_intv=int(sum(a.shape[0] for r in parsed for a in r)),
-                                          n_calls=int(sum(len(r) for r in parsed))))
+                                          n_calls=int(sum(len(r) for r in parsed)),
+                                          max_occ=MAX_OCC, sa_sha256=hashlib.sha256(sa_data).hexdigest(),
+                                          n_occ=int(sum(p.size for p in synth.read_smsa(sa_data)))))
         with open(os.path.join(HERE, "manifest.json"), "w") as fh:
             json.dump(manifest, fh, indent=1)
         print(json.dumps(manifest, indent=1))

@@ -39,6 +39,17 @@ class Fixture:
         assert hashlib.sha256(data).hexdigest() == case["sha256"], "fixture corrupted"
         return data
 
+    @property
+    def sa_bytes(self) -> bytes:
+        """the reference `bwa index` .sa of the golden genome"""
+        return _gz("g1.sa.gz")
+
+    def sa_stream(self, case) -> bytes:
+        """reference bwt_sa of every seed occurrence of the case's stream (SMSA)"""
+        data = _gz(f"g1_{case['name']}.smsa.gz")
+        assert hashlib.sha256(data).hexdigest() == case["sa_sha256"], "fixture corrupted"
+        return data
+
 
 _cache = None
 

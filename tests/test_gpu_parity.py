@@ -213,3 +213,103 @@ def test_gpu_index_builder_golden(gpu_device):
     b = smemgpu.Index.build_gpu(fx.genome, device=gpu_device)
     assert b.primary == fx.index.primary
     assert np.array_equal(b.words, fx.index.words)
+
+
+# ---------------------------------------------------------------- bwt_sa
+def test_sa_golden_fixture(gpu_device, tmp_path):
+    """GPU bwt_sa of every seed occurrence == the reference's (golden SMSA)."""
+    import smemgpu
+    from tests import golden_data
+    fx = golden_data.load()
+    p = str(tmp_path / "g1.sa")
+    with open(p, "wb") as fh:
+        fh.write(fx.sa_bytes)
+    sa = smemgpu.SA.read(p)
+    gpu = smemgpu.Gpu(fx.index, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        for case in fx.cases:
+            reads = fx.reads.subset(np.arange(case["n_reads"]))
+            b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+            b.set_reads(reads.codes, reads.offs)
+            b.run(smemgpu.Options(**case["opt"]))
+            b.sa(case["opt"]["min_seed_len"], case["max_occ"])
+            res = b.fetch()
+            assert res.to_smgo() == fx.stream(case), case["name"]
+            assert res.to_smsa() == fx.sa_stream(case), case["name"]
+            assert b.stats()["n_occ"] == case["n_occ"]
+            b.close()
+    finally:
+        gpu.close()
+
+
+@pytest.mark.parametrize("max_occ", [1, 20, 10000])
+def test_sa_vs_oracle(gpu_device, max_occ):
+    """Random genome with repeats, mixed reads: GPU positions == restated bwt_sa."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(300_000, seed=41)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    oidx = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
+    osa = oracle.OracleSA(sa=sa.samples, sa_intv=32, seq_len=idx.seq_len)
+    try:
+        gpu.load_sa(sa)
+        reads = _reads(g, "mixed", seed=43)
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        b.sa(19, max_occ)
+        res = b.fetch()
+        counts, k = oracle.sa_queries([res.read_calls(i) for i in range(reads.n)], 19, max_occ)
+        assert np.array_equal(res.sa_pos, osa.lookup(oidx, k))
+        assert [res.read_sa(i).size for i in range(reads.n)] == counts.tolist()
+        b.close()
+    finally:
+        gpu.close()
+        osa.close()
+        oidx.close()
+
+
+def test_sa_intervals_and_errors(gpu_device):
+    """Other sampling intervals; SA of another index rejected; sa before run rejected."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(50_000, seed=45)
+    reads = synth.make_reads(g.codes, 400, 150, seed=46)
+    for intv in (1, 8, 128):
+        idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=intv)
+        gpu = smemgpu.Gpu(idx, device=gpu_device)
+        oidx = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
+        osa = oracle.OracleSA(sa=sa.samples, sa_intv=intv, seq_len=idx.seq_len)
+        gpu.load_sa(sa)
+        b = gpu.batch(reads.n, reads.codes.size, 150)
+        with pytest.raises(smemgpu.SmemError):
+            b.sa()
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        b.sa()
+        res = b.fetch()
+        _, k = oracle.sa_queries([res.read_calls(i) for i in range(reads.n)])
+        assert np.array_equal(res.sa_pos, osa.lookup(oidx, k)), intv
+        b.close()
+        gpu.close()
+        osa.close()
+        oidx.close()
+    other_idx, other_sa = smemgpu.Index.build_sa(synth.make_genome(50_001, seed=47).codes)
+    idx = smemgpu.Index.build(g.codes)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    with pytest.raises(smemgpu.SmemError):
+        gpu.load_sa(other_sa)
+    gpu.close()
+
+
+@pytest.mark.parametrize("n_bp", [3000, 250_000])
+def test_gpu_builder_sa_matches_cpu(gpu_device, n_bp):
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(n_bp, seed=48).codes
+    a_idx, a_sa = smemgpu.Index.build_sa(g, sa_intv=32)
+    b_idx, b_sa = smemgpu.Index.build_sa(g, sa_intv=32, gpu=True, device=gpu_device)
+    assert np.array_equal(a_idx.words, b_idx.words) and a_idx.primary == b_idx.primary
+    assert np.array_equal(a_sa.samples, b_sa.samples)

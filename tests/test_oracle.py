@@ -97,6 +97,64 @@ def test_index_builder_small_vs_reference(n_bp, seed, tmp_path, built):
     assert open(p, "rb").read() == open(str(tmp_path / "g.bwt"), "rb").read()
 
 
+@pytest.mark.parametrize("case_i", range(5))
+def test_oracle_sa_matches_reference_golden(fx, oidx, case_i, tmp_path):
+    """Restated bwt_sa == the compiled reference's bwt_sa for every seed
+    occurrence mem_insert_seed generates from the golden stream."""
+    from smemgpu import synth
+    case = fx.cases[case_i]
+    p = str(tmp_path / "g1.sa")
+    with open(p, "wb") as fh:
+        fh.write(fx.sa_bytes)
+    osa = oracle.OracleSA(path=p)
+    counts, k = oracle.sa_queries(synth.read_smgo(fx.stream(case)), case["opt"]["min_seed_len"], case["max_occ"])
+    pos = osa.lookup(oidx, k)
+    want = synth.read_smsa(fx.sa_stream(case))
+    assert [w.size for w in want] == counts.tolist()
+    assert np.array_equal(np.concatenate(want) if want else np.zeros(0, np.uint64), pos)
+    assert pos.size == case["n_occ"]
+    osa.close()
+
+
+def test_sa_builder_matches_reference(fx, tmp_path):
+    """smem_bwt_build_sa's .sa == `bwa index`'s .sa (bwt_cal_sa, interval 32), byte for byte."""
+    import smemgpu
+    idx, sa = smemgpu.Index.build_sa(fx.genome, sa_intv=32)
+    p = str(tmp_path / "mine.sa")
+    sa.write(p)
+    assert open(p, "rb").read() == fx.sa_bytes
+    back = smemgpu.SA.read(p)
+    assert np.array_equal(back.samples, sa.samples) and back.sa_intv == 32
+    with open(str(tmp_path / "mine.bwt"), "wb"):
+        pass
+    idx.write(str(tmp_path / "mine.bwt"))
+    assert open(str(tmp_path / "mine.bwt"), "rb").read() == fx.bwt_bytes
+
+
+@pytest.mark.parametrize("n_bp,seed,intv", [(1, 1, 32), (100, 2, 1), (2000, 3, 8), (3000, 4, 32), (3000, 4, 128)])
+def test_sa_lookup_brute_force(n_bp, seed, intv, built):
+    """Restated bwt_sa == the full suffix array (computed in Python) for every row."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(n_bp, seed=seed, n_chrom=1).codes
+    idx, sa = smemgpu.Index.build_sa(g, sa_intv=intv)
+    n = idx.seq_len
+    text = np.concatenate([g, (3 - g[::-1])]).astype(np.uint8)
+    # full SA of text$ by sorting suffixes (small n only)
+    # suffixes of text$: a proper prefix sorts first, so "$" (the empty suffix) is smallest
+    order = sorted(range(n + 1), key=lambda i: bytes(text[i:].tolist()))
+    oidx = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
+    osa = oracle.OracleSA(sa=sa.samples, sa_intv=intv, seq_len=n)
+    rows = np.arange(n + 1, dtype=np.uint64) if n < 3000 else np.random.default_rng(seed).integers(0, n + 1, 3000).astype(np.uint64)
+    got = osa.lookup(oidx, rows)
+    want = np.array([order[int(r)] if int(r) > 0 else (2 ** 64 - 1 + 0) for r in rows], dtype=np.uint64)
+    # row 0 is the $ suffix: sa[0] = -1 makes bwt_sa return (steps - 1) mod 2^64 there, as the reference does
+    nz = rows != 0
+    assert np.array_equal(got[nz], want[nz])
+    osa.close()
+    oidx.close()
+
+
 def test_bwt_roundtrip(fx, tmp_path):
     import smemgpu
     p = str(tmp_path / "a.bwt")
