@@ -81,16 +81,20 @@ def get_index(args, rank, world, barrier, device=0):
     os.makedirs(args.cache, exist_ok=True)
     n_bp = int(args.genome_mbp * 1e6)
     key = os.path.join(args.cache, f"genome_{n_bp}_{args.seed}.bwt")
-    if rank == 0 and not os.path.exists(key):
+    skey = key[:-4] + ".sa"
+    if rank == 0 and not (os.path.exists(key) and os.path.exists(skey)):
         t = time.time()
         g = synth.make_genome(n_bp, seed=args.seed, n_chrom=24)
-        idx = smemgpu.Index.build_gpu(g.codes, device=device) if args.builder == "gpu" else smemgpu.Index.build(g.codes)
+        idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32, gpu=args.builder == "gpu", device=device)
         idx.write(key + ".tmp")
+        sa.write(skey + ".tmp")
         os.replace(key + ".tmp", key)
+        os.replace(skey + ".tmp", skey)
         del g
-        log(f"index built ({args.builder}): {n_bp} bp genome, {idx.words.nbytes / 1e6:.1f} MB in {time.time() - t:.1f} s")
+        log(f"index built ({args.builder}): {n_bp} bp genome, {idx.words.nbytes / 1e6:.1f} MB .bwt + "
+            f"{sa.samples.nbytes / 1e6:.1f} MB .sa in {time.time() - t:.1f} s")
     barrier()
-    return smemgpu.Index.read(key), key
+    return smemgpu.Index.read(key), key, smemgpu.SA.read(skey)
 
 
 def make_reads(args, rank, genome_codes=None):
@@ -224,6 +228,22 @@ def pcie_inclusive(batch, reads, opt, reps: int = 2) -> float:
     return reads.n / best
 
 
+def sa_lookup(batch, opt, reps: int = 3) -> dict:
+    """The next stage on the same index: bwt_sa of every seed
+    occurrence of the batch (software/bwamem.c:462-474), on the GPU; reported
+    beside the SMEM metric, not part of a step."""
+    batch.run(opt)
+    best = None
+    for _ in range(reps):
+        batch.sa(opt.min_seed_len, 10000)
+        st = batch.stats()
+        if best is None or st["sa_ms"] < best["sa_ms"]:
+            best = st
+    return {"ms_per_batch": round(best["sa_ms"], 3), "occurrences": int(best["n_occ"]),
+            "occurrences_per_s": round(best["n_occ"] / (best["sa_ms"] * 1e-3), 1),
+            "what": "bwt_sa of every seed occurrence (seed length >= 19, x2 <= max_occ 10000), sa_intv 32"}
+
+
 def main():
     args = parse()
     import torch
@@ -233,9 +253,10 @@ def main():
     rank, world, local = d.rank, d.world, d.local
     barrier = d.barrier
 
-    idx, idx_path = get_index(args, rank, world, barrier, d.gpu)
+    idx, idx_path, sa = get_index(args, rank, world, barrier, d.gpu)
     reads = make_reads(args, rank)
     gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu)
+    gpu.load_sa(sa)
     # one batch object (own HIP stream, own buffers) per host worker, each
     # holding the whole read set: a step is one full pass over the reads
     batches = []
@@ -290,6 +311,7 @@ def main():
     st = batch.stats()
     value, elapsed_max = aggregate(d, elapsed, reads.n, args.steps)
     pcie = pcie_inclusive(batch, reads, opt) if rank == 0 else None
+    sa_rep = sa_lookup(batch, opt) if rank == 0 else None
 
     if rank == 0:
         bpr, bpr64, ostats, n_counted = algorithmic_bytes(args, idx, reads)
@@ -344,6 +366,7 @@ def main():
             "cpu_baseline": cpu,
             "compact_ms": round(st["compact_ms"], 3),
             "pcie_inclusive_reads_per_s": round(pcie, 1),
+            "sa_lookup": sa_rep,
             "overflow_reads": st["n_overflow"],
         }
         print(json.dumps(out), flush=True)
