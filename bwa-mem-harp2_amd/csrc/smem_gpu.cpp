@@ -89,6 +89,9 @@ struct HostBuf {
 
 }  // namespace
 
+// device SA sampling interval = 2^SA_DENSE_SHIFT (see smem_gpu_load_sa)
+constexpr uint32_t SA_DENSE_SHIFT = 2;
+
 struct smem_gpu {
     int device = 0;
     int n_cu = 0;
@@ -146,7 +149,7 @@ struct smem_batch {
     bool fetched = false, ran = false;
     uint64_t tot_intv = 0, tot_calls = 0;
     // bwt_sa of the seed occurrences (smem_batch_sa)
-    DevBuf<uint64_t> d_occ_n, d_occ_off, d_sa_pos;
+    DevBuf<uint64_t> d_occ_n, d_occ_off, d_sa_pos, d_kstart;
     DevBuf<uint8_t> d_sa_tmp;
     HostBuf<uint64_t> h_occ_off, h_sa_pos;
     bool sa_ran = false, sa_fetched = false;
@@ -258,6 +261,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
     b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
     b->d_occ_n.release(); b->d_occ_off.release(); b->d_sa_pos.release(); b->d_sa_tmp.release();
+    b->d_kstart.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
     b->h_intv_off.release(); b->h_call_off.release();
     for (auto& ev : b->ev)
@@ -581,6 +585,34 @@ int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
     if (e != hipSuccess) return fail(SMEM_E_DEVICE, "smem_gpu_load_sa: upload", e);
     g->n_sa = sa->n_sa;
     g->sa_shift = (uint32_t)__builtin_ctzll(sa->sa_intv);
+    // a denser device copy (every SA_DENSE-th row, derived by LF walks from the
+    // stored samples: same results, fewer steps per lookup); 8 B per
+    // SA_DENSE symbols of HBM
+    const uint32_t dshift = std::min<uint32_t>(g->sa_shift, SA_DENSE_SHIFT);
+    if (dshift < g->sa_shift) {
+        const uint64_t n_dense = (sa->seq_len + (1ull << dshift)) >> dshift;
+        uint64_t* dense = nullptr;
+        e = hipMalloc(&dense, (n_dense + 1) * sizeof(uint64_t));
+        if (e != hipSuccess) return fail(SMEM_E_NOMEM, "smem_gpu_load_sa: hipMalloc(dense)", e);
+        smem::SaParams S;
+        std::memset(&S, 0, sizeof(S));
+        S.occ64 = g->d_occ64;
+        S.primary = g->primary;
+        std::memcpy(S.L2, g->L2, sizeof(S.L2));
+        S.sa = g->d_sa;
+        S.sa_shift = g->sa_shift;
+        e = smem_launch_sa_densify(&S, dshift, n_dense, dense, nullptr);
+        if (e == hipSuccess) e = hipMemset(dense + n_dense, 0, sizeof(uint64_t));
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            (void)hipFree(dense);
+            return fail(SMEM_E_DEVICE, "smem_gpu_load_sa: densify", e);
+        }
+        (void)hipFree(g->d_sa);
+        g->d_sa = dense;
+        g->n_sa = n_dense;
+        g->sa_shift = dshift;
+    }
     return SMEM_OK;
 }
 
@@ -619,8 +651,10 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     HIP_TRY(hipStreamSynchronize(b->st));
     b->tot_occ = b->h_tot.p[2];
     HIP_TRY(b->d_sa_pos.ensure(std::max<uint64_t>(b->tot_occ, 1)));
+    HIP_TRY(b->d_kstart.ensure(b->tot_occ + 2));  // +2: the walk's aligned 16-B loads
     S.n_occ = b->tot_occ;
     S.pos = b->d_sa_pos.p;
+    S.kstart = b->d_kstart.p;
     const int grid = std::max(1, (int)std::min<uint64_t>((uint64_t)g->n_cu * 8, (b->tot_occ + 255) / 256));
     HIP_TRY(smem_launch_sa_walk(&S, grid, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));

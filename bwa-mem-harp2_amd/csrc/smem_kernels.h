@@ -61,6 +61,7 @@ struct SaParams {
     int min_seed_len;
     uint64_t max_occ;
     uint64_t* n_occ_intv;      // [n_intv] occurrences per interval (count kernel output)
+    uint64_t* kstart;          // [n_occ + 2] the row of each occurrence (fill kernel)
     uint64_t* pos;             // [n_occ] bwt_sa results
 };
 
@@ -97,6 +98,8 @@ hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int write, hipStr
 hipError_t smem_launch_fill_i32(int32_t* p, int32_t v, int n, hipStream_t st);
 hipError_t smem_launch_ovf_slot(const int32_t* items, int n_ovf, int32_t* ovf_slot, hipStream_t st);
 hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t st);
+hipError_t smem_launch_sa_densify(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense, uint64_t* dense,
+                                  hipStream_t st);
 hipError_t smem_launch_sa_walk(const smem::SaParams* S, int grid, hipStream_t st);
 hipError_t smem_launch_offsets(const uint64_t* in, uint64_t* out, int n, void* temp, size_t* temp_bytes,
                                hipStream_t st);

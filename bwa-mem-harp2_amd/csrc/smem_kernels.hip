@@ -1083,63 +1083,110 @@ __global__ __launch_bounds__(256) void sa_count_kernel(SaParams S) {
     S.n_occ_intv[t] = (slen < S.min_seed_len || v.x2 > S.max_occ) ? 0 : v.x2;
 }
 
-// bwt_invPsi on the Occ64 layout
-__device__ __forceinline__ uint64_t inv_psi64(const SaParams& S, uint64_t k) {
-    if (k == S.primary) return 0;
-    const uint64_t kk = k - (k > S.primary);
-    const uint4* b = reinterpret_cast<const uint4*>(S.occ64) + (kk >> 6) * 2;
-    const uint4 cnt = b[0], sym = b[1];
-    const uint32_t pos = (uint32_t)(kk & 63);
-    const uint32_t sel = pos >> 4;
-    const uint32_t w = sel == 0 ? sym.x : (sel == 1 ? sym.y : (sel == 2 ? sym.z : sym.w));
-    const int c = (int)((w >> ((~pos & 15u) << 1)) & 3u);
-    uint32_t C, G, T;
-    count_cgt4(sym, pos, C, G, T);
-    const uint64_t oc = occ_cgt(cnt, 0) + C, og = occ_cgt(cnt, 1) + G, ot = occ_cgt(cnt, 2) + T;
-    const uint64_t occ = c == 0 ? kk + 1 - oc - og - ot : (c == 1 ? oc : (c == 2 ? og : ot));
-    return sel4(c, S.L2[0], S.L2[1], S.L2[2], S.L2[3]) + occ;
+// rows x0 .. x0 + n - 1 of every interval at its occurrence offset
+__global__ __launch_bounds__(256) void sa_fill_kernel(SaParams S) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= S.n_intv) return;
+    const uint64_t o = S.occ_off[t], n = S.occ_off[t + 1] - o;
+    const uint64_t x0 = S.intv[t].x0;
+    for (uint64_t j = 0; j < n; ++j) S.kstart[o + j] = x0 + j;
 }
 
-// One lane per occurrence, occurrences dealt lane-strided; the row of
-// occurrence o is x0 + (o - occ_off[t]) of the interval t that holds it
-// (binary search over occ_off, once per occurrence).  Lanes of a wave walk
-// different numbers of LF steps (0 .. sa_intv-1): a lane that finishes takes
-// its next occurrence in the same loop, so the wave stays full.
+// One lane per occurrence, occurrences dealt lane-strided.  Lanes of a wave
+// walk different numbers of LF steps (0 .. sa_intv-1); a lane that finishes
+// takes its next occurrence in the same loop.  Every iteration makes exactly
+// two 16-B loads per lane from per-lane addresses — the Occ64 bucket (counts,
+// symbols) for a lane that steps, or the 16 B around its SA sample and
+// around its next occurrence's row for a lane that finishes — so the wave
+// waits for one memory round trip per iteration whatever its lanes do.
 __global__ __launch_bounds__(256) void sa_walk_kernel(SaParams S) {
     const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
     uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t mask = (1ull << S.sa_shift) - 1;
-    uint64_t k = 0, steps = 0;
-    bool live = false;
-    auto start = [&](uint64_t occ) {
-        uint64_t lo = 0, hi = S.n_intv;  // largest t with occ_off[t] <= occ
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (S.occ_off[mid] <= occ) lo = mid; else hi = mid;
-        }
-        k = S.intv[lo].x0 + (occ - S.occ_off[lo]);
-        steps = 0;
-    };
-    if (o < S.n_occ) {
-        start(o);
-        live = true;
-    }
+    const uint4* occ = reinterpret_cast<const uint4*>(S.occ64);
+    const uint4* sa16 = reinterpret_cast<const uint4*>(S.sa);
+    const uint4* ks16 = reinterpret_cast<const uint4*>(S.kstart);
+    bool live = o < S.n_occ;
+    uint64_t k = live ? S.kstart[o] : 0, steps = 0;
     while (__any(live)) {
+        const bool step = live && (k & mask) != 0;
+        const uint64_t on = o + lanes;  // next occurrence of this lane
+        const uint64_t kk = k - (k > S.primary);
+        const uint4* pa = step ? occ + (kk >> 6) * 2 : sa16 + ((k >> S.sa_shift) >> 1);
+        const uint4* pb = step ? pa + 1 : ks16 + ((on < S.n_occ ? on : 0) >> 1);
+        uint4 va = {0, 0, 0, 0}, vb = {0, 0, 0, 0};
         if (live) {
-            if (k & mask) {
-                k = inv_psi64(S, k);
-                ++steps;
+            va = *pa;
+            vb = *pb;
+        }
+        if (step) {  // bwt_invPsi (software/bwt.c:71-77) on the Occ64 bucket
+            if (k == S.primary) {
+                k = 0;
             } else {
-                // sa[0] = -1: unsigned wrap as in software/bwt.c:110-113
-                S.pos[o] = steps + S.sa[k >> S.sa_shift];
-                o += lanes;
-                if (o < S.n_occ) start(o); else live = false;
+                const uint32_t pos = (uint32_t)(kk & 63), sel = pos >> 4;
+                const uint32_t w = sel == 0 ? vb.x : (sel == 1 ? vb.y : (sel == 2 ? vb.z : vb.w));
+                const int c = (int)((w >> ((~pos & 15u) << 1)) & 3u);
+                uint32_t C, G, T;
+                count_cgt4(vb, pos, C, G, T);
+                const uint64_t oc = occ_cgt(va, 0) + C, og = occ_cgt(va, 1) + G, ot = occ_cgt(va, 2) + T;
+                const uint64_t n = c == 0 ? kk + 1 - oc - og - ot : (c == 1 ? oc : (c == 2 ? og : ot));
+                k = sel4(c, S.L2[0], S.L2[1], S.L2[2], S.L2[3]) + n;
             }
+            ++steps;
+        } else if (live) {
+            // sa[0] = -1: unsigned wrap as in software/bwt.c:110-113
+            const uint64_t si = k >> S.sa_shift;
+            S.pos[o] = steps + ((si & 1) ? ((uint64_t)va.w << 32 | va.z) : ((uint64_t)va.y << 32 | va.x));
+            o = on;
+            live = o < S.n_occ;
+            k = (o & 1) ? ((uint64_t)vb.w << 32 | vb.z) : ((uint64_t)vb.y << 32 | vb.x);
+            steps = 0;
         }
     }
 }
 
+// A denser device copy of the sampled SA: dense[i] = bwt_sa(i * D) for
+// D = 2^dshift dividing sa_intv, each computed by the same LF walk to the
+// next stored sample.  bwt_sa(k) walked to the first multiple of D and
+// finished from dense[] equals the reference's walk to the first multiple of
+// sa_intv (same steps, same unsigned arithmetic, sa[0] = -1 included), so
+// lookups take (D-1)/2 steps on average instead of (sa_intv-1)/2.
+__global__ __launch_bounds__(256) void sa_densify_kernel(SaParams S, uint32_t dshift, uint64_t n_dense,
+                                                          uint64_t* __restrict__ dense) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_dense) return;
+    const uint64_t mask = (1ull << S.sa_shift) - 1;
+    const uint4* occ = reinterpret_cast<const uint4*>(S.occ64);
+    uint64_t k = i << dshift, steps = 0;
+    while (k & mask) {
+        if (k == S.primary) {
+            k = 0;
+        } else {
+            const uint64_t kk = k - (k > S.primary);
+            const uint4 va = occ[(kk >> 6) * 2], vb = occ[(kk >> 6) * 2 + 1];
+            const uint32_t pos = (uint32_t)(kk & 63), sel = pos >> 4;
+            const uint32_t w = sel == 0 ? vb.x : (sel == 1 ? vb.y : (sel == 2 ? vb.z : vb.w));
+            const int c = (int)((w >> ((~pos & 15u) << 1)) & 3u);
+            uint32_t C, G, T;
+            count_cgt4(vb, pos, C, G, T);
+            const uint64_t oc = occ_cgt(va, 0) + C, og = occ_cgt(va, 1) + G, ot = occ_cgt(va, 2) + T;
+            const uint64_t n = c == 0 ? kk + 1 - oc - og - ot : (c == 1 ? oc : (c == 2 ? og : ot));
+            k = sel4(c, S.L2[0], S.L2[1], S.L2[2], S.L2[3]) + n;
+        }
+        ++steps;
+    }
+    dense[i] = steps + S.sa[k >> S.sa_shift];
+}
+
 }  // namespace smem
+
+extern "C" hipError_t smem_launch_sa_densify(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense,
+                                             uint64_t* dense, hipStream_t st) {
+    if (n_dense == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::sa_densify_kernel, dim3((unsigned)((n_dense + 255) / 256)), dim3(256), 0, st, *S, dshift,
+                       n_dense, dense);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t st) {
     if (S->n_intv == 0) return hipSuccess;
@@ -1149,6 +1196,7 @@ extern "C" hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t 
 
 extern "C" hipError_t smem_launch_sa_walk(const smem::SaParams* S, int grid, hipStream_t st) {
     if (S->n_occ == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::sa_fill_kernel, dim3((unsigned)((S->n_intv + 255) / 256)), dim3(256), 0, st, *S);
     hipLaunchKernelGGL(smem::sa_walk_kernel, dim3(grid), dim3(256), 0, st, *S);
     return hipGetLastError();
 }
