@@ -241,7 +241,8 @@ def sa_lookup(batch, opt, reps: int = 3) -> dict:
             best = st
     return {"ms_per_batch": round(best["sa_ms"], 3), "occurrences": int(best["n_occ"]),
             "occurrences_per_s": round(best["n_occ"] / (best["sa_ms"] * 1e-3), 1),
-            "what": "bwt_sa of every seed occurrence (seed length >= 19, x2 <= max_occ 10000), sa_intv 32"}
+            "what": "bwt_sa of every seed occurrence (seed length >= 19, x2 <= max_occ 10000); "
+                    ".sa sa_intv 32, device copy densified to every 4th row at load"}
 
 
 def main():

@@ -149,7 +149,10 @@ int  smem_batch_results(const smem_batch_t *b, const smem_intv_t **intv, const u
 /* ------------------------------------------------------- SA lookup */
 /* Keep the sampled SA of the uploaded index resident in HBM (the index's
  * .sa, software/bwt.c:877-897; bwa_idx_load's bwt_restore_sa).  SMEM_E_ARG
- * if it does not belong to the index. */
+ * if it does not belong to the index.  Reads sa->sa[0 .. n_sa-1] only (the
+ * reference's bwt->sa array as is).  The device copy is densified to every
+ * 4th row by LF walks from these samples (8 B per 4 symbols of HBM); lookups
+ * return exactly what bwt_sa does with the .sa's own interval. */
 int  smem_gpu_load_sa(smem_gpu_t *gpu, const smem_sa_t *sa);
 /* After smem_batch_run: bwt_sa (software/bwt.c:104-114) of every seed
  * occurrence mem_insert_seed() generates from the lists — each interval with
