@@ -263,3 +263,46 @@ def write_smsa(per_read) -> bytes:
         parts.append(struct.pack("<I", p.size))
         parts.append(p.tobytes())
     return b"".join(parts)
+
+
+SEED_DT = np.dtype([("rbeg", "<i8"), ("qbeg", "<i4"), ("len", "<i4")])  # mem_seed_t
+
+
+def read_smch(path_or_bytes) -> list:
+    """Parse an SMCH stream (include/smem_formats.h) into [read] -> list of
+    (pos, seeds) with seeds a SEED_DT array, in the stream's chain order."""
+    if isinstance(path_or_bytes, (bytes, bytearray)):
+        data = bytes(path_or_bytes)
+    else:
+        with open(path_or_bytes, "rb") as fh:
+            data = fh.read()
+    if data[:8] != b"SMCH0001":
+        raise ValueError("not an SMCH stream")
+    (n_reads,) = struct.unpack_from("<Q", data, 8)
+    pos = 16
+    out = []
+    for _ in range(n_reads):
+        (nc,) = struct.unpack_from("<I", data, pos)
+        pos += 4
+        chains = []
+        for _ in range(nc):
+            cpos, n = struct.unpack_from("<qI", data, pos)
+            pos += 12
+            chains.append((cpos, np.frombuffer(data, dtype=SEED_DT, count=n, offset=pos).copy()))
+            pos += 16 * n
+        out.append(chains)
+    if pos != len(data):
+        raise ValueError("trailing bytes in SMCH stream")
+    return out
+
+
+def write_smch(per_read) -> bytes:
+    """SMCH stream bytes from [read] -> [(pos, seeds)]."""
+    parts = [b"SMCH0001", struct.pack("<Q", len(per_read))]
+    for chains in per_read:
+        parts.append(struct.pack("<I", len(chains)))
+        for cpos, seeds in chains:
+            seeds = np.ascontiguousarray(seeds, dtype=SEED_DT)
+            parts.append(struct.pack("<qI", int(cpos), seeds.size))
+            parts.append(seeds.tobytes())
+    return b"".join(parts)

@@ -25,6 +25,15 @@
  *   char     magic[8]      = "SMSA0001"
  *   uint64_t n_reads
  *   per read:  uint32_t n_occ ; n_occ x uint64_t position (forward-reverse coordinate)
+ *
+ * Chains file ("SMCH0001") — per read, the chains mem_chain() returns
+ * (software/bwamem.c:593-614; kbtree in-order, software/kbtree.h:336-358),
+ * optionally after mem_chain_flt() (software/bwamem.c:629-690):
+ *   char     magic[8]      = "SMCH0001"
+ *   uint64_t n_reads
+ *   per read:  uint32_t n_chains
+ *              per chain: int64_t pos ; uint32_t n ;
+ *                         n x { int64_t rbeg ; int32_t qbeg ; int32_t len }  (mem_seed_t)
  */
 #ifndef SMEM_FORMATS_H
 #define SMEM_FORMATS_H
@@ -37,6 +46,7 @@
 #define SMRD_MAGIC "SMRD0001"
 #define SMGO_MAGIC "SMGO0001"
 #define SMSA_MAGIC "SMSA0001"
+#define SMCH_MAGIC "SMCH0001"
 
 typedef struct {
 	uint64_t n_reads, n_bases;
@@ -77,6 +87,13 @@ static inline int smrd_load(const char *fn, smrd_reads_t *r)
 static inline int smgo_write_header(FILE *fp, uint64_t n_reads)
 {
 	if (fwrite(SMGO_MAGIC, 1, 8, fp) != 8) return -1;
+	if (fwrite(&n_reads, 8, 1, fp) != 1) return -1;
+	return 0;
+}
+
+static inline int smch_write_header(FILE *fp, uint64_t n_reads)
+{
+	if (fwrite(SMCH_MAGIC, 1, 8, fp) != 8) return -1;
 	if (fwrite(&n_reads, 8, 1, fp) != 1) return -1;
 	return 0;
 }

@@ -41,6 +41,11 @@ class Stats(C.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
+class ChainOptT(C.Structure):
+    _fields_ = [("w", C.c_int), ("max_chain_gap", C.c_int), ("min_seed_len", C.c_int), ("mask_level", C.c_float),
+                ("drop_ratio", C.c_float), ("filter", C.c_int)]
+
+
 _lib = None
 
 
@@ -76,6 +81,8 @@ def load() -> C.CDLL:
         lib.orc_sa_lookup.restype = C.c_uint64
         lib.orc_sa_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int]
         lib.orc_sa_batch.restype = None
+        lib.orc_chain.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(ChainOptT), C.c_int,
+                                  C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64)]
         _lib = lib
     return _lib
 
@@ -235,3 +242,58 @@ def ref_bench(bwt: str, smrd: str, threads: int, max_reads: int, min_seed_len=19
                         str(split_width), str(start_width)], check=True, capture_output=True, text=True)
     kv = dict(tok.split("=") for tok in p.stdout.split())
     return {k: float(v) for k, v in kv.items()}
+
+
+SEED_DT = np.dtype([("rbeg", "<i8"), ("qbeg", "<i4"), ("len", "<i4")])  # mem_seed_t
+
+
+def chain_seeds(lists_per_read, positions_per_read, min_seed_len: int = 19, max_occ: int = 10000):
+    """The seed sequence mem_insert_seed generates (software/bwamem.c:462-474):
+    for every interval with seed length >= min_seed_len and x2 <= max_occ, in
+    order, one (rbeg = bwt_sa(x0 + j), qbeg, len) per occurrence j < x2.
+    positions_per_read are those bwt_sa values (an SMSA stream's). Returns
+    (seeds SEED_DT array, seed_off[n_reads + 1])."""
+    parts, counts = [], []
+    for lists, pos in zip(lists_per_read, positions_per_read):
+        q, l = [], []
+        for a in lists:
+            if a.shape[0] == 0:
+                continue
+            x2, info = a[:, 2], a[:, 3]
+            beg = (info >> 32).astype(np.int64)
+            slen = (info & 0xFFFFFFFF).astype(np.int64) - beg
+            keep = (slen >= min_seed_len) & (x2 <= max_occ)
+            rep = np.where(keep, x2, 0).astype(np.int64)
+            q.append(np.repeat(beg, rep))
+            l.append(np.repeat(slen, rep))
+        qb = np.concatenate(q) if q else np.zeros(0, np.int64)
+        if qb.size != len(pos):
+            raise ValueError("positions do not match the lists")
+        s = np.zeros(qb.size, dtype=SEED_DT)
+        s["rbeg"] = np.asarray(pos, dtype=np.uint64).view(np.int64)
+        s["qbeg"] = qb
+        s["len"] = np.concatenate(l) if l else 0
+        parts.append(s)
+        counts.append(qb.size)
+    seeds = np.concatenate(parts) if parts else np.zeros(0, SEED_DT)
+    off = np.concatenate([[0], np.cumsum(counts, dtype=np.uint64)]).astype(np.uint64)
+    return seeds, off
+
+
+def chain(seeds, seed_off, l_pac: int, w=100, max_chain_gap=10000, min_seed_len=19, mask_level=0.5,
+          drop_ratio=0.5, filter=1, threads: int = 1) -> bytes:
+    """mem_chain (+ mem_chain_flt when filter) of every read: SMCH bytes."""
+    lib = load()
+    seeds = np.ascontiguousarray(seeds, dtype=SEED_DT)
+    seed_off = np.ascontiguousarray(seed_off, dtype=np.uint64)
+    o = ChainOptT(w, max_chain_gap, min_seed_len, mask_level, drop_ratio, int(filter))
+    out = C.POINTER(C.c_uint8)()
+    out_len = C.c_uint64()
+    sp = seeds.ctypes.data if seeds.size else None
+    rc = lib.orc_chain(seed_off.size - 1, sp, seed_off.ctypes.data, int(l_pac), C.byref(o), threads, C.byref(out),
+                       C.byref(out_len))
+    if rc != 0:
+        raise RuntimeError("orc_chain failed")
+    data = C.string_at(out, out_len.value)
+    lib.orc_free(out)
+    return data

@@ -22,6 +22,12 @@
  *       into seeds (software/bwamem.c:467), the reference bwt_sa()
  *       (software/bwt.c:104-114) of each occurrence x0 + j, j < x2
  *       (software/bwamem.c:469-474), written as SMSA (include/smem_formats.h).
+ *   chain <in.bwt> <in.sa> <reads.smrd> <out.smch> <k> <r> <s> <start_width> <max_occ> <w>
+ *         <max_chain_gap> <mask_level> <drop_ratio> <filter>
+ *       For every read, the reference mem_chain() (software/bwamem.c:593) and,
+ *       when filter != 0, mem_chain_flt() (software/bwamem.c:629) as
+ *       mem_align1_core calls them (software/bwamem.c:1448-1449); chains
+ *       written as SMCH (include/smem_formats.h).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -228,6 +234,70 @@ static int cmd_sa(int argc, char **argv)
 	return 0;
 }
 
+/* mem_seed_t / mem_chain_t / mem_chain_v are private to software/bwamem.c
+ * (:317-327); these are layout-identical declarations to read its results */
+typedef struct { int64_t rbeg; int32_t qbeg, len; } h_seed_t;
+typedef struct { int n, m; int64_t pos; h_seed_t *seeds; } h_chain_t;
+typedef struct { size_t n, m; h_chain_t *a; } h_chain_v;
+extern h_chain_v mem_chain(const mem_opt_t *opt, const bwt_t *bwt, int64_t l_pac, int len, const uint8_t *seq);
+extern int mem_chain_flt(const mem_opt_t *opt, int n_chn, h_chain_t *chains);
+
+static int cmd_chain(int argc, char **argv)
+{
+	bwt_t *bwt;
+	smrd_reads_t r;
+	mem_opt_t *opt;
+	FILE *out;
+	uint64_t i;
+	int filter;
+	if (argc < 15) {
+		fprintf(stderr, "usage: chain <bwt> <sa> <reads> <out> <k> <r> <s> <sw> <max_occ> <w> <gap> <mask> <drop> <filter>\n");
+		return 1;
+	}
+	opt = mem_opt_init();
+	opt->min_seed_len = atoi(argv[5]);
+	opt->split_factor = (float)atof(argv[6]);
+	opt->split_width = atoi(argv[7]);
+	if (atoi(argv[8]) == 2) opt->flag |= MEM_F_NO_EXACT;
+	opt->max_occ = atoi(argv[9]);
+	opt->w = atoi(argv[10]);
+	opt->max_chain_gap = atoi(argv[11]);
+	opt->mask_level = (float)atof(argv[12]);
+	opt->chain_drop_ratio = (float)atof(argv[13]);
+	filter = atoi(argv[14]);
+	bwt = bwt_restore_bwt(argv[1]);
+	bwt_restore_sa(argv[2], bwt);
+	if (smrd_load(argv[3], &r) != 0) return 1;
+	out = fopen(argv[4], "wb");
+	if (!out) return 1;
+	smch_write_header(out, r.n_reads);
+	for (i = 0; i < r.n_reads; ++i) {
+		h_chain_v c = mem_chain(opt, bwt, (int64_t)(bwt->seq_len >> 1), r.len[i], r.codes + r.off[i]);
+		uint32_t nc, j;
+		if (filter) c.n = mem_chain_flt(opt, (int)c.n, c.a);
+		nc = (uint32_t)c.n;
+		fwrite(&nc, 4, 1, out);
+		for (j = 0; j < nc; ++j) {
+			uint32_t n = (uint32_t)c.a[j].n;
+			int k;
+			fwrite(&c.a[j].pos, 8, 1, out);
+			fwrite(&n, 4, 1, out);
+			for (k = 0; k < c.a[j].n; ++k) {
+				fwrite(&c.a[j].seeds[k].rbeg, 8, 1, out);
+				fwrite(&c.a[j].seeds[k].qbeg, 4, 1, out);
+				fwrite(&c.a[j].seeds[k].len, 4, 1, out);
+			}
+		}
+		for (j = 0; j < c.m && j < c.n; ++j) free(c.a[j].seeds);
+		free(c.a);
+	}
+	fclose(out);
+	smrd_free(&r);
+	free(opt);
+	bwt_destroy(bwt);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	if (argc < 2) {
@@ -243,6 +313,7 @@ int main(int argc, char **argv)
 	if (strcmp(argv[1], "smem") == 0) return cmd_smem(argc - 1, argv + 1);
 	if (strcmp(argv[1], "bench") == 0) return cmd_bench(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
+	if (strcmp(argv[1], "chain") == 0) return cmd_chain(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

@@ -100,6 +100,21 @@ uint64_t orc_sa_lookup(const orc_bwt_t *b, const orc_sa_t *s, uint64_t k);
 /* out[i] = bwt_sa(bwt, k[i]) for n positions, n_threads pthreads */
 void orc_sa_batch(const orc_bwt_t *b, const orc_sa_t *s, const uint64_t *k, uint64_t n, uint64_t *out, int n_threads);
 
+/* ------------------------------------------------ chaining (chain_oracle.c) */
+typedef struct { int64_t rbeg; int32_t qbeg, len; } orc_seed_t;   /* mem_seed_t */
+typedef struct {
+	int w;                 /* band width, software/bwamem.c:53 */
+	int max_chain_gap;     /* software/bwamem.c:61 */
+	int min_seed_len;      /* the filter's drop margin (min_seed_len << 1) */
+	float mask_level;      /* software/bwamem.c:63 */
+	float drop_ratio;      /* chain_drop_ratio, software/bwamem.c:64 */
+	int filter;            /* 1: mem_chain_flt after mem_chain */
+} orc_chain_opt_t;
+/* mem_chain (+ mem_chain_flt) of every read; read i's seed sequence is
+ * seeds[seed_off[i] .. seed_off[i+1]).  *out = SMCH stream (orc_free). */
+int orc_chain(int64_t n_reads, const orc_seed_t *seeds, const uint64_t *seed_off, int64_t l_pac,
+		const orc_chain_opt_t *o, int n_threads, uint8_t **out, uint64_t *out_len);
+
 #ifdef __cplusplus
 }
 #endif

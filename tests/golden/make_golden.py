@@ -15,13 +15,22 @@ reference code itself:
   g1.sa.gz            the `bwa index` sampled suffix array (.sa, software/bwt.c:852)
   g1_<case>.smsa.gz   reference bwt_sa() of every seed occurrence of that stream
                       (software/bwamem.c:467-474, max_occ 10000)
+  g1_<case>_<chain>_f<0|1>.smch.gz
+                      reference mem_chain() of every read (software/bwamem.c:593),
+                      without (f0) and with (f1) mem_chain_flt() (software/bwamem.c:629)
   manifest.json       cases, options, sha256 of the uncompressed streams
+
+  g2.*, g2_<case>*     the same for a repeat-dense genome (make_g2)
+
+    python tests/golden/make_golden.py --chains-only   # (re)make only the g1 .smch files
+    python tests/golden/make_golden.py --g2-only       # (re)make only the g2 set
 """
 import gzip
 import hashlib
 import json
 import os
 import shutil
+import subprocess
 import sys
 import tempfile
 
@@ -44,6 +53,127 @@ CASES = [
     dict(name="reseed", n_reads=500, opt=dict(min_seed_len=19, split_factor=1.0, split_width=500, start_width=1)),
     dict(name="k30", n_reads=500, opt=dict(min_seed_len=30, split_factor=2.0, split_width=3, start_width=1)),
 ]
+
+
+# chain option sets (mem_opt_t w / max_chain_gap / mask_level / chain_drop_ratio,
+# software/bwamem.c:53-64); "std" is mem_opt_init's
+CHAIN_OPTS = [
+    dict(name="std", w=100, max_chain_gap=10000, mask_level=0.5, drop_ratio=0.5),
+    dict(name="tight", w=5, max_chain_gap=40, mask_level=0.3, drop_ratio=0.8),
+]
+CHAIN_CASES = {"default": ["std", "tight"], "noexact": ["std"], "k14s20": ["std", "tight"], "reseed": ["std"],
+               "k30": ["std"]}
+
+
+def ref_chain(tmp, smrd, case, copt, filt, genome="g1"):
+    out = os.path.join(tmp, "c.smch")
+    o = case["opt"]
+    subprocess.run([oracle.REF, "chain", os.path.join(tmp, genome + ".bwt"), os.path.join(tmp, genome + ".sa"), smrd,
+                    out,
+                    str(o["min_seed_len"]), str(o["split_factor"]), str(o["split_width"]), str(o["start_width"]),
+                    str(MAX_OCC), str(copt["w"]), str(copt["max_chain_gap"]), str(copt["mask_level"]),
+                    str(copt["drop_ratio"]), str(filt)], check=True)
+    with open(out, "rb") as fh:
+        return fh.read()
+
+
+def make_chains(tmp, reads, manifest):
+    """chain fixtures for every case of the manifest (files g1.bwt / g1.sa in tmp)"""
+    copts = {c["name"]: c for c in CHAIN_OPTS}
+    for case in manifest["cases"]:
+        sub = reads.subset(np.arange(case["n_reads"]))
+        p = os.path.join(tmp, "sub.smrd")
+        synth.write_smrd(p, sub)
+        case["chains"] = []
+        for cname in CHAIN_CASES[case["name"]]:
+            for filt in (0, 1):
+                data = ref_chain(tmp, p, case, copts[cname], filt)
+                fn = f"g1_{case['name']}_{cname}_f{filt}.smch.gz"
+                gz_write(os.path.join(HERE, fn), data)
+                case["chains"].append(dict(copts[cname], file=fn, filter=filt,
+                                           sha256=hashlib.sha256(data).hexdigest()))
+
+
+G2_CASES = [
+    dict(name="default", opt=dict(min_seed_len=19, split_factor=1.5, split_width=10, start_width=1)),
+    dict(name="k14s20", opt=dict(min_seed_len=14, split_factor=1.5, split_width=20, start_width=1)),
+]
+
+
+def make_g2():
+    """g2: a repeat-dense genome (60 % copies of 4 families, tandem and exact
+    repeats) whose reads carry tens to hundreds of seeds and chains, so the
+    chain tree splits to several levels and the chain filter sorts long
+    lists.  Files g2.* and manifest["g2"]."""
+    if not oracle.ref_available():
+        oracle.build(ref=True)
+    tmp = tempfile.mkdtemp()
+    try:
+        genome = synth.make_genome(150_000, seed=21, repeat_frac=0.6, n_families=4, exact_frac=0.01,
+                                   tandem_frac=0.01)
+        fa = os.path.join(tmp, "g2.fa")
+        synth.write_fasta(fa, genome)
+        oracle.ref_index(fa, os.path.join(tmp, "g2"))
+        reads = synth.concat_reads([synth.make_reads(genome.codes, 300, 150, seed=201),
+                                    synth.make_reads(genome.codes, 100, 250, seed=202, sub_rate=0.01),
+                                    synth.make_reads(genome.codes, 100, (15, 200), seed=203, n_rate=0.01)])
+        smrd = os.path.join(tmp, "r2.smrd")
+        synth.write_smrd(smrd, reads)
+        for src, dst in (("g2.fa", "g2.fa.gz"), ("g2.bwt", "g2.bwt.gz"), ("g2.sa", "g2.sa.gz"),
+                         ("r2.smrd", "r2.smrd.gz")):
+            with open(os.path.join(tmp, src), "rb") as fh:
+                gz_write(os.path.join(HERE, dst), fh.read())
+        cases = []
+        copts = {c["name"]: c for c in CHAIN_OPTS}
+        for case in G2_CASES:
+            out = os.path.join(tmp, case["name"] + ".smgo")
+            oracle.ref_smem(os.path.join(tmp, "g2.bwt"), smrd, out, **case["opt"])
+            with open(out, "rb") as fh:
+                data = fh.read()
+            gz_write(os.path.join(HERE, f"g2_{case['name']}.smgo.gz"), data)
+            sa_out = os.path.join(tmp, case["name"] + ".smsa")
+            oracle.ref_sa(os.path.join(tmp, "g2.bwt"), os.path.join(tmp, "g2.sa"), out, sa_out,
+                          min_seed_len=case["opt"]["min_seed_len"], max_occ=MAX_OCC)
+            with open(sa_out, "rb") as fh:
+                sa_data = fh.read()
+            gz_write(os.path.join(HERE, f"g2_{case['name']}.smsa.gz"), sa_data)
+            c = dict(case, n_reads=reads.n, sha256=hashlib.sha256(data).hexdigest(), max_occ=MAX_OCC,
+                     sa_sha256=hashlib.sha256(sa_data).hexdigest(), chains=[])
+            for cname in ("std", "tight"):
+                for filt in (0, 1):
+                    cd = ref_chain(tmp, smrd, case, copts[cname], filt, genome="g2")
+                    fn = f"g2_{case['name']}_{cname}_f{filt}.smch.gz"
+                    gz_write(os.path.join(HERE, fn), cd)
+                    c["chains"].append(dict(copts[cname], file=fn, filter=filt,
+                                            sha256=hashlib.sha256(cd).hexdigest()))
+            cases.append(c)
+        with open(os.path.join(HERE, "manifest.json")) as fh:
+            manifest = json.load(fh)
+        manifest["g2"] = {"genome": dict(n_bp=150_000, seed=21, repeat_frac=0.6, n_families=4), "cases": cases}
+        with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+            json.dump(manifest, fh, indent=1)
+    finally:
+        shutil.rmtree(tmp)
+
+
+def chains_only():
+    if not oracle.ref_available():
+        oracle.build(ref=True)
+    tmp = tempfile.mkdtemp()
+    try:
+        for name in ("g1.bwt", "g1.sa"):
+            with gzip.open(os.path.join(HERE, name + ".gz"), "rb") as fh, open(os.path.join(tmp, name), "wb") as o:
+                o.write(fh.read())
+        with gzip.open(os.path.join(HERE, "r1.smrd.gz"), "rb") as fh, open(os.path.join(tmp, "r1.smrd"), "wb") as o:
+            o.write(fh.read())
+        reads = synth.read_smrd(os.path.join(tmp, "r1.smrd"))
+        with open(os.path.join(HERE, "manifest.json")) as fh:
+            manifest = json.load(fh)
+        make_chains(tmp, reads, manifest)
+        with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+            json.dump(manifest, fh, indent=1)
+    finally:
+        shutil.rmtree(tmp)
 
 
 def make_reads(g):
@@ -108,6 +238,7 @@ def main():
                                           n_calls=int(sum(len(r) for r in parsed)),
                                           max_occ=MAX_OCC, sa_sha256=hashlib.sha256(sa_data).hexdigest(),
                                           n_occ=int(sum(p.size for p in synth.read_smsa(sa_data)))))
+        make_chains(tmp, reads, manifest)
         with open(os.path.join(HERE, "manifest.json"), "w") as fh:
             json.dump(manifest, fh, indent=1)
         print(json.dumps(manifest, indent=1))
@@ -116,4 +247,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--chains-only" in sys.argv:
+        chains_only()
+    elif "--g2-only" in sys.argv:
+        make_g2()
+    else:
+        main()
+        make_g2()

@@ -75,3 +75,61 @@ def load() -> Fixture:
             index = smemgpu.Index.read(b)
         _cache = Fixture(manifest, genome, bwt_bytes, reads, index)
     return _cache
+
+
+# ------------------------------------------------------------ chains (+ g2)
+def gz(name: str) -> bytes:
+    return _gz(name)
+
+
+def genome_cases(genome: str):
+    """the seeding cases of a golden genome ("g1" or the repeat-dense "g2")"""
+    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+        m = json.load(fh)
+    return m["cases"] if genome == "g1" else m["g2"]["cases"]
+
+
+def chain_fixtures():
+    """every (genome, seeding case, chain option set + filter) with a reference
+    SMCH stream"""
+    out = []
+    for g in ("g1", "g2"):
+        for c in genome_cases(g):
+            for ch in c.get("chains", []):
+                out.append((g, c, ch))
+    return out
+
+
+def l_pac(genome: str) -> int:
+    import struct
+    return struct.unpack_from("<5Q", _gz(f"{genome}.bwt.gz"), 0)[4] // 2
+
+
+def smgo(genome: str, case) -> bytes:
+    data = _gz(f"{genome}_{case['name']}.smgo.gz")
+    assert hashlib.sha256(data).hexdigest() == case["sha256"], "fixture corrupted"
+    return data
+
+
+def smsa(genome: str, case) -> bytes:
+    data = _gz(f"{genome}_{case['name']}.smsa.gz")
+    assert hashlib.sha256(data).hexdigest() == case["sa_sha256"], "fixture corrupted"
+    return data
+
+
+def smch(chain) -> bytes:
+    data = _gz(chain["file"])
+    assert hashlib.sha256(data).hexdigest() == chain["sha256"], "fixture corrupted"
+    return data
+
+
+def files(genome: str, d: str):
+    """write the genome's .bwt / .sa / reads into directory d; returns the paths"""
+    reads = "r1.smrd" if genome == "g1" else "r2.smrd"
+    out = {}
+    for name in (f"{genome}.bwt", f"{genome}.sa", reads):
+        p = os.path.join(d, name)
+        with open(p, "wb") as fh:
+            fh.write(_gz(name + ".gz"))
+        out[name.split(".")[-1]] = p
+    return out

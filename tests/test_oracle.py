@@ -193,3 +193,48 @@ def test_no_device_is_an_error_not_a_fallback(built):
     idx = smemgpu.Index.build(synth.make_genome(2000, seed=1).codes)
     with pytest.raises(smemgpu.SmemError, match="SMEM_E_DEVICE"):
         smemgpu.Gpu(idx, device=0)
+
+
+CHAINS = golden_data.chain_fixtures()
+
+
+@pytest.mark.parametrize("g,case,ch", CHAINS, ids=[c["file"].split(".")[0] for _, _, c in CHAINS])
+def test_oracle_chains_match_reference_golden(g, case, ch):
+    """mem_chain (+ mem_chain_flt) restated (oracle/chain_oracle.c) over the
+    golden seed sequence == the compiled reference's chains, byte for byte."""
+    from smemgpu import synth
+    lists = synth.read_smgo(golden_data.smgo(g, case))
+    pos = synth.read_smsa(golden_data.smsa(g, case))
+    seeds, off = oracle.chain_seeds(lists, pos, case["opt"]["min_seed_len"], case["max_occ"])
+    got = oracle.chain(seeds, off, golden_data.l_pac(g), w=ch["w"], max_chain_gap=ch["max_chain_gap"],
+                       min_seed_len=case["opt"]["min_seed_len"], mask_level=ch["mask_level"],
+                       drop_ratio=ch["drop_ratio"], filter=ch["filter"], threads=4)
+    assert got == golden_data.smch(ch)
+
+
+def test_g2_fixture_is_repeat_dense():
+    """g2 exists to reach multi-level chain trees, long filter sorts and
+    duplicate chain keys; keep it that way"""
+    from smemgpu import synth
+    g, case, ch = [x for x in CHAINS if x[0] == "g2" and x[2]["name"] == "tight" and x[2]["filter"] == 0][0]
+    chains = synth.read_smch(golden_data.smch(ch))
+    assert max(len(r) for r in chains) > 120          # three tree levels
+    assert sum(len(r) - len({p for p, _ in r}) for r in chains) > 0
+
+
+def test_oracle_g2_streams_match_reference(tmp_path):
+    """the restated seeding loop and bwt_sa on the repeat-dense genome"""
+    from smemgpu import synth
+    p = golden_data.files("g2", str(tmp_path))
+    oi = oracle.OracleIndex(p["bwt"])
+    osa = oracle.OracleSA(p["sa"])
+    reads = synth.read_smrd(p["smrd"])
+    for case in golden_data.genome_cases("g2"):
+        data, _, _ = oracle.seed(oi, reads.codes, reads.offs, threads=4, **case["opt"])
+        assert data == golden_data.smgo("g2", case)
+        lists = synth.read_smgo(data)
+        _, k = oracle.sa_queries(lists, case["opt"]["min_seed_len"], case["max_occ"])
+        exp = np.concatenate(synth.read_smsa(golden_data.smsa("g2", case)))
+        assert np.array_equal(osa.lookup(oi, k), exp)
+    osa.close()
+    oi.close()
