@@ -1,0 +1,84 @@
+// Seed chaining on the device: mem_chain's tree
+// insertion loop and mem_chain_flt, one lane per read, over the SA positions
+// smem_batch_sa left in HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smem {
+
+// mem_seed_t (software/bwamem.c:317-320)
+struct SeedRec {
+    int64_t rbeg;
+    int32_t qbeg, len;
+};
+
+// a chain while it grows: its first seed (pos = first rbeg, first_qbeg) and
+// last seed (what test_and_merge reads, software/bwamem.c:334-354); seeds
+// are linked through ChainParams::next by occurrence index
+struct ChainRec {
+    int64_t pos, last_rbeg;
+    int32_t first_qbeg, last_qbeg, last_len, n;
+    uint32_t first, last;
+};
+
+// kbtree(chn) node at KB_DEFAULT_SIZE: t = 8, at most 15 keys / 16 children
+// (software/kbtree.h:52-60, 369); children are node indices in the read's pool
+constexpr int BT_T = 8;
+constexpr int BT_MAX = 2 * BT_T - 1;
+constexpr uint32_t BT_NONE = 0xffffffffu;
+struct BNode {
+    int64_t key[BT_MAX];
+    int32_t n, leaf;
+    uint32_t id[BT_MAX];
+    uint32_t child[BT_MAX + 1];
+    uint32_t pad[1];
+};
+static_assert(sizeof(BNode) == 256, "BNode is one 256-B record");
+
+// flt_aux_t of mem_chain_flt (software/bwamem.c:619-624); p, p2 are chain
+// positions, p2 = -1 for none
+struct FltRec {
+    int32_t beg, end, w, p, p2;
+};
+
+// one chain of the output: its seeds are seeds[seed_off .. seed_off + n)
+struct OutChain {
+    int64_t pos;
+    uint64_t seed_off;
+    int32_t n, pad;
+};
+
+struct ChainParams {
+    // inputs: the batch's flat intervals (x0, x1, x2, info) and bwt_sa results
+    const uint64_t* intv;      // 4 words per interval
+    const uint64_t* intv_off;  // [n_reads + 1]
+    const uint64_t* occ_off;   // [n_intv + 1], occurrences of kept intervals
+    const uint64_t* pos;       // [n_occ]
+    int n_reads;
+    int64_t l_pac;
+    int w, max_chain_gap, min_seed_len, filter;
+    float mask_level, drop_ratio;
+    // scratch, indexed by occurrence (a read owns [occ_off[intv_off[r]], ...))
+    SeedRec* seed;
+    uint32_t* next;
+    ChainRec* chn;
+    BNode* node;               // read r's pool starts at occ_begin / 7 + 3 r
+    uint32_t* ord;             // tree order
+    uint32_t* ord2;            // filtered order
+    FltRec* flt;
+    uint64_t* n_out;           // [n_reads] chains kept
+    uint64_t* ns_out;          // [n_reads] seeds in them
+    // output (write kernel)
+    const uint64_t* chain_off; // [n_reads + 1]
+    const uint64_t* seed_off;  // [n_reads + 1]
+    OutChain* out_chain;
+    SeedRec* out_seed;
+};
+
+}  // namespace smem
+
+extern "C" {
+hipError_t smem_launch_chain_build(const smem::ChainParams* P, hipStream_t st);
+hipError_t smem_launch_chain_write(const smem::ChainParams* P, hipStream_t st);
+}

@@ -23,6 +23,7 @@
 
 #include "smem_gpu.h"
 #include "smem_kernels.h"
+#include "chain_kernels.h"
 
 using smem::CallRec;
 using smem::Intv;
@@ -154,6 +155,20 @@ struct smem_batch {
     HostBuf<uint64_t> h_occ_off, h_sa_pos;
     bool sa_ran = false, sa_fetched = false;
     uint64_t tot_occ = 0;
+    int sa_min_seed_len = 0;
+    // chains (smem_batch_chain)
+    DevBuf<smem::SeedRec> d_seed, d_out_seed;
+    DevBuf<uint32_t> d_next, d_ord, d_ord2;
+    DevBuf<smem::ChainRec> d_chn;
+    DevBuf<smem::BNode> d_node;
+    DevBuf<smem::FltRec> d_flt;
+    DevBuf<uint64_t> d_n_out, d_ns_out, d_chain_off, d_seed_off;
+    DevBuf<smem::OutChain> d_out_chain;
+    HostBuf<uint64_t> h_chain_off;
+    HostBuf<smem::OutChain> h_out_chain;
+    HostBuf<smem::SeedRec> h_out_seed;
+    bool chain_ran = false, chain_fetched = false;
+    uint64_t tot_chains = 0, tot_seeds = 0;
     smem_batch_stats_t stats{};
 };
 
@@ -261,7 +276,11 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
     b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
     b->d_occ_n.release(); b->d_occ_off.release(); b->d_sa_pos.release(); b->d_sa_tmp.release();
-    b->d_kstart.release();
+    b->d_kstart.release(); b->h_occ_off.release(); b->h_sa_pos.release();
+    b->d_seed.release(); b->d_out_seed.release(); b->d_next.release(); b->d_ord.release(); b->d_ord2.release();
+    b->d_chn.release(); b->d_node.release(); b->d_flt.release(); b->d_n_out.release(); b->d_ns_out.release();
+    b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release();
+    b->h_chain_off.release(); b->h_out_chain.release(); b->h_out_seed.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
     b->h_intv_off.release(); b->h_call_off.release();
     for (auto& ev : b->ev)
@@ -322,7 +341,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     if (e == hipSuccess) e = b->d_intv_off.ensure(R + 1);
     if (e == hipSuccess) e = b->d_call_off.ensure(R + 1);
     if (e == hipSuccess) e = b->h_ctr.ensure(8);
-    if (e == hipSuccess) e = b->h_tot.ensure(4);
+    if (e == hipSuccess) e = b->h_tot.ensure(8);
     if (e == hipSuccess) e = b->h_intv_off.ensure(R + 1);
     if (e == hipSuccess) e = b->h_call_off.ensure(R + 1);
     if (e == hipSuccess) {
@@ -416,6 +435,8 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->sa_ran = false;
     b->sa_fetched = false;
     b->tot_occ = 0;
+    b->chain_ran = b->chain_fetched = false;
+    b->tot_chains = b->tot_seeds = 0;
     b->stats = smem_batch_stats_t{};
     b->stats.block = 256;
     smem::SeedParams P;
@@ -559,9 +580,23 @@ int smem_batch_fetch(smem_batch_t* b) {
             HIP_TRY(hipMemcpyAsync(b->h_sa_pos.p, b->d_sa_pos.p, sizeof(uint64_t) * b->tot_occ, hipMemcpyDeviceToHost,
                                    b->st));
     }
+    if (b->chain_ran) {
+        HIP_TRY(b->h_chain_off.ensure(n + 1));
+        HIP_TRY(b->h_out_chain.ensure(std::max<uint64_t>(b->tot_chains, 1)));
+        HIP_TRY(b->h_out_seed.ensure(std::max<uint64_t>(b->tot_seeds, 1)));
+        HIP_TRY(hipMemcpyAsync(b->h_chain_off.p, b->d_chain_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost,
+                               b->st));
+        if (b->tot_chains)
+            HIP_TRY(hipMemcpyAsync(b->h_out_chain.p, b->d_out_chain.p, sizeof(smem::OutChain) * b->tot_chains,
+                                   hipMemcpyDeviceToHost, b->st));
+        if (b->tot_seeds)
+            HIP_TRY(hipMemcpyAsync(b->h_out_seed.p, b->d_out_seed.p, sizeof(smem::SeedRec) * b->tot_seeds,
+                                   hipMemcpyDeviceToHost, b->st));
+    }
     HIP_TRY(hipStreamSynchronize(b->st));
     b->fetched = true;
     b->sa_fetched = b->sa_ran;
+    b->chain_fetched = b->chain_ran;
     return SMEM_OK;
 }
 
@@ -665,6 +700,102 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     b->stats.n_occ = b->tot_occ;
     b->sa_ran = true;
     b->sa_fetched = false;
+    b->sa_min_seed_len = min_seed_len;
+    b->chain_ran = b->chain_fetched = false;
+    return SMEM_OK;
+}
+
+void smem_chain_opt_default(smem_chain_opt_t* o) {
+    if (!o) return;
+    o->w = 100;                   // software/bwamem.c:53
+    o->max_chain_gap = 10000;     // software/bwamem.c:61
+    o->mask_level = 0.50f;        // software/bwamem.c:63
+    o->chain_drop_ratio = 0.50f;  // software/bwamem.c:64
+    o->filter = 1;                // mem_align1_core runs mem_chain_flt (software/bwamem.c:1449)
+}
+
+int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt) {
+    g_err[0] = 0;
+    if (!b || !b->sa_ran) return fail(SMEM_E_ARG, "smem_batch_chain: run smem_batch_sa first");
+    if (!opt || l_pac < 0 || opt->w < 0) return fail(SMEM_E_ARG, "smem_batch_chain: bad options");
+    if (b->tot_occ >= (1ull << 32) - 1) return fail(SMEM_E_CAPACITY, "smem_batch_chain: too many seed occurrences");
+    HIP_TRY(hipSetDevice(b->g->device));
+    const int n = b->n_reads;
+    const uint64_t no = std::max<uint64_t>(b->tot_occ, 1);
+    HIP_TRY(b->d_seed.ensure(no));
+    HIP_TRY(b->d_next.ensure(no));
+    HIP_TRY(b->d_chn.ensure(no));
+    HIP_TRY(b->d_node.ensure(b->tot_occ / 7 + 3ull * (uint64_t)n + 8));
+    HIP_TRY(b->d_ord.ensure(no));
+    HIP_TRY(b->d_ord2.ensure(no));
+    HIP_TRY(b->d_flt.ensure(opt->filter ? no : 1));
+    HIP_TRY(b->d_n_out.ensure(std::max(n, 1)));
+    HIP_TRY(b->d_ns_out.ensure(std::max(n, 1)));
+    HIP_TRY(b->d_chain_off.ensure(n + 1));
+    HIP_TRY(b->d_seed_off.ensure(n + 1));
+    size_t tmp = 0;
+    HIP_TRY(smem_launch_offsets(nullptr, nullptr, std::max(n, 1), nullptr, &tmp, b->st));
+    HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
+    smem::ChainParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.intv = reinterpret_cast<const uint64_t*>(b->d_flat_intv.p);
+    P.intv_off = b->d_intv_off.p;
+    P.occ_off = b->d_occ_off.p;
+    P.pos = b->d_sa_pos.p;
+    P.n_reads = n;
+    P.l_pac = l_pac;
+    P.w = opt->w;
+    P.max_chain_gap = opt->max_chain_gap;
+    P.min_seed_len = b->sa_min_seed_len;
+    P.filter = opt->filter ? 1 : 0;
+    P.mask_level = opt->mask_level;
+    P.drop_ratio = opt->chain_drop_ratio;
+    P.seed = b->d_seed.p;
+    P.next = b->d_next.p;
+    P.chn = b->d_chn.p;
+    P.node = b->d_node.p;
+    P.ord = b->d_ord.p;
+    P.ord2 = b->d_ord2.p;
+    P.flt = b->d_flt.p;
+    P.n_out = b->d_n_out.p;
+    P.ns_out = b->d_ns_out.p;
+    P.chain_off = b->d_chain_off.p;
+    P.seed_off = b->d_seed_off.p;
+    HIP_TRY(hipEventRecord(b->ev[0], b->st));
+    HIP_TRY(smem_launch_chain_build(&P, b->st));
+    tmp = b->d_sa_tmp.n;
+    HIP_TRY(smem_launch_offsets(b->d_n_out.p, b->d_chain_off.p, n, b->d_sa_tmp.p, &tmp, b->st));
+    tmp = b->d_sa_tmp.n;
+    HIP_TRY(smem_launch_offsets(b->d_ns_out.p, b->d_seed_off.p, n, b->d_sa_tmp.p, &tmp, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_tot.p + 3, b->d_chain_off.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_tot.p + 4, b->d_seed_off.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    b->tot_chains = b->h_tot.p[3];
+    b->tot_seeds = b->h_tot.p[4];
+    HIP_TRY(b->d_out_chain.ensure(std::max<uint64_t>(b->tot_chains, 1)));
+    HIP_TRY(b->d_out_seed.ensure(std::max<uint64_t>(b->tot_seeds, 1)));
+    P.out_chain = b->d_out_chain.p;
+    P.out_seed = b->d_out_seed.p;
+    HIP_TRY(smem_launch_chain_write(&P, b->st));
+    HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
+    b->stats.chain_ms = ms;
+    b->stats.n_chains = b->tot_chains;
+    b->chain_ran = true;
+    b->chain_fetched = false;
+    return SMEM_OK;
+}
+
+int smem_batch_chain_results(const smem_batch_t* b, const smem_chain_t** chains, const uint64_t** chain_off,
+                             const smem_seed_t** seeds, uint64_t* n_chains, uint64_t* n_seeds) {
+    if (!b || !b->chain_fetched) return SMEM_E_ARG;
+    if (chains) *chains = reinterpret_cast<const smem_chain_t*>(b->h_out_chain.p);
+    if (chain_off) *chain_off = b->h_chain_off.p;
+    if (seeds) *seeds = reinterpret_cast<const smem_seed_t*>(b->h_out_seed.p);
+    if (n_chains) *n_chains = b->tot_chains;
+    if (n_seeds) *n_seeds = b->tot_seeds;
     return SMEM_OK;
 }
 

@@ -28,6 +28,7 @@ EXPORTED = [
     "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_batch_debug", "smem_strerror",
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
+    "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results",
 ]
 
 
@@ -57,7 +58,16 @@ class OptT(C.Structure):
 class BatchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
                 ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int),
-                ("sa_ms", C.c_double), ("n_occ", C.c_uint64)]
+                ("sa_ms", C.c_double), ("n_occ", C.c_uint64), ("chain_ms", C.c_double), ("n_chains", C.c_uint64)]
+
+
+class ChainOptT(C.Structure):
+    _fields_ = [("w", C.c_int), ("max_chain_gap", C.c_int), ("mask_level", C.c_float),
+                ("chain_drop_ratio", C.c_float), ("filter", C.c_int)]
+
+
+SEED_DT = np.dtype([("rbeg", "<i8"), ("qbeg", "<i4"), ("len", "<i4")])          # smem_seed_t = mem_seed_t
+CHAIN_DT = np.dtype([("pos", "<i8"), ("seed_off", "<u8"), ("n", "<i4"), ("pad", "<i4")])  # smem_chain_t
 
 
 _lib = None
@@ -88,6 +98,11 @@ def load() -> C.CDLL:
     lib.smem_gpu_load_sa.argtypes = [C.c_void_p, P(SaT)]
     lib.smem_batch_sa.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.smem_batch_sa_results.argtypes = [C.c_void_p, P(P(C.c_uint64)), P(P(C.c_uint64)), P(C.c_uint64)]
+    lib.smem_chain_opt_default.argtypes = [P(ChainOptT)]
+    lib.smem_chain_opt_default.restype = None
+    lib.smem_batch_chain.argtypes = [C.c_void_p, C.c_int64, P(ChainOptT)]
+    lib.smem_batch_chain_results.argtypes = [C.c_void_p, P(C.c_void_p), P(P(C.c_uint64)), P(C.c_void_p),
+                                             P(C.c_uint64), P(C.c_uint64)]
     lib.smem_gpu_device_count.argtypes = []
     lib.smem_gpu_init.argtypes = [P(C.c_void_p), C.c_int, C.c_void_p, C.c_uint64, C.c_uint64, P(C.c_uint64)]
     lib.smem_gpu_shutdown.argtypes = [C.c_void_p]
@@ -255,6 +270,21 @@ class Results:
     call_off: np.ndarray  # (n_reads + 1,) uint64
     occ_off: np.ndarray | None = None  # (N + 1,) uint64, when Batch.sa() ran
     sa_pos: np.ndarray | None = None   # (n_occ,) uint64 bwt_sa positions
+    chains: np.ndarray | None = None   # CHAIN_DT, when Batch.chain() ran
+    chain_off: np.ndarray | None = None  # (n_reads + 1,) uint64
+    seeds: np.ndarray | None = None    # SEED_DT, each chain's seeds contiguous
+
+    def read_chains(self, i: int) -> list:
+        """read i's chains as [(pos, seeds)], in mem_chain(+flt) order."""
+        out = []
+        for c in self.chains[int(self.chain_off[i]):int(self.chain_off[i + 1])]:
+            o = int(c["seed_off"])
+            out.append((int(c["pos"]), self.seeds[o:o + int(c["n"])]))
+        return out
+
+    def to_smch(self) -> bytes:
+        from . import synth
+        return synth.write_smch([self.read_chains(i) for i in range(self.chain_off.size - 1)])
 
     def read_sa(self, i: int) -> np.ndarray:
         """bwt_sa positions of read i's seed occurrences, in interval order."""
@@ -352,6 +382,13 @@ class Batch:
         """bwt_sa of every seed occurrence of the last run (smem_batch_sa)."""
         _check(load().smem_batch_sa(self._h, min_seed_len, max_occ), "smem_batch_sa")
 
+    def chain(self, l_pac: int, w: int = 100, max_chain_gap: int = 10000, mask_level: float = 0.5,
+              drop_ratio: float = 0.5, filter: bool = True) -> None:
+        """mem_chain (+ mem_chain_flt) of every read of the last run, over
+        the positions of the last sa() (smem_batch_chain)."""
+        o = ChainOptT(w, max_chain_gap, mask_level, drop_ratio, int(bool(filter)))
+        _check(load().smem_batch_chain(self._h, int(l_pac), C.byref(o)), "smem_batch_chain")
+
     def debug_words(self, n_words: int) -> np.ndarray:
         out = np.zeros(n_words, dtype=np.uint64)
         rc = load().smem_batch_debug(self._h, out.ctypes.data, n_words)
@@ -382,6 +419,17 @@ class Batch:
             n_occ = int(no.value)
             res.occ_off = np.ctypeslib.as_array(oo, shape=(ni + 1,)).copy()
             res.sa_pos = np.ctypeslib.as_array(pos, shape=(max(n_occ, 1),))[:n_occ].copy()
+        ch, sd = C.c_void_p(), C.c_void_p()
+        cho = C.POINTER(C.c_uint64)()
+        nch, nsd = C.c_uint64(), C.c_uint64()
+        if lib.smem_batch_chain_results(self._h, C.byref(ch), C.byref(cho), C.byref(sd), C.byref(nch),
+                                        C.byref(nsd)) == 0:
+            nc, ns = int(nch.value), int(nsd.value)
+            res.chain_off = np.ctypeslib.as_array(cho, shape=(n + 1,)).copy()
+            res.chains = np.frombuffer((C.c_char * (max(nc, 1) * CHAIN_DT.itemsize)).from_address(ch.value),
+                                       dtype=CHAIN_DT)[:nc].copy()
+            res.seeds = np.frombuffer((C.c_char * (max(ns, 1) * SEED_DT.itemsize)).from_address(sd.value),
+                                      dtype=SEED_DT)[:ns].copy()
         return res
 
     def close(self) -> None:

@@ -164,6 +164,40 @@ int  smem_gpu_load_sa(smem_gpu_t *gpu, const smem_sa_t *sa);
 int  smem_batch_sa(smem_batch_t *b, int min_seed_len, int max_occ);
 int  smem_batch_sa_results(const smem_batch_t *b, const uint64_t **pos, const uint64_t **occ_off, uint64_t *n_occ);
 
+/* ------------------------------------------------------- chaining */
+/* mem_seed_t (software/bwamem.c:317-320) */
+typedef struct {
+	int64_t rbeg;          /* forward-reverse coordinate (bwt_sa) */
+	int32_t qbeg, len;
+} smem_seed_t;
+/* one chain of mem_chain_t (software/bwamem.c:322-326): pos and its n seeds,
+ * seeds[seed_off .. seed_off + n) of smem_batch_chain_results */
+typedef struct {
+	int64_t pos;
+	uint64_t seed_off;
+	int32_t n, pad;
+} smem_chain_t;
+/* the mem_opt_t fields chaining reads (software/bwamem.h:39-53) */
+typedef struct {
+	int w;                    /* band width, 100 */
+	int max_chain_gap;        /* 10000 */
+	float mask_level;         /* 0.50 */
+	float chain_drop_ratio;   /* 0.50 */
+	int filter;               /* 1: mem_chain_flt after mem_chain, as mem_align1_core does */
+} smem_chain_opt_t;
+void smem_chain_opt_default(smem_chain_opt_t *opt);
+/* After smem_batch_sa: mem_chain (software/bwamem.c:593-614) of every read on
+ * the GPU — the seed sequence of mem_insert_seed (software/bwamem.c:462-499),
+ * test_and_merge into the kbtree of chains, in-order chain list — and, when
+ * opt->filter, mem_chain_flt (software/bwamem.c:629-690).  l_pac is the
+ * forward strand length (bns->l_pac).  The filter's drop margin uses the
+ * min_seed_len given to smem_batch_sa.  smem_batch_fetch copies the chains;
+ * smem_batch_chain_results returns them per read: chain_off[n_reads + 1]
+ * into chains[], each chain's seeds contiguous in seeds[]. */
+int  smem_batch_chain(smem_batch_t *b, int64_t l_pac, const smem_chain_opt_t *opt);
+int  smem_batch_chain_results(const smem_batch_t *b, const smem_chain_t **chains, const uint64_t **chain_off,
+                              const smem_seed_t **seeds, uint64_t *n_chains, uint64_t *n_seeds);
+
 /* ---------------------------------------------------------- telemetry */
 typedef struct {
 	double kernel_ms;        /* seeding kernel(s), HIP events on the batch stream */
@@ -174,6 +208,8 @@ typedef struct {
 	int grid, block;         /* launch shape of the seeding kernel */
 	double sa_ms;            /* smem_batch_sa kernels */
 	uint64_t n_occ;          /* seed occurrences resolved by smem_batch_sa */
+	double chain_ms;         /* smem_batch_chain kernels */
+	uint64_t n_chains;       /* chains kept by smem_batch_chain */
 } smem_batch_stats_t;
 int  smem_batch_stats(const smem_batch_t *b, smem_batch_stats_t *st);
 

@@ -1,0 +1,147 @@
+"""GPU parity of the chaining stage, through the C ABI.
+
+Bar: bit-exact — per read, the chains mem_chain returns (kbtree in-order,
+software/bwamem.c:593-614) and, with the filter, what mem_chain_flt keeps
+and in which order (software/bwamem.c:629-690): pos, every seed's rbeg /
+qbeg / len, in order.  Checked against the compiled reference's own chains
+(tests/golden/*.smch.gz: g1 and the repeat-dense g2, two option sets, both
+filter modes) and against the restatement (oracle/chain_oracle.c) on larger
+repeat-rich genomes: deep chain trees, duplicate chain keys, strand
+bridging, long filter sorts, reads without seeds.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests import golden_data
+
+pytestmark = pytest.mark.gpu
+
+CHAINS = golden_data.chain_fixtures()
+
+
+def _chain_kw(ch):
+    return dict(w=ch["w"], max_chain_gap=ch["max_chain_gap"], mask_level=ch["mask_level"],
+                drop_ratio=ch["drop_ratio"], filter=bool(ch["filter"]))
+
+
+@pytest.fixture(scope="module")
+def golden_gpus(gpu_device, tmp_path_factory):
+    import smemgpu
+    from smemgpu import synth
+    out = {}
+    for g in ("g1", "g2"):
+        p = golden_data.files(g, str(tmp_path_factory.mktemp(g)))
+        idx = smemgpu.Index.read(p["bwt"])
+        gpu = smemgpu.Gpu(idx, device=gpu_device)
+        gpu.load_sa(smemgpu.SA.read(p["sa"]))
+        out[g] = (gpu, synth.read_smrd(p["smrd"]))
+    yield out
+    for gpu, _ in out.values():
+        gpu.close()
+
+
+@pytest.mark.parametrize("g,case,ch", CHAINS, ids=[c["file"].split(".")[0] for _, _, c in CHAINS])
+def test_chain_golden_fixture(golden_gpus, g, case, ch):
+    """GPU chains == the reference's mem_chain (+ mem_chain_flt) output."""
+    import smemgpu
+    gpu, reads = golden_gpus[g]
+    reads = reads.subset(np.arange(case["n_reads"]))
+    b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+    try:
+        b.set_reads(reads.codes, reads.offs)
+        b.run(smemgpu.Options(**case["opt"]))
+        b.sa(case["opt"]["min_seed_len"], case["max_occ"])
+        b.chain(golden_data.l_pac(g), **_chain_kw(ch))
+        res = b.fetch()
+        assert res.to_smch() == golden_data.smch(ch)
+        assert b.stats()["n_chains"] == res.chains.size
+    finally:
+        b.close()
+
+
+def _oracle_chains(res, n_reads, l_pac, min_seed_len, max_occ, **kw):
+    lists = [res.read_calls(i) for i in range(n_reads)]
+    pos = [res.read_sa(i) for i in range(n_reads)]
+    seeds, off = oracle.chain_seeds(lists, pos, min_seed_len, max_occ)
+    return oracle.chain(seeds, off, l_pac, min_seed_len=min_seed_len, threads=8, **kw)
+
+
+@pytest.mark.parametrize("opts", [
+    dict(w=100, max_chain_gap=10000, mask_level=0.5, drop_ratio=0.5),
+    dict(w=5, max_chain_gap=40, mask_level=0.3, drop_ratio=0.8),
+    dict(w=0, max_chain_gap=1, mask_level=0.0, drop_ratio=1.0),
+], ids=["std", "tight", "degenerate"])
+@pytest.mark.parametrize("filt", [0, 1])
+def test_chain_vs_oracle_repeat_dense(gpu_device, opts, filt):
+    """A 1 Mbp genome that is 70 % diverged copies of 6 families plus
+    tandem/exact repeats; 6000 mixed reads, max_occ 10000: hundreds of chains
+    per read in places (three-level trees, long filter sorts)."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(1_000_000, seed=71, repeat_frac=0.7, n_families=6, exact_frac=0.02, tandem_frac=0.01)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        reads = synth.concat_reads([synth.make_reads(g.codes, 4000, 150, seed=72, sub_rate=0.01),
+                                    synth.make_reads(g.codes, 1000, (10, 300), seed=73, n_rate=0.01),
+                                    synth.make_reads(g.codes, 1000, 101, seed=74, random_frac=0.3)])
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        b.sa(19, 10000)
+        l_pac = idx.seq_len // 2
+        b.chain(l_pac, filter=bool(filt), **opts)
+        res = b.fetch()
+        want = _oracle_chains(res, reads.n, l_pac, 19, 10000, filter=filt, **opts)
+        assert res.to_smch() == want
+        per = [len(res.read_chains(i)) for i in range(reads.n)]
+        assert max(per) > 120  # the tree splits to three levels somewhere
+        b.close()
+    finally:
+        gpu.close()
+
+
+def test_chain_strand_bridging_and_empty(gpu_device):
+    """Reads across the forward/reverse boundary (seeds skipped by
+    software/bwamem.c:477), reads with no seeds, and an empty batch."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(40_000, seed=75, n_chrom=1)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        G = g.codes
+        tail_head = np.concatenate([G[-80:], (3 - G[-80:])[::-1][:70]])  # crosses into the reverse strand
+        parts = [synth.make_reads(G, 300, 150, seed=76), synth.make_reads(G, 50, 12, seed=77)]
+        reads = synth.concat_reads(parts)
+        codes = np.concatenate([reads.codes, tail_head.astype(np.uint8), np.zeros(0, np.uint8)])
+        offs = np.concatenate([reads.offs, [reads.offs[-1] + tail_head.size, reads.offs[-1] + tail_head.size]])
+        n = offs.size - 1
+        b = gpu.batch(n, codes.size, 150)
+        b.set_reads(codes, offs)
+        b.run()
+        b.sa(19, 10000)
+        l_pac = idx.seq_len // 2
+        for filt in (0, 1):
+            b.chain(l_pac, filter=bool(filt))
+            res = b.fetch()
+            assert res.to_smch() == _oracle_chains(res, n, l_pac, 19, 10000, filter=filt)
+        assert len(res.read_chains(n - 1)) == 0
+        b.close()
+        e = gpu.batch(1, 1, 1)
+        e.set_reads(np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+        e.run()
+        e.sa()
+        e.chain(l_pac)
+        res = e.fetch()
+        assert res.chains.size == 0 and res.chain_off.tolist() == [0]
+        e.close()
+        f = gpu.batch(4, 600, 150)
+        with pytest.raises(smemgpu.SmemError):
+            f.chain(l_pac)  # before run / sa
+        f.close()
+    finally:
+        gpu.close()
