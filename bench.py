@@ -245,6 +245,24 @@ def sa_lookup(batch, opt, reps: int = 3) -> dict:
                     ".sa sa_intv 32, device copy densified to every 4th row at load"}
 
 
+def chain_report(batch, opt, l_pac: int, reps: int = 3) -> dict:
+    """The stage after bwt_sa: mem_chain + mem_chain_flt of
+    every read of the batch on the GPU (software/bwamem.c:593-690), over the
+    SA positions left in HBM; reported beside the SMEM metric."""
+    batch.run(opt)
+    batch.sa(opt.min_seed_len, 10000)
+    best = None
+    for _ in range(reps):
+        batch.chain(l_pac)
+        st = batch.stats()
+        if best is None or st["chain_ms"] < best["chain_ms"]:
+            best = st
+    n = batch.n_reads
+    return {"ms_per_batch": round(best["chain_ms"], 3), "chains": int(best["n_chains"]),
+            "seed_occurrences": int(best["n_occ"]), "reads_per_s": round(n / (best["chain_ms"] * 1e-3), 1),
+            "what": "mem_chain (kbtree of chains, test_and_merge) + mem_chain_flt, w 100, max_chain_gap 10000"}
+
+
 def main():
     args = parse()
     import torch
@@ -319,6 +337,7 @@ def main():
     value, elapsed_max = aggregate(d, elapsed, reads.n, args.steps)
     pcie = pcie_inclusive(batch, reads, opt) if rank == 0 else None
     sa_rep = sa_lookup(batch, opt) if rank == 0 else None
+    chain_rep = chain_report(batch, opt, idx.seq_len // 2) if rank == 0 else None
 
     if rank == 0:
         bpr, bpr64, ostats, n_counted = algorithmic_bytes(args, idx, reads)
@@ -378,6 +397,7 @@ def main():
             "compact_ms": round(compact_alone, 3),
             "pcie_inclusive_reads_per_s": round(pcie, 1),
             "sa_lookup": sa_rep,
+            "chaining": chain_rep,
             "overflow_reads": st["n_overflow"],
         }
         print(json.dumps(out), flush=True)

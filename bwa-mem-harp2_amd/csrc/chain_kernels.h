@@ -28,6 +28,7 @@ constexpr int BT_T = 8;
 constexpr int BT_MAX = 2 * BT_T - 1;
 constexpr uint32_t BT_NONE = 0xffffffffu;
 struct BNode {
+    static constexpr uint32_t MAX_ID = 0xfffffff0u;
     int64_t key[BT_MAX];
     int32_t n, leaf;
     uint32_t id[BT_MAX];
@@ -35,6 +36,17 @@ struct BNode {
     uint32_t pad[1];
 };
 static_assert(sizeof(BNode) == 256, "BNode is one 256-B record");
+// the same node with 16-bit chain ids and children (the heavy path's LDS
+// pool: 184 B, 835 nodes in 150 KB)
+struct LNode {
+    static constexpr uint32_t MAX_ID = 0xffffu;
+    int64_t key[BT_MAX];
+    uint16_t id[BT_MAX];
+    uint16_t child[BT_MAX + 1];
+    uint8_t n, leaf;
+    uint8_t pad[6];
+};
+static_assert(sizeof(LNode) == 192, "LNode size");
 
 // flt_aux_t of mem_chain_flt (software/bwamem.c:619-624); p, p2 are chain
 // positions, p2 = -1 for none
@@ -69,6 +81,14 @@ struct ChainParams {
     FltRec* flt;
     uint64_t* n_out;           // [n_reads] chains kept
     uint64_t* ns_out;          // [n_reads] seeds in them
+    // reads with more than heavy_min occurrences go to chain_heavy_kernel:
+    // heavy[0 .. ) giants (> giant_min), heavy[n_reads .. ) the rest;
+    // heavy_ctr = {giants, rest, claimed}
+    uint32_t heavy_min, giant_min;
+    uint32_t* heavy;           // [2 n_reads]
+    uint32_t* heavy_ctr;       // [4]
+    uint32_t lds_bytes;        // dynamic LDS of chain_heavy_kernel
+    uint64_t* dbg;             // optional phase clocks of the heavy path (16 words per item)
     // output (write kernel)
     const uint64_t* chain_off; // [n_reads + 1]
     const uint64_t* seed_off;  // [n_reads + 1]
@@ -79,6 +99,6 @@ struct ChainParams {
 }  // namespace smem
 
 extern "C" {
-hipError_t smem_launch_chain_build(const smem::ChainParams* P, hipStream_t st);
-hipError_t smem_launch_chain_write(const smem::ChainParams* P, hipStream_t st);
+hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_cu, hipStream_t st);
+hipError_t smem_launch_chain_write(const smem::ChainParams* P, int n_cu, hipStream_t st);
 }

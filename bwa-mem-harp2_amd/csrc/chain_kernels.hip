@@ -14,24 +14,36 @@
 namespace smem {
 namespace {
 
+// The chain tree in two node formats with one code path: BNode (u32 ids and
+// children, HBM pools) and LNode (u16, the LDS pool of the heavy path).
+
 // leftmost key == k (eq) or else the last key < k (-1 if none): kbtree's
-// __kb_getp_aux (software/kbtree.h:97-110); keys are sorted, so that is the
-// count of keys below k, all 15 loaded independently
-__device__ __forceinline__ int node_find(const BNode* x, int64_t k, bool& eq) {
+// __kb_getp_aux (software/kbtree.h:97-110).  Keys are sorted, so that is the
+// count of keys below k; all 15 are loaded unconditionally (the slots past n
+// are ignored) so the loads issue together.
+template <class N>
+__device__ __forceinline__ int node_find(const N* x, int64_t k, bool& eq) {
     const int n = x->n;
+    int64_t kv[BT_MAX];
+#pragma unroll
+    for (int i = 0; i < BT_MAX; ++i) kv[i] = x->key[i];
     int below = 0;
 #pragma unroll
-    for (int i = 0; i < BT_MAX; ++i) below += (i < n && x->key[i] < k) ? 1 : 0;
-    eq = below < n && x->key[below] == k;
+    for (int i = 0; i < BT_MAX; ++i) below += (i < n) & (kv[i] < k);
+    int64_t at = kv[0];
+#pragma unroll
+    for (int i = 1; i < BT_MAX; ++i) at = below == i ? kv[i] : at;
+    eq = below < n && at == k;
     return eq ? below : below - 1;
 }
 
 // kb_intervalp's `lower` (software/kbtree.h:150-166)
-__device__ int tree_lower(const BNode* pool, uint32_t root, int64_t k) {
+template <class N>
+__device__ __forceinline__ int tree_lower(const N* pool, uint32_t root, int64_t k) {
     uint32_t x = root;
     int lower = -1;
     for (;;) {
-        const BNode* nd = pool + x;
+        const N* nd = pool + x;
         bool eq;
         const int i = node_find(nd, k, eq);
         if (i >= 0 && eq) return (int)nd->id[i];
@@ -41,18 +53,20 @@ __device__ int tree_lower(const BNode* pool, uint32_t root, int64_t k) {
     }
 }
 
-__device__ __forceinline__ void node_init(BNode* x, int leaf) {
+template <class N>
+__device__ __forceinline__ void node_init(N* x, int leaf) {
     x->n = 0;
     x->leaf = leaf;
 }
 
 // __kb_split (software/kbtree.h:172-186): full child y = x.child[i] keeps its
 // lower 7 keys, a new right sibling takes the upper 7, the middle moves up
-__device__ void node_split(BNode* pool, uint32_t xi, int i, uint32_t yi, uint32_t& n_nodes) {
-    BNode* x = pool + xi;
-    BNode* y = pool + yi;
+template <class N>
+__device__ __forceinline__ void node_split(N* pool, uint32_t xi, int i, uint32_t yi, uint32_t& n_nodes) {
+    N* x = pool + xi;
+    N* y = pool + yi;
     const uint32_t zi = n_nodes++;
-    BNode* z = pool + zi;
+    N* z = pool + zi;
     node_init(z, y->leaf);
     z->n = BT_T - 1;
     for (int j = 0; j < BT_T - 1; ++j) {
@@ -75,7 +89,8 @@ __device__ void node_split(BNode* pool, uint32_t xi, int i, uint32_t yi, uint32_
 }
 
 // kb_putp (software/kbtree.h:188-224)
-__device__ void tree_insert(BNode* pool, uint32_t& root, uint32_t& n_nodes, uint32_t id, int64_t k) {
+template <class N>
+__device__ __forceinline__ void tree_insert(N* pool, uint32_t& root, uint32_t& n_nodes, uint32_t id, int64_t k) {
     uint32_t x = root;
     bool eq;
     if (pool[x].n == BT_MAX) {
@@ -94,7 +109,7 @@ __device__ void tree_insert(BNode* pool, uint32_t& root, uint32_t& n_nodes, uint
         }
         x = pool[x].child[i];
     }
-    BNode* nd = pool + x;
+    N* nd = pool + x;
     const int i = node_find(nd, k, eq);
     for (int j = nd->n - 1; j >= i + 1; --j) {
         nd->key[j + 1] = nd->key[j];
@@ -106,7 +121,8 @@ __device__ void tree_insert(BNode* pool, uint32_t& root, uint32_t& n_nodes, uint
 }
 
 // __kb_traverse (software/kbtree.h:336-358): in-order chain ids into out
-__device__ int tree_inorder(const BNode* pool, uint32_t root, uint32_t* out) {
+template <class N>
+__device__ __forceinline__ int tree_inorder(const N* pool, uint32_t root, uint32_t* out) {
     uint32_t sx[24];
     int si[24];
     int top = 0, n_out = 0;
@@ -114,8 +130,8 @@ __device__ int tree_inorder(const BNode* pool, uint32_t root, uint32_t* out) {
     si[0] = 0;
     for (;;) {
         while (sx[top] != BT_NONE && si[top] <= pool[sx[top]].n) {
-            const BNode* nd = pool + sx[top];
-            sx[top + 1] = nd->leaf ? BT_NONE : nd->child[si[top]];
+            const N* nd = pool + sx[top];
+            sx[top + 1] = nd->leaf ? BT_NONE : (uint32_t)nd->child[si[top]];
             si[top + 1] = 0;
             ++top;
         }
@@ -129,7 +145,7 @@ __device__ int tree_inorder(const BNode* pool, uint32_t root, uint32_t* out) {
 
 // mem_chain_weight (software/bwamem.c:501-521), the second loop's `end`
 // advanced by query coordinates as the reference writes it
-__device__ int chain_weight(const ChainRec& c, const SeedRec* seed, const uint32_t* next) {
+__device__ __forceinline__ int chain_weight(const ChainRec& c, const SeedRec* seed, const uint32_t* next) {
     int64_t end = 0;
     int w = 0;
     uint32_t o = c.first;
@@ -158,12 +174,12 @@ __device__ __forceinline__ void flt_swap(FltRec* a, size_t i, size_t j) {
     a[j] = t;
 }
 
-__device__ void flt_insertsort(FltRec* a, size_t n) {
+__device__ __forceinline__ void flt_insertsort(FltRec* a, size_t n) {
     for (size_t i = 1; i < n; ++i)
         for (size_t j = i; j > 0 && flt_lt(a[j], a[j - 1]); --j) flt_swap(a, j, j - 1);
 }
 
-__device__ void flt_combsort(FltRec* a, size_t n) {
+__device__ __forceinline__ void flt_combsort(FltRec* a, size_t n) {
     const double shrink = 1.2473309501039786540366528676643;
     size_t gap = n;
     bool swapped;
@@ -183,7 +199,7 @@ __device__ void flt_combsort(FltRec* a, size_t n) {
 }
 
 // ks_introsort(mem_flt) (software/ksort.h:176-224), comparison for comparison
-__device__ void flt_sort(FltRec* a, size_t n) {
+__device__ __forceinline__ void flt_sort(FltRec* a, size_t n) {
     size_t sl[64], sr[64];
     int sd[64];
     int top = 0, d;
@@ -250,35 +266,41 @@ __device__ void flt_sort(FltRec* a, size_t n) {
     }
 }
 
-}  // namespace
+// Where mem_insert_seed's loop over a read stands (software/bwamem.c:462-499).
+struct InsState {
+    uint64_t iv, o;               // next interval / occurrence
+    uint32_t n_ch, root, n_nodes;
+};
 
-__global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P.n_reads) return;
-    const uint64_t i0 = P.intv_off[r], i1 = P.intv_off[r + 1];
-    const uint64_t S = P.occ_off[i0], E = P.occ_off[i1];
-    if (S == E) {
-        P.n_out[r] = 0;
-        P.ns_out[r] = 0;
-        return;
-    }
-    BNode* pool = P.node + (S / 7 + 3ull * (uint64_t)r);
+__device__ __forceinline__ void ins_start(InsState& st, const ChainParams& P, uint64_t i0) {
+    st.iv = i0;
+    st.o = P.occ_off[i0];
+    st.n_ch = 0;
+    st.root = 0;
+    st.n_nodes = 1;
+}
+
+// Run the loop over read [i0, i1) (occurrences from S) with the chain tree in
+// `pool` (cap nodes).  false: a new chain would need more nodes than cap;
+// `st` then names the seed to resume at (nothing of it has been applied).
+template <class N>
+__device__ __forceinline__ bool insert_read(const ChainParams& P, uint64_t i1, uint64_t S, N* pool, uint32_t cap,
+                                            InsState& st) {
     ChainRec* chn = P.chn + S;
-    uint32_t root = 0, n_nodes = 1, n_ch = 0;
-    node_init(pool, 1);
-    // the seed loop of mem_insert_seed (software/bwamem.c:462-499)
-    for (uint64_t iv = i0; iv < i1; ++iv) {
-        const uint64_t a = P.occ_off[iv], b = P.occ_off[iv + 1];
-        if (a == b) continue;
-        const uint64_t info = P.intv[iv * 4 + 3];
+    if (st.n_nodes == 1 && st.n_ch == 0) node_init(pool, 1);
+    for (; st.iv < i1; ++st.iv) {
+        const uint64_t b = P.occ_off[st.iv + 1];
+        if (st.o >= b) continue;
+        const uint64_t info = P.intv[st.iv * 4 + 3];
         const int32_t qbeg = (int32_t)(info >> 32);
         const int32_t len = (int32_t)((uint32_t)info - (uint32_t)(info >> 32));
-        for (uint64_t o = a; o < b; ++o) {
+        for (; st.o < b; ++st.o) {
+            const uint64_t o = st.o;
             const int64_t rb = (int64_t)P.pos[o];
             if (rb < P.l_pac && P.l_pac < rb + len) continue;  // bridges the strands
             P.seed[o] = SeedRec{rb, qbeg, len};
-            if (n_ch) {
-                const int lw = tree_lower(pool, root, rb);
+            if (st.n_ch) {
+                const int lw = tree_lower(pool, st.root, rb);
                 if (lw >= 0) {
                     // test_and_merge (software/bwamem.c:334-354)
                     ChainRec c = chn[lw];
@@ -300,6 +322,8 @@ __global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
                     }
                 }
             }
+            // one insertion allocates at most one node per level plus a root
+            if (st.n_nodes + 24 > cap || st.n_ch >= N::MAX_ID) return false;
             ChainRec c;
             c.pos = rb;
             c.last_rbeg = rb;
@@ -308,68 +332,630 @@ __global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
             c.last_len = len;
             c.n = 1;
             c.first = c.last = (uint32_t)(o - S);
-            chn[n_ch] = c;
-            tree_insert(pool, root, n_nodes, n_ch, rb);
-            ++n_ch;
+            chn[st.n_ch] = c;
+            tree_insert(pool, st.root, st.n_nodes, st.n_ch, rb);
+            ++st.n_ch;
         }
     }
+    return true;
+}
+
+// mem_chain_flt's drop loop (software/bwamem.c:652-664) by one lane
+__device__ __forceinline__ int flt_drop_serial(FltRec* a, int n, float mask_level, float drop_ratio, int msl) {
+    int m = 1;
+    for (int i = 1; i < n; ++i) {
+        int j;
+        for (j = 0; j < m; ++j) {
+            const int b_max = a[j].beg > a[i].beg ? a[j].beg : a[i].beg;
+            const int e_min = a[j].end < a[i].end ? a[j].end : a[i].end;
+            if (e_min > b_max) {
+                const int li = a[i].end - a[i].beg, lj = a[j].end - a[j].beg;
+                const int min_l = li < lj ? li : lj;
+                if ((float)(e_min - b_max) >= (float)min_l * mask_level) {
+                    if (a[j].p2 < 0) a[j].p2 = a[i].p;
+                    if ((float)a[i].w < (float)a[j].w * drop_ratio && a[j].w - a[i].w >= msl << 1) break;
+                }
+            }
+        }
+        if (j == m) a[m++] = a[i];
+    }
+    return m;
+}
+
+// the same loop with the 64 lanes of a wave scanning the kept list j in
+// order, 64 entries at a time: the first j that drops chain i ends the scan
+// (p2 is set on the significant overlaps up to and including it)
+__device__ __forceinline__ int flt_drop_wave(FltRec* a, int n, float mask_level, float drop_ratio, int msl, int lane) {
+    int m = 1;
+    for (int i = 1; i < n; ++i) {
+        const FltRec ai = a[i];
+        bool dropped = false;
+        for (int base = 0; base < m; base += 64) {
+            const int j = base + lane;
+            bool sig = false, drop = false;
+            if (j < m) {
+                const FltRec aj = a[j];
+                const int b_max = aj.beg > ai.beg ? aj.beg : ai.beg;
+                const int e_min = aj.end < ai.end ? aj.end : ai.end;
+                if (e_min > b_max) {
+                    const int li = ai.end - ai.beg, lj = aj.end - aj.beg;
+                    const int min_l = li < lj ? li : lj;
+                    if ((float)(e_min - b_max) >= (float)min_l * mask_level) {
+                        sig = true;
+                        drop = (float)ai.w < (float)aj.w * drop_ratio && aj.w - ai.w >= msl << 1;
+                    }
+                }
+            }
+            const uint64_t bd = __ballot(sig && drop);
+            const int limit = bd ? base + (int)__builtin_ctzll(bd) : 0x7fffffff;
+            if (sig && j <= limit && a[j].p2 < 0) a[j].p2 = ai.p;
+            if (bd) {
+                dropped = true;
+                break;
+            }
+        }
+        if (!dropped) {
+            if (lane == 0) a[m] = ai;
+            ++m;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    return m;
+}
+
+// weights + sort + reorder of mem_chain_flt (software/bwamem.c:636-651) by
+// one lane; ord holds the tree order, ord2 receives the sorted order
+__device__ __forceinline__ void flt_prepare_serial(const ChainParams& P, uint64_t S, FltRec* a, const uint32_t* ord,
+                                                   uint32_t* ord2, int n) {
+    const ChainRec* chn = P.chn + S;
+    for (int i = 0; i < n; ++i) {
+        const ChainRec c = chn[ord[i]];
+        a[i] = FltRec{c.first_qbeg, c.last_qbeg + c.last_len, chain_weight(c, P.seed + S, P.next + S), i, -1};
+    }
+    flt_sort(a, (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        ord2[i] = ord[a[i].p];
+        a[i].p = i;
+    }
+}
+
+// chains kept by mark + squeeze (software/bwamem.c:665-688): flags in ord
+// (free by now), kept order compacted in ord2; returns the count
+__device__ __forceinline__ int flt_squeeze_serial(const FltRec* a, int m, uint32_t* ord, uint32_t* ord2, int n) {
+    for (int i = 0; i < n; ++i) ord[i] = 0;
+    for (int i = 0; i < m; ++i) {
+        ord[a[i].p] = 1;
+        if (a[i].p2 >= 0) ord[a[i].p2] = 1;
+    }
+    int k = 0;
+    for (int i = 0; i < n; ++i)
+        if (ord[i]) ord2[k++] = ord2[i];
+    return k;
+}
+
+__device__ __forceinline__ uint64_t seeds_in(const ChainParams& P, uint64_t S, const uint32_t* ord2, int n_keep) {
+    uint64_t ns = 0;
+    for (int i = 0; i < n_keep; ++i) ns += (uint64_t)P.chn[S + ord2[i]].n;
+    return ns;
+}
+
+constexpr int ACT_NONE = 0, ACT_APPEND = 1, ACT_NEW = 2;
+
+__device__ __forceinline__ int rl32(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t rlu(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
+    const uint32_t lo = rlu((uint32_t)(uint64_t)v, l), hi = rlu((uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const int64_t o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// kb_putp by a whole wave (same result as tree_insert): lane i handles key
+// slot i of a node -- one LDS round per node search, parallel shifts and
+// split copies
+template <class N>
+__device__ __forceinline__ int node_find_wave(const N* x, int64_t k, int lane, bool& eq) {
+    const int n = x->n;
+    const int64_t kv = lane < BT_MAX ? x->key[lane] : INT64_MAX;
+    const int below = __builtin_popcountll(__ballot(lane < n && kv < k));
+    eq = __ballot(lane == below && lane < n && kv == k) != 0;
+    return eq ? below : below - 1;
+}
+
+template <class N>
+__device__ __forceinline__ void node_split_wave(N* pool, uint32_t xi, int i, uint32_t yi, uint32_t& n_nodes,
+                                                int lane) {
+    N* x = pool + xi;
+    N* y = pool + yi;
+    const uint32_t zi = n_nodes++;
+    N* z = pool + zi;
+    const int leaf = y->leaf;
+    const int n = x->n;
+    // reads first (all lanes), then writes
+    int64_t zk = 0, xk = 0;
+    uint32_t zid = 0, zc = 0, xid = 0, xc = 0;
+    if (lane < BT_T - 1) {
+        zk = y->key[BT_T + lane];
+        zid = y->id[BT_T + lane];
+    }
+    if (!leaf && lane < BT_T) zc = y->child[BT_T + lane];
+    if (lane >= i + 1 && lane <= n) xc = x->child[lane];
+    if (lane >= i && lane < n) {
+        xk = x->key[lane];
+        xid = x->id[lane];
+    }
+    const int64_t mk = y->key[BT_T - 1];
+    const uint32_t mid = y->id[BT_T - 1];
+    __builtin_amdgcn_wave_barrier();
+    if (lane < BT_T - 1) {
+        z->key[lane] = zk;
+        z->id[lane] = zid;
+    }
+    if (!leaf && lane < BT_T) z->child[lane] = zc;
+    if (lane >= i + 1 && lane <= n) x->child[lane + 1] = xc;
+    if (lane >= i && lane < n) {
+        x->key[lane + 1] = xk;
+        x->id[lane + 1] = xid;
+    }
+    if (lane == 0) {
+        z->n = BT_T - 1;
+        z->leaf = leaf;
+        y->n = BT_T - 1;
+        x->child[i + 1] = zi;
+        x->key[i] = mk;
+        x->id[i] = mid;
+        x->n = n + 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read these next (HBM pool too)
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <class N>
+__device__ __forceinline__ void tree_insert_wave(N* pool, uint32_t& root, uint32_t& n_nodes, uint32_t id, int64_t k,
+                                                 int lane) {
+    uint32_t x = root;
+    bool eq;
+    if (pool[x].n == BT_MAX) {
+        const uint32_t s = n_nodes++;
+        if (lane == 0) {
+            node_init(pool + s, 0);
+            pool[s].child[0] = x;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        node_split_wave(pool, s, 0, x, n_nodes, lane);
+        root = x = s;
+    }
+    while (!pool[x].leaf) {
+        int i = node_find_wave(pool + x, k, lane, eq) + 1;
+        const uint32_t c = pool[x].child[i];
+        if (pool[c].n == BT_MAX) {
+            node_split_wave(pool, x, i, c, n_nodes, lane);
+            if (k > pool[x].key[i]) ++i;
+        }
+        x = pool[x].child[i];
+    }
+    N* nd = pool + x;
+    const int i = node_find_wave(nd, k, lane, eq);
+    const int n = nd->n;
+    int64_t kv = 0;
+    uint32_t iv = 0;
+    const bool mv = lane >= i + 1 && lane < n;
+    if (mv) {
+        kv = nd->key[lane];
+        iv = nd->id[lane];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (mv) {
+        nd->key[lane + 1] = kv;
+        nd->id[lane + 1] = iv;
+    }
+    if (lane == 0) {
+        nd->key[i + 1] = k;
+        nd->id[i + 1] = id;
+        nd->n = n + 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Wave form of the same loop for one read, exact by construction: a window
+// of 64 seeds, one per lane, whose tree lookups and chain-record loads run
+// in parallel against the chains as they stood before the window, then a
+// scan over the window's seeds in order in which the whole wave decides each
+// seed from registers: its lower chain is the snapshot's unless a chain
+// created earlier in the window has a pos in between, and a chain's state
+// is the snapshot's unless an earlier seed of the window changed it (both
+// found from lane masks).  Where the real tree could answer differently --
+// equal keys: a window chain tying the lower chain or another window chain,
+// or a lower chain whose pos is duplicated in the tree once the window has
+// created chains -- the scan stops and the next window starts at that seed,
+// whose snapshot lookup is then exact.  Chain records and links are
+// committed per window, the window's new chains inserted in seed order.
+// Returns false when the node pool cannot take a window's new chains; `o`
+// then names the first seed not yet applied.
+template <class N>
+__device__ __forceinline__ bool insert_read_wave(const ChainParams& P, uint64_t S, uint64_t E, N* pool, uint32_t cap,
+                                                 uint64_t& o, uint32_t& n_ch, uint32_t& root, uint32_t& n_nodes,
+                                                 int lane, int64_t* dups, int& n_dup, uint64_t* dbg) {
+    ChainRec* chn = P.chn + S;
+    uint64_t t_look = 0, t_scan = 0, t_commit = 0, n_win = 0, t0, t1;
+    while (o < E) {
+        t0 = __builtin_readcyclecounter();
+        ++n_win;
+        const uint64_t so = o + (uint64_t)lane;
+        const int n_live = E - o < 64 ? (int)(E - o) : 64;
+        const bool live = lane < n_live;
+        SeedRec sd{0, 0, 0};
+        if (live) sd = P.seed[so];
+        const int64_t rb = sd.rbeg;
+        const bool skip = !live || (rb < P.l_pac && P.l_pac < rb + sd.len);
+        const uint64_t skm = __ballot(skip);
+        int lw0 = -1;
+        if (!skip && n_ch) lw0 = tree_lower(pool, root, rb);
+        ChainRec c0{};
+        if (lw0 >= 0) c0 = chn[lw0];
+        // pot: earlier seeds of the window whose pos would sit between my
+        // snapshot lower chain and me, were they to start chains
+        uint64_t pot = 0;
+        for (int t = 0; t < n_live; ++t) {
+            if ((skm >> t) & 1) continue;
+            const int64_t rt = rl64(rb, t);
+            if (t < lane && rt <= rb && (lw0 < 0 || rt >= c0.pos)) pot |= 1ull << t;
+        }
+        t1 = __builtin_readcyclecounter();
+        t_look += t1 - t0;
+        t0 = t1;
+        // window slots, filled by the scan
+        int m_id = -1;
+        ChainRec ms{};
+        uint32_t m_prev = 0;
+        uint64_t new_mask = 0, app_mask = 0;
+        int n_done = n_live;
+        for (int s = 0; s < n_live; ++s) {
+            if ((skm >> s) & 1) continue;
+            const int64_t rbs = rl64(rb, s);
+            const int32_t qs = rl32(sd.qbeg, s), ls = rl32(sd.len, s);
+            const int lw0s = rl32(lw0, s);
+            const int64_t v0 = rl64(c0.pos, s);
+            const uint64_t pm = (uint64_t)rl64((int64_t)pot, s) & new_mask;
+            int low = lw0s;
+            bool from_window = false;
+            if (pm) {
+                int64_t best = INT64_MIN;
+                int bt = -1, ties = 0;
+                for (uint64_t m = pm; m; m &= m - 1) {
+                    const int t = __builtin_ctzll(m);
+                    const int64_t r = rl64(rb, t);
+                    if (r > best) {
+                        best = r;
+                        bt = t;
+                        ties = 1;
+                    } else if (r == best) {
+                        ++ties;
+                    }
+                }
+                if ((lw0s >= 0 && best == v0) || ties > 1) {
+                    n_done = s;
+                    break;
+                }
+                low = rl32(m_id, bt);
+                from_window = true;
+            } else if (lw0s >= 0 && new_mask && n_dup != 0) {
+                // the snapshot's answer among duplicate keys may move once
+                // window chains are in the tree
+                bool dup = n_dup < 0;
+                for (int j = lane; !dup && j < n_dup; j += 64) dup = dups[j] == v0;
+                if (__ballot(dup)) {
+                    n_done = s;
+                    break;
+                }
+            }
+            int act = ACT_NEW;
+            ChainRec c{};
+            if (low >= 0) {
+                // the lower chain's state: its last change in the window, else the snapshot's
+                const uint64_t chm = __ballot(m_id == low) & ((1ull << s) - 1) & (new_mask | app_mask);
+                if (chm) {
+                    const int t = 63 - __builtin_clzll(chm);
+                    c.pos = rl64(ms.pos, t);
+                    c.last_rbeg = rl64(ms.last_rbeg, t);
+                    c.first_qbeg = rl32(ms.first_qbeg, t);
+                    c.last_qbeg = rl32(ms.last_qbeg, t);
+                    c.last_len = rl32(ms.last_len, t);
+                    c.n = rl32(ms.n, t);
+                    c.first = rlu(ms.first, t);
+                    c.last = rlu(ms.last, t);
+                } else {
+                    c.pos = v0;
+                    c.last_rbeg = rl64(c0.last_rbeg, s);
+                    c.first_qbeg = rl32(c0.first_qbeg, s);
+                    c.last_qbeg = rl32(c0.last_qbeg, s);
+                    c.last_len = rl32(c0.last_len, s);
+                    c.n = rl32(c0.n, s);
+                    c.first = rlu(c0.first, s);
+                    c.last = rlu(c0.last, s);
+                }
+                (void)from_window;
+                // test_and_merge (software/bwamem.c:334-354)
+                if (qs >= c.first_qbeg && qs + ls <= c.last_qbeg + c.last_len && rbs >= c.pos &&
+                    rbs + ls <= c.last_rbeg + c.last_len) {
+                    act = ACT_NONE;
+                } else {
+                    const bool strand_ok = !((c.last_rbeg < P.l_pac || c.pos < P.l_pac) && rbs >= P.l_pac);
+                    const int64_t x = (int64_t)qs - c.last_qbeg, y = rbs - c.last_rbeg;
+                    if (strand_ok && y >= 0 && x - y <= P.w && y - x <= P.w && x - c.last_len < P.max_chain_gap &&
+                        y - c.last_len < P.max_chain_gap)
+                        act = ACT_APPEND;
+                }
+            }
+            const uint32_t me = (uint32_t)(o + (uint64_t)s - S);
+            if (act == ACT_APPEND) {
+                if (lane == s) {
+                    m_id = low;
+                    ms = c;
+                    m_prev = c.last;
+                    ms.last = me;
+                    ms.last_rbeg = rbs;
+                    ms.last_qbeg = qs;
+                    ms.last_len = ls;
+                    ms.n = c.n + 1;
+                }
+                app_mask |= 1ull << s;
+            } else if (act == ACT_NEW) {
+                if (lane == s) {
+                    m_id = (int)(n_ch + (uint32_t)__builtin_popcountll(new_mask));
+                    ms.pos = rbs;
+                    ms.last_rbeg = rbs;
+                    ms.first_qbeg = qs;
+                    ms.last_qbeg = qs;
+                    ms.last_len = ls;
+                    ms.n = 1;
+                    ms.first = ms.last = me;
+                }
+                // a key equal to the lower chain's: the tree holds it twice from now on
+                if (low >= 0 && c.pos == rbs) {
+                    if (lane == 0 && n_dup >= 0 && n_dup < 256) dups[n_dup] = rbs;
+                    n_dup = (n_dup >= 0 && n_dup < 256) ? n_dup + 1 : -1;
+                }
+                new_mask |= 1ull << s;
+            }
+        }
+        t1 = __builtin_readcyclecounter();
+        t_scan += t1 - t0;
+        t0 = t1;
+        // commit seeds [0, n_done) of the window
+        const uint64_t done_mask = n_done >= 64 ? ~0ull : ((1ull << n_done) - 1);
+        const uint64_t nm = new_mask & done_mask, am = app_mask & done_mask;
+        const int k_new = __builtin_popcountll(nm);
+        if (k_new && (n_nodes + 24u * (uint32_t)k_new > cap || n_ch + (uint32_t)k_new >= N::MAX_ID)) return false;
+        // chain records: each modified chain's last state in the window
+        const uint64_t mod = nm | am;
+        bool final_state = ((mod >> lane) & 1) != 0;
+        for (uint64_t m = mod; m; m &= m - 1) {
+            const int u = __builtin_ctzll(m);
+            const int idu = rl32(m_id, u);
+            if (lane < u && m_id == idu) final_state = false;
+        }
+        if (final_state) chn[m_id] = ms;
+        if ((am >> lane) & 1) P.next[S + m_prev] = (uint32_t)(so - S);
+        uint32_t id = n_ch;
+        for (uint64_t m = nm; m; m &= m - 1) {
+            const int t = __builtin_ctzll(m);
+            tree_insert_wave(pool, root, n_nodes, id++, rl64(rb, t), lane);
+        }
+        n_ch += (uint32_t)k_new;
+        o += (uint64_t)n_done;
+        __syncthreads();  // this window's stores before the next window's loads
+        t_commit += __builtin_readcyclecounter() - t0;
+    }
+    if (dbg && lane == 0) {
+        dbg[10] += n_win;
+        dbg[11] += t_look;
+        dbg[12] += t_scan;
+        dbg[13] += t_commit;
+    }
+    return true;
+}
+
+}  // namespace
+
+// one lane per read with at most P.heavy_min seed occurrences; heavier
+// reads are listed for chain_heavy_kernel (giants, > P.giant_min, first)
+__global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= P.n_reads) return;
+    const uint64_t i0 = P.intv_off[r], i1 = P.intv_off[r + 1];
+    const uint64_t S = P.occ_off[i0], E = P.occ_off[i1];
+    if (S == E) {
+        P.n_out[r] = 0;
+        P.ns_out[r] = 0;
+        return;
+    }
+    if (E - S > (uint64_t)P.heavy_min) {
+        const int gi = E - S > (uint64_t)P.giant_min ? 0 : 1;
+        const uint32_t slot = atomicAdd(P.heavy_ctr + gi, 1u);
+        P.heavy[gi * (uint64_t)P.n_reads + slot] = (uint32_t)r;
+        return;
+    }
+    BNode* pool = P.node + (S / 7 + 3ull * (uint64_t)r);
+    InsState st;
+    ins_start(st, P, i0);
+    insert_read(P, i1, S, pool, 0xffffffffu, st);
     uint32_t* ord = P.ord + S;
     uint32_t* ord2 = P.ord2 + S;
-    const SeedRec* seed = P.seed + S;
-    const uint32_t* next = P.next + S;
-    const int n = n_ch ? tree_inorder(pool, root, ord) : 0;
+    const int n = st.n_ch ? tree_inorder(pool, st.root, ord) : 0;
     int n_keep = n;
     if (!P.filter || n <= 1) {
         for (int i = 0; i < n; ++i) ord2[i] = ord[i];
     } else {
-        // mem_chain_flt (software/bwamem.c:629-690)
         FltRec* a = P.flt + S;
-        for (int i = 0; i < n; ++i) {
-            const ChainRec c = chn[ord[i]];
-            a[i] = FltRec{c.first_qbeg, c.last_qbeg + c.last_len, chain_weight(c, seed, next), i, -1};
-        }
-        flt_sort(a, (size_t)n);
-        for (int i = 0; i < n; ++i) {
-            ord2[i] = ord[a[i].p];
-            a[i].p = i;
-        }
-        int m = 1;
-        for (int i = 1; i < n; ++i) {
-            int j;
-            for (j = 0; j < m; ++j) {
-                const int b_max = a[j].beg > a[i].beg ? a[j].beg : a[i].beg;
-                const int e_min = a[j].end < a[i].end ? a[j].end : a[i].end;
-                if (e_min > b_max) {
-                    const int li = a[i].end - a[i].beg, lj = a[j].end - a[j].beg;
-                    const int min_l = li < lj ? li : lj;
-                    if ((float)(e_min - b_max) >= (float)min_l * P.mask_level) {
-                        if (a[j].p2 < 0) a[j].p2 = a[i].p;
-                        if ((float)a[i].w < (float)a[j].w * P.drop_ratio && a[j].w - a[i].w >= P.min_seed_len << 1)
-                            break;
-                    }
-                }
-            }
-            if (j == m) a[m++] = a[i];
-        }
-        // keep flags by sorted position (ord is free now), then squeeze
-        for (int i = 0; i < n; ++i) ord[i] = 0;
-        for (int i = 0; i < m; ++i) {
-            ord[a[i].p] = 1;
-            if (a[i].p2 >= 0) ord[a[i].p2] = 1;
-        }
-        n_keep = 0;
-        for (int i = 0; i < n; ++i)
-            if (ord[i]) ord2[n_keep++] = ord2[i];
+        flt_prepare_serial(P, S, a, ord, ord2, n);
+        const int m = flt_drop_serial(a, n, P.mask_level, P.drop_ratio, P.min_seed_len);
+        n_keep = flt_squeeze_serial(a, m, ord, ord2, n);
     }
-    uint64_t ns = 0;
-    for (int i = 0; i < n_keep; ++i) ns += (uint64_t)chn[ord2[i]].n;
     P.n_out[r] = (uint64_t)n_keep;
-    P.ns_out[r] = ns;
+    P.ns_out[r] = seeds_in(P, S, ord2, n_keep);
 }
 
-__global__ __launch_bounds__(256) void chain_write_kernel(ChainParams P) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P.n_reads) return;
+// one wave per heavy read, persistent over the two lists (giants first):
+// the chain tree and the filter's records live in LDS (dynamic, P.lds_bytes)
+// while they fit and in the read's HBM pool otherwise; insertion, traversal
+// and the introsort run on lane 0 (their order is the reference's), the
+// weights and the drop loop on all 64 lanes
+__global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_item;
+    __shared__ uint32_t s_u32[2];
+    __shared__ int64_t s_dups[256];
+    const int lane = threadIdx.x;
+    const uint32_t n_giant = P.heavy_ctr[0], n_all = n_giant + P.heavy_ctr[1];
+    for (;;) {
+        if (lane == 0) s_item = atomicAdd(P.heavy_ctr + 2, 1u);
+        __syncthreads();
+        const uint32_t item = s_item;
+        __syncthreads();
+        if (item >= n_all) break;
+        const uint32_t r = item < n_giant ? P.heavy[item] : P.heavy[(uint64_t)P.n_reads + (item - n_giant)];
+        const uint64_t i0 = P.intv_off[r], i1 = P.intv_off[r + 1];
+        const uint64_t S = P.occ_off[i0];
+        uint32_t* ord = P.ord + S;
+        uint32_t* ord2 = P.ord2 + S;
+        __shared__ int s_n;
+        uint64_t* dbg = (P.dbg && item < 64) ? P.dbg + item * 16 : nullptr;
+        if (dbg && lane == 0) {
+            dbg[0] = r;
+            dbg[1] = P.occ_off[i1] - S;
+            dbg[2] = __builtin_readcyclecounter();
+        }
+        // seed records of the read, all lanes (mem_seed_t of every occurrence)
+        for (uint64_t iv = i0; iv < i1; ++iv) {
+            const uint64_t a = P.occ_off[iv], b = P.occ_off[iv + 1];
+            if (a == b) continue;
+            const uint64_t info = P.intv[iv * 4 + 3];
+            const int32_t qbeg = (int32_t)(info >> 32);
+            const int32_t len = (int32_t)((uint32_t)info - (uint32_t)(info >> 32));
+            for (uint64_t o = a + (uint64_t)lane; o < b; o += 64) P.seed[o] = SeedRec{(int64_t)P.pos[o], qbeg, len};
+        }
+        __syncthreads();
+        {
+            const uint64_t E = P.occ_off[i1];
+            LNode* lpool = reinterpret_cast<LNode*>(lds_raw);
+            uint64_t o = S;
+            uint32_t n_ch = 0, root = 0, n_nodes = 1;
+            if (lane == 0) node_init(lpool, 1);
+            __syncthreads();
+            int n_dup = 0;
+            const bool in_lds = insert_read_wave(P, S, E, lpool, P.lds_bytes / sizeof(LNode), o, n_ch, root, n_nodes,
+                                                 lane, s_dups, n_dup, dbg);
+            BNode* gpool = P.node + (S / 7 + 3ull * (uint64_t)r);
+            if (!in_lds) {
+                // out of LDS: move the tree to the read's HBM pool, go on there
+                for (uint32_t j = lane; j < n_nodes; j += 64) {
+                    const LNode& l = lpool[j];
+                    BNode& g = gpool[j];
+                    g.n = l.n;
+                    g.leaf = l.leaf;
+                    for (int q = 0; q < BT_MAX; ++q) {
+                        g.key[q] = l.key[q];
+                        g.id[q] = l.id[q];
+                    }
+                    for (int q = 0; q <= BT_MAX; ++q) g.child[q] = l.child[q];
+                }
+                __syncthreads();
+                insert_read_wave(P, S, E, gpool, 0xffffffffu, o, n_ch, root, n_nodes, lane, s_dups, n_dup, dbg);
+            }
+            if (lane == 0) {
+                int n;
+                if (in_lds) n = n_ch ? tree_inorder(lpool, root, ord) : 0;
+                else n = n_ch ? tree_inorder(gpool, root, ord) : 0;
+                s_n = n;
+                if (dbg) {
+                    dbg[3] = __builtin_readcyclecounter();
+                    dbg[4] = n;
+                }
+            }
+        }
+        __syncthreads();
+        const int n = s_n;
+        int n_keep = n;
+        if (!P.filter || n <= 1) {
+            for (int i = lane; i < n; i += 64) ord2[i] = ord[i];
+        } else {
+            const bool in_lds = (uint64_t)n * sizeof(FltRec) <= (uint64_t)P.lds_bytes;
+            FltRec* la = reinterpret_cast<FltRec*>(lds_raw);
+            FltRec* ga = P.flt + S;
+            // weights, one chain per lane
+            for (int i = lane; i < n; i += 64) {
+                const ChainRec c = P.chn[S + ord[i]];
+                const FltRec f{c.first_qbeg, c.last_qbeg + c.last_len, chain_weight(c, P.seed + S, P.next + S), i, -1};
+                if (in_lds) la[i] = f;
+                else ga[i] = f;
+            }
+            __syncthreads();
+            if (dbg && lane == 0) dbg[5] = __builtin_readcyclecounter();
+            if (lane == 0) {
+                if (in_lds) flt_sort(la, (size_t)n);
+                else flt_sort(ga, (size_t)n);
+            }
+            __syncthreads();
+            if (dbg && lane == 0) dbg[6] = __builtin_readcyclecounter();
+            for (int i = lane; i < n; i += 64) {
+                if (in_lds) {
+                    ord2[i] = ord[la[i].p];
+                    la[i].p = i;
+                } else {
+                    ord2[i] = ord[ga[i].p];
+                    ga[i].p = i;
+                }
+            }
+            __syncthreads();
+            const int m = in_lds ? flt_drop_wave(la, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane)
+                                 : flt_drop_wave(ga, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane);
+            __syncthreads();
+            if (dbg && lane == 0) {
+                dbg[7] = __builtin_readcyclecounter();
+                dbg[8] = m;
+            }
+            for (int i = lane; i < n; i += 64) ord[i] = 0;
+            __syncthreads();
+            for (int i = lane; i < m; i += 64) {
+                const FltRec f = in_lds ? la[i] : ga[i];
+                ord[f.p] = 1;
+                if (f.p2 >= 0) ord[f.p2] = 1;
+            }
+            __syncthreads();
+            // squeeze in order, 64 at a time
+            n_keep = 0;
+            for (int base = 0; base < n; base += 64) {
+                const int i = base + lane;
+                const bool keep = i < n && ord[i] != 0;
+                const uint64_t bk = __ballot(keep);
+                const uint32_t v = keep ? ord2[i] : 0;
+                __syncthreads();
+                if (keep) ord2[n_keep + __builtin_popcountll(bk & ((1ull << lane) - 1))] = v;
+                n_keep += __builtin_popcountll(bk);
+                __syncthreads();
+            }
+        }
+        uint64_t ns = 0;
+        for (int i = lane; i < n_keep; i += 64) ns += (uint64_t)P.chn[S + ord2[i]].n;
+        for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off);
+        if (lane == 0) {
+            P.n_out[r] = (uint64_t)n_keep;
+            P.ns_out[r] = ns;
+            if (dbg) dbg[9] = __builtin_readcyclecounter();
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void write_chains(const ChainParams& P, uint32_t r, int lane, int width) {
     const uint64_t c0 = P.chain_off[r], nc = P.chain_off[r + 1] - c0;
     if (nc == 0) return;
     const uint64_t S = P.occ_off[P.intv_off[r]];
@@ -378,24 +964,64 @@ __global__ __launch_bounds__(256) void chain_write_kernel(ChainParams P) {
     const SeedRec* seed = P.seed + S;
     const uint32_t* next = P.next + S;
     uint64_t so = P.seed_off[r];
-    for (uint64_t i = 0; i < nc; ++i) {
-        const ChainRec c = chn[ord2[i]];
-        P.out_chain[c0 + i] = OutChain{c.pos, so, c.n, 0};
-        uint32_t o = c.first;
-        for (int j = 0; j < c.n; ++j, o = next[o]) P.out_seed[so++] = seed[o];
+    // chains in order, `width` lanes at a time; seed offsets by a prefix sum
+    for (uint64_t base = 0; base < nc; base += (uint64_t)width) {
+        const uint64_t i = base + (uint64_t)lane;
+        const bool live = i < nc;
+        const ChainRec c = live ? chn[ord2[i]] : ChainRec{};
+        uint64_t incl = live ? (uint64_t)c.n : 0;
+        for (int off = 1; off < width; off <<= 1) {
+            const uint64_t t = __shfl_up(incl, off, width);
+            if (lane >= off) incl += t;
+        }
+        const uint64_t total = __shfl(incl, width - 1, width);
+        if (live) {
+            uint64_t w = so + incl - (uint64_t)c.n;
+            P.out_chain[c0 + i] = OutChain{c.pos, w, c.n, 0};
+            uint32_t o = c.first;
+            for (int j = 0; j < c.n; ++j, o = next[o]) P.out_seed[w++] = seed[o];
+        }
+        so += total;
+    }
+}
+
+__global__ __launch_bounds__(256) void chain_write_kernel(ChainParams P) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= P.n_reads) return;
+    const uint64_t S = P.occ_off[P.intv_off[r]], E = P.occ_off[P.intv_off[r + 1]];
+    if (E - S > (uint64_t)P.heavy_min) return;  // chain_write_heavy_kernel
+    write_chains(P, (uint32_t)r, 0, 1);
+}
+
+__global__ __launch_bounds__(64) void chain_write_heavy_kernel(ChainParams P) {
+    const uint32_t n_giant = P.heavy_ctr[0], n_all = n_giant + P.heavy_ctr[1];
+    for (uint32_t item = blockIdx.x; item < n_all; item += gridDim.x) {
+        const uint32_t r = item < n_giant ? P.heavy[item] : P.heavy[(uint64_t)P.n_reads + (item - n_giant)];
+        write_chains(P, r, threadIdx.x, 64);
     }
 }
 
 }  // namespace smem
 
-extern "C" hipError_t smem_launch_chain_build(const smem::ChainParams* P, hipStream_t st) {
+extern "C" hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_cu, hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(P->heavy_ctr, 0, 4 * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(smem::chain_build_kernel, dim3((P->n_reads + 255) / 256), dim3(256), 0, st, *P);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // more than the default 64 KB of dynamic LDS per workgroup (gfx950 has 160 KB per CU)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(smem::chain_heavy_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)P->lds_bytes);
+    hipLaunchKernelGGL(smem::chain_heavy_kernel, dim3(n_cu), dim3(64), P->lds_bytes, st, *P);
     return hipGetLastError();
 }
 
-extern "C" hipError_t smem_launch_chain_write(const smem::ChainParams* P, hipStream_t st) {
+extern "C" hipError_t smem_launch_chain_write(const smem::ChainParams* P, int n_cu, hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;
     hipLaunchKernelGGL(smem::chain_write_kernel, dim3((P->n_reads + 255) / 256), dim3(256), 0, st, *P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(smem::chain_write_heavy_kernel, dim3(n_cu * 4), dim3(64), 0, st, *P);
     return hipGetLastError();
 }

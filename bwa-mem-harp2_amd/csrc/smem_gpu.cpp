@@ -92,6 +92,10 @@ struct HostBuf {
 
 // device SA sampling interval = 2^SA_DENSE_SHIFT (see smem_gpu_load_sa)
 constexpr uint32_t SA_DENSE_SHIFT = 2;
+// chaining: reads with more seed occurrences than this get a wave each
+// (chain_heavy_kernel), giants first; its chain tree / filter records live
+// in CHAIN_HEAVY_LDS bytes of LDS (one such workgroup per CU)
+constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 1024, CHAIN_HEAVY_LDS = 150 * 1024;
 
 struct smem_gpu {
     int device = 0;
@@ -164,6 +168,7 @@ struct smem_batch {
     DevBuf<smem::FltRec> d_flt;
     DevBuf<uint64_t> d_n_out, d_ns_out, d_chain_off, d_seed_off;
     DevBuf<smem::OutChain> d_out_chain;
+    DevBuf<uint32_t> d_heavy;
     HostBuf<uint64_t> h_chain_off;
     HostBuf<smem::OutChain> h_out_chain;
     HostBuf<smem::SeedRec> h_out_seed;
@@ -279,7 +284,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_kstart.release(); b->h_occ_off.release(); b->h_sa_pos.release();
     b->d_seed.release(); b->d_out_seed.release(); b->d_next.release(); b->d_ord.release(); b->d_ord2.release();
     b->d_chn.release(); b->d_node.release(); b->d_flt.release(); b->d_n_out.release(); b->d_ns_out.release();
-    b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release();
+    b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release(); b->d_heavy.release();
     b->h_chain_off.release(); b->h_out_chain.release(); b->h_out_seed.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
     b->h_intv_off.release(); b->h_call_off.release();
@@ -733,6 +738,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     HIP_TRY(b->d_ns_out.ensure(std::max(n, 1)));
     HIP_TRY(b->d_chain_off.ensure(n + 1));
     HIP_TRY(b->d_seed_off.ensure(n + 1));
+    HIP_TRY(b->d_heavy.ensure(2ull * (uint64_t)n + 4));
     size_t tmp = 0;
     HIP_TRY(smem_launch_offsets(nullptr, nullptr, std::max(n, 1), nullptr, &tmp, b->st));
     HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
@@ -761,8 +767,22 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.ns_out = b->d_ns_out.p;
     P.chain_off = b->d_chain_off.p;
     P.seed_off = b->d_seed_off.p;
+    P.heavy_min = CHAIN_HEAVY_MIN;
+    P.giant_min = CHAIN_GIANT_MIN;
+    P.heavy_ctr = b->d_heavy.p;
+    P.heavy = b->d_heavy.p + 4;
+    P.lds_bytes = CHAIN_HEAVY_LDS;
+    // test hooks: SMEM_CHAIN_LDS shrinks the heavy path's LDS (exercises its
+    // HBM fallbacks), SMEM_CHAIN_HEAVY_MIN moves the lane/wave split
+    if (const char* v = getenv("SMEM_CHAIN_LDS")) P.lds_bytes = (uint32_t)std::max(1024, atoi(v));
+    if (const char* v = getenv("SMEM_CHAIN_HEAVY_MIN")) P.heavy_min = (uint32_t)std::max(0, atoi(v));
+    if (getenv("SMEM_CHAIN_DBG")) {
+        HIP_TRY(b->d_dbg.ensure(64 * 16));
+        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 64 * 16 * sizeof(uint64_t), b->st));
+        P.dbg = b->d_dbg.p;
+    }
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
-    HIP_TRY(smem_launch_chain_build(&P, b->st));
+    HIP_TRY(smem_launch_chain_build(&P, b->g->n_cu, b->st));
     tmp = b->d_sa_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_n_out.p, b->d_chain_off.p, n, b->d_sa_tmp.p, &tmp, b->st));
     tmp = b->d_sa_tmp.n;
@@ -776,7 +796,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     HIP_TRY(b->d_out_seed.ensure(std::max<uint64_t>(b->tot_seeds, 1)));
     P.out_chain = b->d_out_chain.p;
     P.out_seed = b->d_out_seed.p;
-    HIP_TRY(smem_launch_chain_write(&P, b->st));
+    HIP_TRY(smem_launch_chain_write(&P, b->g->n_cu, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
     HIP_TRY(hipStreamSynchronize(b->st));
     float ms = 0.f;

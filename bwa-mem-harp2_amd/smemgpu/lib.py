@@ -369,6 +369,10 @@ class Batch:
         _check(load().smem_batch_set_reads_packed(self._h, offs.size - 1, codes.ctypes.data, offs.ctypes.data),
                "smem_batch_set_reads_packed")
 
+    @property
+    def n_reads(self) -> int:
+        return int(self._keep[1].size - 1)
+
     def run(self, opt: Options = Options()) -> None:
         o = opt.c()
         _check(load().smem_batch_run(self._h, C.byref(o)), "smem_batch_run")

@@ -145,3 +145,35 @@ def test_chain_strand_bridging_and_empty(gpu_device):
         f.close()
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("env", [dict(SMEM_CHAIN_HEAVY_MIN="0"), dict(SMEM_CHAIN_HEAVY_MIN="100000"),
+                                 dict(SMEM_CHAIN_LDS="2048")], ids=["all-wave", "all-lane", "lds-overflow"])
+def test_chain_paths_agree(gpu_device, monkeypatch, env):
+    """The lane-per-read path, the wave-per-read path and the wave path's
+    HBM fallbacks (chain tree / filter records beyond its LDS) give the
+    restatement's chains."""
+    import smemgpu
+    from smemgpu import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.make_genome(300_000, seed=81, repeat_frac=0.6, n_families=4, tandem_frac=0.01)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        reads = synth.concat_reads([synth.make_reads(g.codes, 1500, 150, seed=82, sub_rate=0.01),
+                                    synth.make_reads(g.codes, 300, (10, 250), seed=83)])
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        b.sa(19, 10000)
+        l_pac = idx.seq_len // 2
+        for filt in (0, 1):
+            b.chain(l_pac, filter=bool(filt), w=5, max_chain_gap=40)
+            res = b.fetch()
+            assert res.to_smch() == _oracle_chains(res, reads.n, l_pac, 19, 10000, filter=filt, w=5,
+                                                   max_chain_gap=40)
+        b.close()
+    finally:
+        gpu.close()
