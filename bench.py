@@ -62,7 +62,8 @@ def parse():
     p.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
     p.add_argument("--read-len", type=int, default=150)
     p.add_argument("--sub", type=float, default=0.02)
-    p.add_argument("--genome-mbp", type=float, default=2000.0)
+    p.add_argument("--genome-mbp", type=float, default=3101.804739,
+                   help="synthetic genome size; default = human_g1k_v37 l_pac (6.2 G symbols with its reverse complement)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu", help="index construction (same bytes)")
     p.add_argument("--lanes-per-cu", type=int, default=0)

@@ -28,7 +28,7 @@ EXPORTED = [
     "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_batch_debug", "smem_strerror",
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
-    "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results",
+    "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results", "smem_bwt_build_gpu_large",
 ]
 
 
@@ -91,6 +91,7 @@ def load() -> C.CDLL:
     lib.smem_index_free.restype = None
     lib.smem_bwt_build_sa.argtypes = [C.c_void_p, C.c_uint64, C.c_int, P(IndexT), P(SaT)]
     lib.smem_bwt_build_gpu_sa.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int, P(IndexT), P(SaT)]
+    lib.smem_bwt_build_gpu_large.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int, P(IndexT), P(SaT)]
     lib.smem_sa_read.argtypes = [C.c_char_p, P(SaT)]
     lib.smem_sa_write.argtypes = [C.c_char_p, P(SaT)]
     lib.smem_sa_free.argtypes = [P(SaT)]
@@ -161,19 +162,28 @@ class Index:
         return cls(raw)
 
     @classmethod
-    def build_gpu(cls, fwd_codes: np.ndarray, device: int = 0) -> "Index":
-        """Same bytes as build(), constructed on a HIP device (prefix doubling)."""
+    def build_gpu(cls, fwd_codes: np.ndarray, device: int = 0, large: bool = False) -> "Index":
+        """Same bytes as build(), constructed on a HIP device (prefix doubling;
+        large=True forces the bucketed 64-bit builder used past 2^32 symbols)."""
         fwd = np.ascontiguousarray(fwd_codes, dtype=np.uint8)
         raw = IndexT()
-        _check(load().smem_bwt_build_gpu(device, fwd.ctypes.data, fwd.size, C.byref(raw)), "smem_bwt_build_gpu")
+        if large:
+            _check(load().smem_bwt_build_gpu_large(device, fwd.ctypes.data, fwd.size, 0, C.byref(raw), None),
+                   "smem_bwt_build_gpu_large")
+        else:
+            _check(load().smem_bwt_build_gpu(device, fwd.ctypes.data, fwd.size, C.byref(raw)), "smem_bwt_build_gpu")
         return cls(raw)
 
     @classmethod
-    def build_sa(cls, fwd_codes: np.ndarray, sa_intv: int = 32, gpu: bool = False, device: int = 0):
+    def build_sa(cls, fwd_codes: np.ndarray, sa_intv: int = 32, gpu: bool = False, device: int = 0,
+                 large: bool = False):
         """(Index, SA): the .bwt and the sampled SA bwa index writes beside it."""
         fwd = np.ascontiguousarray(fwd_codes, dtype=np.uint8)
         raw, sraw = IndexT(), SaT()
-        if gpu:
+        if gpu and large:
+            _check(load().smem_bwt_build_gpu_large(device, fwd.ctypes.data, fwd.size, sa_intv, C.byref(raw),
+                                                   C.byref(sraw)), "smem_bwt_build_gpu_large")
+        elif gpu:
             _check(load().smem_bwt_build_gpu_sa(device, fwd.ctypes.data, fwd.size, sa_intv, C.byref(raw), C.byref(sraw)),
                    "smem_bwt_build_gpu_sa")
         else:

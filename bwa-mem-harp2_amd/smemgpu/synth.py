@@ -148,7 +148,7 @@ def make_reads(genome_codes: np.ndarray, n_reads: int, read_len, seed: int = 1, 
         lens = rng.integers(read_len[0], read_len[1] + 1, size=n_reads).astype(np.int32)
     else:
         lens = np.full(n_reads, int(read_len), dtype=np.int32)
-    lens = np.minimum(lens, G).astype(np.int32)
+    lens = np.minimum(lens, min(G, 2**31 - 1)).astype(np.int32)
     offs = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)])
     total = int(offs[-1])
     codes = np.empty(total, dtype=np.uint8)

@@ -100,6 +100,12 @@ int  smem_bwt_build_sa(const uint8_t *fwd_codes, uint64_t n_fwd, int sa_intv, sm
 /* the same on a HIP device (prefix doubling, as smem_bwt_build_gpu) */
 int  smem_bwt_build_gpu_sa(int device, const uint8_t *fwd_codes, uint64_t n_fwd, int sa_intv, smem_index_t *idx,
                            smem_sa_t *sa);
+/* The bucketed builder with 64-bit suffix positions (both strands up to 2^34
+ * symbols: a human-size genome).  smem_bwt_build_gpu(_sa) switch to it by
+ * themselves once 2 * n_fwd no longer fits 32 bits; called directly it runs
+ * at any size (tests compare it with the CPU builder).  sa may be NULL. */
+int  smem_bwt_build_gpu_large(int device, const uint8_t *fwd_codes, uint64_t n_fwd, int sa_intv, smem_index_t *idx,
+                              smem_sa_t *sa);
 /* .sa file I/O (software/bwt.c:852-897) */
 int  smem_sa_read(const char *fn, smem_sa_t *sa);
 int  smem_sa_write(const char *fn, const smem_sa_t *sa);

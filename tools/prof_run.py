@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--genome-mbp", type=float, default=2000)
+    p.add_argument("--genome-mbp", type=float, default=3101.804739)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--reads", type=int, default=1_000_000)
     p.add_argument("--read-len", type=int, default=150)

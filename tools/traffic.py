@@ -44,7 +44,7 @@ def run_pass(counter: str, out_dir: str, a) -> float:
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--genome-mbp", type=float, default=2000.0)
+    p.add_argument("--genome-mbp", type=float, default=3101.804739)
     p.add_argument("--reads", type=int, default=1_000_000)
     p.add_argument("--read-len", type=int, default=150)
     p.add_argument("--seed", type=int, default=1)
