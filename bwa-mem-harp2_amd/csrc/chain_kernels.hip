@@ -403,6 +403,84 @@ __device__ __forceinline__ int flt_drop_wave(FltRec* a, int n, float mask_level,
     return m;
 }
 
+// The same loop again, pruned, for drop_ratio > 0.  The kept list is in
+// weight order (descending), and drop(i, j) -- w_i < w_j * drop_ratio and
+// w_j - w_i >= 2 min_seed_len -- is monotone in w_j, so the j that can drop
+// i form a prefix [0, J_i) of it: the first dropping j is searched there
+// only.  p2 is set on the significant overlaps j <= that j (all j if none);
+// once set it never changes, so only the kept chains with p2 still unset are
+// visited for it: they are listed in U (any order; a marked j leaves U).
+// Same kept list and p2 values as flt_drop_serial.
+__device__ __forceinline__ bool flt_sig(const FltRec& ai, const FltRec& aj, float mask_level) {
+    const int b_max = aj.beg > ai.beg ? aj.beg : ai.beg;
+    const int e_min = aj.end < ai.end ? aj.end : ai.end;
+    if (e_min <= b_max) return false;
+    const int li = ai.end - ai.beg, lj = aj.end - aj.beg;
+    const int min_l = li < lj ? li : lj;
+    return (float)(e_min - b_max) >= (float)min_l * mask_level;
+}
+
+__device__ __forceinline__ int flt_drop_pruned(FltRec* a, uint32_t* U, int n, float mask_level, float drop_ratio,
+                                               int msl, int lane) {
+    int m = 1, nu = 1;
+    if (lane == 0) U[0] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int i = 1; i < n; ++i) {
+        const FltRec ai = a[i];
+        // first j of the droppers' prefix with a significant overlap
+        int jstar = -1;
+        for (int base = 0; base < m; base += 64) {
+            const int j = base + lane;
+            bool can = false, hit = false;
+            if (j < m) {
+                const FltRec aj = a[j];
+                can = (float)ai.w < (float)aj.w * drop_ratio && aj.w - ai.w >= msl << 1;
+                hit = can && flt_sig(ai, aj, mask_level);
+            }
+            const uint64_t bh = __ballot(hit);
+            if (bh) {
+                jstar = base + (int)__builtin_ctzll(bh);
+                break;
+            }
+            if (__ballot(can) != __ballot(j < m)) break;  // the prefix ends in this chunk
+        }
+        const int limit = jstar >= 0 ? jstar : m - 1;
+        // p2 on the significant overlaps j <= limit among those still unset
+        int out = 0;
+        for (int base = 0; base < nu; base += 64) {
+            const int u = base + lane;
+            uint32_t j = 0;
+            bool keep = false;
+            if (u < nu) {
+                j = U[u];
+                keep = true;
+                if ((int)j <= limit && flt_sig(ai, a[j], mask_level)) {
+                    a[j].p2 = ai.p;
+                    keep = false;
+                }
+            }
+            const uint64_t bk = __ballot(keep);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            if (keep) U[out + __builtin_popcountll(bk & ((1ull << lane) - 1))] = j;
+            out += __builtin_popcountll(bk);
+        }
+        nu = out;
+        if (jstar < 0) {
+            if (lane == 0) {
+                a[m] = ai;
+                U[nu] = (uint32_t)m;
+            }
+            ++m;
+            ++nu;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    return m;
+}
+
 // weights + sort + reorder of mem_chain_flt (software/bwamem.c:636-651) by
 // one lane; ord holds the tree order, ord2 receives the sorted order
 __device__ __forceinline__ void flt_prepare_serial(const ChainParams& P, uint64_t S, FltRec* a, const uint32_t* ord,
@@ -827,11 +905,12 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
         uint32_t* ord = P.ord + S;
         uint32_t* ord2 = P.ord2 + S;
         __shared__ int s_n;
-        uint64_t* dbg = (P.dbg && item < 64) ? P.dbg + item * 16 : nullptr;
+        uint64_t* dbg = (P.dbg && item < 256) ? P.dbg + item * 16 : nullptr;
         if (dbg && lane == 0) {
             dbg[0] = r;
             dbg[1] = P.occ_off[i1] - S;
             dbg[2] = __builtin_readcyclecounter();
+            dbg[14] = __builtin_amdgcn_s_memrealtime();
         }
         // seed records of the read, all lanes (mem_seed_t of every occurrence)
         for (uint64_t iv = i0; iv < i1; ++iv) {
@@ -915,8 +994,18 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 }
             }
             __syncthreads();
-            const int m = in_lds ? flt_drop_wave(la, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane)
-                                 : flt_drop_wave(ga, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane);
+            int m;
+            if (P.drop_ratio > 0.f) {
+                // U: LDS after the records while both fit, else the read's ord
+                // rows (free until the marks below)
+                const bool u_lds = in_lds && (uint64_t)n * (sizeof(FltRec) + 4) <= (uint64_t)P.lds_bytes;
+                uint32_t* U = u_lds ? reinterpret_cast<uint32_t*>(la + n) : ord;
+                m = in_lds ? flt_drop_pruned(la, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane)
+                           : flt_drop_pruned(ga, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane);
+            } else {
+                m = in_lds ? flt_drop_wave(la, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane)
+                           : flt_drop_wave(ga, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane);
+            }
             __syncthreads();
             if (dbg && lane == 0) {
                 dbg[7] = __builtin_readcyclecounter();
@@ -949,7 +1038,10 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
         if (lane == 0) {
             P.n_out[r] = (uint64_t)n_keep;
             P.ns_out[r] = ns;
-            if (dbg) dbg[9] = __builtin_readcyclecounter();
+            if (dbg) {
+                dbg[9] = __builtin_readcyclecounter();
+                dbg[15] = __builtin_amdgcn_s_memrealtime();
+            }
         }
         __syncthreads();
     }

@@ -777,8 +777,8 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     if (const char* v = getenv("SMEM_CHAIN_LDS")) P.lds_bytes = (uint32_t)std::max(1024, atoi(v));
     if (const char* v = getenv("SMEM_CHAIN_HEAVY_MIN")) P.heavy_min = (uint32_t)std::max(0, atoi(v));
     if (getenv("SMEM_CHAIN_DBG")) {
-        HIP_TRY(b->d_dbg.ensure(64 * 16));
-        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 64 * 16 * sizeof(uint64_t), b->st));
+        HIP_TRY(b->d_dbg.ensure(256 * 16));
+        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 256 * 16 * sizeof(uint64_t), b->st));
         P.dbg = b->d_dbg.p;
     }
     HIP_TRY(hipEventRecord(b->ev[0], b->st));

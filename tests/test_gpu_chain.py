@@ -71,7 +71,8 @@ def _oracle_chains(res, n_reads, l_pac, min_seed_len, max_occ, **kw):
     dict(w=100, max_chain_gap=10000, mask_level=0.5, drop_ratio=0.5),
     dict(w=5, max_chain_gap=40, mask_level=0.3, drop_ratio=0.8),
     dict(w=0, max_chain_gap=1, mask_level=0.0, drop_ratio=1.0),
-], ids=["std", "tight", "degenerate"])
+    dict(w=100, max_chain_gap=10000, mask_level=0.5, drop_ratio=0.0),
+], ids=["std", "tight", "degenerate", "nodrop"])
 @pytest.mark.parametrize("filt", [0, 1])
 def test_chain_vs_oracle_repeat_dense(gpu_device, opts, filt):
     """A 1 Mbp genome that is 70 % diverged copies of 6 families plus

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--genome-mbp", type=float, default=2000)
+    p.add_argument("--genome-mbp", type=float, default=3101.804739)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--reads", type=int, default=1_000_000)
     p.add_argument("--reps", type=int, default=2)
@@ -50,11 +50,12 @@ def main():
             ms.append(b.stats()["chain_ms"])
         out[f"filter{int(filt)}_ms"] = ms
     if os.environ.get("SMEM_CHAIN_DBG"):
-        d = b.debug_words(64 * 16).reshape(64, 16).astype(np.int64)
-        out["heavy_phases_cycles"] = [dict(read=int(x[0]), seeds=int(x[1]), chains=int(x[4]), insert=int(x[3] - x[2]),
+        d = b.debug_words(256 * 16).reshape(256, 16).astype(np.int64)
+        d = d[np.argsort(-(d[:, 9] - d[:, 2]))]
+        out["heavy_phases_cycles"] = [dict(total=int(x[9] - x[2]), us=(x[15] - x[14]) / 100.0, read=int(x[0]), seeds=int(x[1]), chains=int(x[4]), insert=int(x[3] - x[2]),
                                            weights=int(x[5] - x[3]), sort=int(x[6] - x[5]), drop=int(x[7] - x[6]),
                                            kept=int(x[8]), tail=int(x[9] - x[7]), windows=int(x[10]), look=int(x[11]),
-                                           scan=int(x[12]), commit=int(x[13])) for x in d[:12] if x[9]]
+                                           scan=int(x[12]), commit=int(x[13])) for x in d[:16] if x[9]]
     res = b.fetch()
     n_seed = np.array([res.read_sa(i).size for i in range(reads.n)]) if reads.n <= 2_000_000 else None
     n_chain = np.diff(res.chain_off)
