@@ -88,6 +88,7 @@ struct ChainParams {
     uint32_t* heavy;           // [2 n_reads]
     uint32_t* heavy_ctr;       // [4]
     uint32_t lds_bytes;        // dynamic LDS of chain_heavy_kernel
+    int cluster;               // heavy path: position-cluster decomposition (0: tree path only)
     uint64_t* dbg;             // optional phase clocks of the heavy path (16 words per item)
     // output (write kernel)
     const uint64_t* chain_off; // [n_reads + 1]

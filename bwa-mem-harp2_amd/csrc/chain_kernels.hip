@@ -525,14 +525,6 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
     const uint32_t lo = rlu((uint32_t)(uint64_t)v, l), hi = rlu((uint32_t)((uint64_t)v >> 32), l);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ int64_t wave_max64(int64_t v) {
-    for (int off = 32; off > 0; off >>= 1) {
-        const int64_t o = __shfl_xor(v, off);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
 // kb_putp by a whole wave (same result as tree_insert): lane i handles key
 // slot i of a node -- one LDS round per node search, parallel shifts and
 // split copies
@@ -841,6 +833,189 @@ __device__ __forceinline__ bool insert_read_wave(const ChainParams& P, uint64_t 
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Heavy reads by position clusters.  Sort the read's seeds by rbeg; cut the
+// sorted list where two neighbours are G = max(max_chain_gap, 1) + the
+// longest seed apart or more.  A chain's consecutive seeds are less than G
+// apart (test_and_merge appends only when y - last_len < max_chain_gap,
+// contains only when rb + len <= last_rbeg + last_len), so every chain lies
+// in one cluster, and a seed whose lower chain (kb_intervalp) lies in an
+// earlier cluster is at least G past that chain's last seed: test_and_merge
+// fails and the seed starts a chain -- what it does with no lower chain.  So
+// each cluster runs mem_insert_seed's loop on its own seeds, in their order,
+// against its own chains: the lower chain is the cluster's chain with the
+// largest pos <= rb.  That is the tree's answer while no two chains share a
+// pos; a cluster that creates an equal pos (kbtree's answer then depends on
+// the node layout) sends the read back to the tree path.  With distinct keys
+// the in-order traversal is pos order: clusters in order, pos order inside.
+// One lane runs one cluster (64 per round), its sorted chain list (pos << 20
+// | local id) kept in the LDS slots of the cluster's already-read seeds.
+// ---------------------------------------------------------------------------
+constexpr int CL_OBITS = 20;  // seed index bits in the sort keys
+constexpr uint64_t CL_OMASK = (1ull << CL_OBITS) - 1;
+
+__device__ __forceinline__ void wave_bitonic(uint64_t* key, uint32_t npad, int lane) {
+    for (uint32_t k = 2; k <= npad; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = lane; t < (npad >> 1); t += 64) {
+                const uint32_t i = 2 * t - (t & (j - 1));
+                const uint32_t l = i + j;
+                const uint64_t a = key[i], b = key[l];
+                const bool up = (i & k) == 0;
+                if ((a > b) == up) {
+                    key[i] = b;
+                    key[l] = a;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t& total) {
+    uint32_t incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+    }
+    total = __shfl(incl, 63, 64);
+    return incl - v;
+}
+
+// true: chains built, tree order in ord[0, n_out); false: a cluster made an
+// equal chain key (nothing of the output is final; run the tree path)
+__device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t E, uint64_t* key, int lane,
+                                     int& n_out) {
+    const uint32_t N = (uint32_t)(E - S);
+    uint32_t npad = 2;
+    while (npad < N) npad <<= 1;
+    ChainRec* chn = P.chn + S;
+    const SeedRec* seed = P.seed + S;
+    uint32_t* ord = P.ord + S;
+    uint32_t* cstart = P.ord2 + S;  // free until the filter's reorder
+    // keys (rb, o); seeds bridging the strands sort last and are not used
+    int32_t lmax = 0;
+    for (uint32_t o = lane; o < npad; o += 64) {
+        uint64_t k = ~0ull;
+        if (o < N) {
+            const SeedRec sd = seed[o];
+            if (!(sd.rbeg < P.l_pac && P.l_pac < sd.rbeg + sd.len)) {
+                k = ((uint64_t)sd.rbeg << CL_OBITS) | o;
+                lmax = sd.len > lmax ? sd.len : lmax;
+            }
+        }
+        key[o] = k;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t t = __shfl_xor(lmax, off);
+        lmax = t > lmax ? t : lmax;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    wave_bitonic(key, npad, lane);
+    const int64_t G = (int64_t)(P.max_chain_gap > 1 ? P.max_chain_gap : 1) + lmax;
+    // clusters: heads where the gap to the previous seed is >= G; second
+    // keys (cluster, o) in place; cluster starts to cstart
+    uint32_t n_valid = 0, n_cl = 0;
+    uint64_t carry = 0;  // the previous chunk's last key, before it was rewritten
+    for (uint32_t base = 0; base < N; base += 64) {
+        const uint32_t p = base + lane;
+        uint64_t k = 0;
+        bool valid = false;
+        if (p < N) {
+            k = key[p];
+            valid = k != ~0ull;
+        }
+        uint64_t kp = __shfl_up(k, 1, 64);
+        if (lane == 0) kp = carry;
+        carry = __shfl(k, 63, 64);
+        const bool head = valid && (p == 0 || (int64_t)(k >> CL_OBITS) - (int64_t)(kp >> CL_OBITS) >= G);
+        const uint64_t hm = __ballot(head);
+        const uint32_t cid = n_cl + (uint32_t)__builtin_popcountll(hm & ((2ull << lane) - 1)) - 1;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        if (valid) key[p] = ((uint64_t)cid << CL_OBITS) | (k & CL_OMASK);
+        if (head) cstart[cid] = p;
+        n_cl += (uint32_t)__builtin_popcountll(hm);
+        n_valid += (uint32_t)__builtin_popcountll(__ballot(valid));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    wave_bitonic(key, npad, lane);  // cluster order kept, seed order inside
+    bool dup = false;
+    uint32_t n_tot = 0;
+    for (uint32_t r0 = 0; r0 < n_cl; r0 += 64) {
+        const uint32_t kc = r0 + lane;
+        uint32_t cs = 0, ce = 0;
+        if (kc < n_cl) {
+            cs = cstart[kc];
+            ce = kc + 1 < n_cl ? cstart[kc + 1] : n_valid;
+        }
+        uint32_t n_ch = 0;
+        for (uint32_t p = cs; p < ce; ++p) {
+            const uint32_t o = (uint32_t)(key[p] & CL_OMASK);
+            const SeedRec sd = seed[o];
+            const int64_t rb = sd.rbeg;
+            // lower chain: the last list entry with pos <= rb
+            int lo = 0, hi = (int)n_ch;  // first entry with pos > rb
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)(key[cs + mid] >> CL_OBITS) <= rb) lo = mid + 1;
+                else hi = mid;
+            }
+            const int L = lo - 1;
+            bool make = true;
+            if (L >= 0) {
+                const uint64_t e = key[cs + L];
+                const uint32_t id = cs + (uint32_t)(e & CL_OMASK);
+                ChainRec c = chn[id];
+                // test_and_merge (software/bwamem.c:334-354)
+                if (sd.qbeg >= c.first_qbeg && sd.qbeg + sd.len <= c.last_qbeg + c.last_len && rb >= c.pos &&
+                    rb + sd.len <= c.last_rbeg + c.last_len) {
+                    make = false;  // contained
+                } else {
+                    const bool strand_ok = !((c.last_rbeg < P.l_pac || c.pos < P.l_pac) && rb >= P.l_pac);
+                    const int64_t x = (int64_t)sd.qbeg - c.last_qbeg, y = rb - c.last_rbeg;
+                    if (strand_ok && y >= 0 && x - y <= P.w && y - x <= P.w && x - c.last_len < P.max_chain_gap &&
+                        y - c.last_len < P.max_chain_gap) {
+                        P.next[S + c.last] = o;
+                        c.last = o;
+                        c.last_rbeg = rb;
+                        c.last_qbeg = sd.qbeg;
+                        c.last_len = sd.len;
+                        c.n += 1;
+                        chn[id] = c;
+                        make = false;
+                    }
+                }
+                if (make && c.pos == rb) dup = true;
+            }
+            if (make) {
+                ChainRec c;
+                c.pos = rb;
+                c.last_rbeg = rb;
+                c.first_qbeg = sd.qbeg;
+                c.last_qbeg = sd.qbeg;
+                c.last_len = sd.len;
+                c.n = 1;
+                c.first = c.last = o;
+                chn[cs + n_ch] = c;
+                // insert after L; the slots up to cs + n_ch are already read
+                for (int q = (int)n_ch; q > L + 1; --q) key[cs + q] = key[cs + q - 1];
+                key[cs + L + 1] = ((uint64_t)rb << CL_OBITS) | n_ch;
+                ++n_ch;
+            }
+        }
+        uint32_t tot;
+        const uint32_t base = wave_excl_scan(n_ch, lane, tot);
+        for (uint32_t j = 0; j < n_ch; ++j) ord[n_tot + base + j] = cs + (uint32_t)(key[cs + j] & CL_OMASK);
+        n_tot += tot;
+    }
+    n_out = (int)n_tot;
+    return __ballot(dup) == 0;
+}
+
 }  // namespace
 
 // one lane per read with at most P.heavy_min seed occurrences; heavier
@@ -889,7 +1064,6 @@ __global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
 __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_item;
-    __shared__ uint32_t s_u32[2];
     __shared__ int64_t s_dups[256];
     const int lane = threadIdx.x;
     const uint32_t n_giant = P.heavy_ctr[0], n_all = n_giant + P.heavy_ctr[1];
@@ -922,7 +1096,25 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             for (uint64_t o = a + (uint64_t)lane; o < b; o += 64) P.seed[o] = SeedRec{(int64_t)P.pos[o], qbeg, len};
         }
         __syncthreads();
-        {
+        bool done = false;
+        if (P.cluster) {
+            const uint64_t E = P.occ_off[i1];
+            uint32_t npad = 2;
+            while (npad < E - S) npad <<= 1;
+            if (E - S < (1ull << CL_OBITS) && (uint64_t)npad * 8 <= P.lds_bytes) {
+                int n = 0;
+                done = insert_read_clusters(P, S, E, reinterpret_cast<uint64_t*>(lds_raw), lane, n);
+                if (done && lane == 0) {
+                    s_n = n;
+                    if (dbg) {
+                        dbg[3] = __builtin_readcyclecounter();
+                        dbg[4] = n;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (!done) {
             const uint64_t E = P.occ_off[i1];
             LNode* lpool = reinterpret_cast<LNode*>(lds_raw);
             uint64_t o = S;

@@ -776,6 +776,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     // HBM fallbacks), SMEM_CHAIN_HEAVY_MIN moves the lane/wave split
     if (const char* v = getenv("SMEM_CHAIN_LDS")) P.lds_bytes = (uint32_t)std::max(1024, atoi(v));
     if (const char* v = getenv("SMEM_CHAIN_HEAVY_MIN")) P.heavy_min = (uint32_t)std::max(0, atoi(v));
+    P.cluster = getenv("SMEM_CHAIN_TREE_ONLY") ? 0 : 1;
     if (getenv("SMEM_CHAIN_DBG")) {
         HIP_TRY(b->d_dbg.ensure(256 * 16));
         HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 256 * 16 * sizeof(uint64_t), b->st));

@@ -149,11 +149,14 @@ def test_chain_strand_bridging_and_empty(gpu_device):
 
 
 @pytest.mark.parametrize("env", [dict(SMEM_CHAIN_HEAVY_MIN="0"), dict(SMEM_CHAIN_HEAVY_MIN="100000"),
-                                 dict(SMEM_CHAIN_LDS="2048")], ids=["all-wave", "all-lane", "lds-overflow"])
+                                 dict(SMEM_CHAIN_LDS="2048"), dict(SMEM_CHAIN_TREE_ONLY="1"),
+                                 dict(SMEM_CHAIN_TREE_ONLY="1", SMEM_CHAIN_HEAVY_MIN="0")],
+                         ids=["all-wave", "all-lane", "lds-overflow", "tree-only", "tree-only-all-wave"])
 def test_chain_paths_agree(gpu_device, monkeypatch, env):
-    """The lane-per-read path, the wave-per-read path and the wave path's
-    HBM fallbacks (chain tree / filter records beyond its LDS) give the
-    restatement's chains."""
+    """The lane-per-read path, the wave-per-read paths (position clusters,
+    and the chain tree they fall back to on equal chain keys) and the wave
+    path's HBM fallbacks (chain tree / filter records beyond its LDS) give
+    the restatement's chains."""
     import smemgpu
     from smemgpu import synth
     for k, v in env.items():
