@@ -89,6 +89,8 @@ struct ChainParams {
     uint32_t* heavy_ctr;       // [4]
     uint32_t lds_bytes;        // dynamic LDS of chain_heavy_kernel
     int cluster;               // heavy path: position-cluster decomposition (0: tree path only)
+    int wave_sort;             // heavy path: mem_chain_flt's introsort by the wave (0: lane 0 alone)
+    uint32_t sort_lane_max;    // wave sort: segments up to this size are cut by one lane
     uint64_t* dbg;             // optional phase clocks of the heavy path (16 words per item)
     // output (write kernel)
     const uint64_t* chain_off; // [n_reads + 1]

@@ -883,10 +883,39 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_
     return incl - v;
 }
 
+constexpr uint32_t CODE_SKIP = 0, CODE_NEW = 1, CODE_REPLAY = 2;
+constexpr int MERGE_NEW = 0, MERGE_CONTAINED = 1, MERGE_APPEND = 2;
+
+// test_and_merge (software/bwamem.c:334-354) of seed (rb, qb, ln) against chain c
+__device__ __forceinline__ int merge_test(const ChainParams& P, const ChainRec& c, int64_t rb, int32_t qb,
+                                          int32_t ln) {
+    if (qb >= c.first_qbeg && qb + ln <= c.last_qbeg + c.last_len && rb >= c.pos &&
+        rb + ln <= c.last_rbeg + c.last_len)
+        return MERGE_CONTAINED;
+    const bool strand_ok = !((c.last_rbeg < P.l_pac || c.pos < P.l_pac) && rb >= P.l_pac);
+    const int64_t x = (int64_t)qb - c.last_qbeg, y = rb - c.last_rbeg;
+    if (strand_ok && y >= 0 && x - y <= P.w && y - x <= P.w && x - c.last_len < P.max_chain_gap &&
+        y - c.last_len < P.max_chain_gap)
+        return MERGE_APPEND;
+    return MERGE_NEW;
+}
+
+__device__ __forceinline__ void chain_append(ChainRec& c, uint32_t o, int64_t rb, int32_t qb, int32_t ln) {
+    c.last = o;
+    c.last_rbeg = rb;
+    c.last_qbeg = qb;
+    c.last_len = ln;
+    c.n += 1;
+}
+
 // true: chains built, tree order in ord[0, n_out); false: a cluster made an
-// equal chain key (nothing of the output is final; run the tree path)
+// equal chain key and the tree replay must finish the read.  Chain ids are
+// the index of the chain's first seed.  code[o] records, per seed, what the
+// replay does with it: CODE_NEW (this seed starts a chain: kb_putp it),
+// CODE_REPLAY (a seed of a cluster past its first equal key), or CODE_SKIP;
+// n_cand counts the first two.
 __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t E, uint64_t* key, int lane,
-                                     int& n_out) {
+                                     int& n_out, uint32_t& n_cand) {
     const uint32_t N = (uint32_t)(E - S);
     uint32_t npad = 2;
     while (npad < N) npad <<= 1;
@@ -894,6 +923,7 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
     const SeedRec* seed = P.seed + S;
     uint32_t* ord = P.ord + S;
     uint32_t* cstart = P.ord2 + S;  // free until the filter's reorder
+    uint32_t* code = reinterpret_cast<uint32_t*>(P.flt + S);  // free until the filter
     // keys (rb, o); seeds bridging the strands sort last and are not used
     int32_t lmax = 0;
     for (uint32_t o = lane; o < npad; o += 64) {
@@ -903,6 +933,8 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
             if (!(sd.rbeg < P.l_pac && P.l_pac < sd.rbeg + sd.len)) {
                 k = ((uint64_t)sd.rbeg << CL_OBITS) | o;
                 lmax = sd.len > lmax ? sd.len : lmax;
+            } else {
+                code[o] = CODE_SKIP;
             }
         }
         key[o] = k;
@@ -944,7 +976,7 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
     __builtin_amdgcn_wave_barrier();
     wave_bitonic(key, npad, lane);  // cluster order kept, seed order inside
     bool dup = false;
-    uint32_t n_tot = 0;
+    uint32_t n_tot = 0, n_mine = 0;
     for (uint32_t r0 = 0; r0 < n_cl; r0 += 64) {
         const uint32_t kc = r0 + lane;
         uint32_t cs = 0, ce = 0;
@@ -953,8 +985,14 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
             ce = kc + 1 < n_cl ? cstart[kc + 1] : n_valid;
         }
         uint32_t n_ch = 0;
+        bool cdup = false;
         for (uint32_t p = cs; p < ce; ++p) {
             const uint32_t o = (uint32_t)(key[p] & CL_OMASK);
+            if (cdup) {  // past an equal chain key: the tree replay decides
+                code[o] = CODE_REPLAY;
+                ++n_mine;
+                continue;
+            }
             const SeedRec sd = seed[o];
             const int64_t rb = sd.rbeg;
             // lower chain: the last list entry with pos <= rb
@@ -967,53 +1005,309 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
             const int L = lo - 1;
             bool make = true;
             if (L >= 0) {
-                const uint64_t e = key[cs + L];
-                const uint32_t id = cs + (uint32_t)(e & CL_OMASK);
+                const uint32_t id = (uint32_t)(key[cs + L] & CL_OMASK);
                 ChainRec c = chn[id];
-                // test_and_merge (software/bwamem.c:334-354)
-                if (sd.qbeg >= c.first_qbeg && sd.qbeg + sd.len <= c.last_qbeg + c.last_len && rb >= c.pos &&
-                    rb + sd.len <= c.last_rbeg + c.last_len) {
-                    make = false;  // contained
-                } else {
-                    const bool strand_ok = !((c.last_rbeg < P.l_pac || c.pos < P.l_pac) && rb >= P.l_pac);
-                    const int64_t x = (int64_t)sd.qbeg - c.last_qbeg, y = rb - c.last_rbeg;
-                    if (strand_ok && y >= 0 && x - y <= P.w && y - x <= P.w && x - c.last_len < P.max_chain_gap &&
-                        y - c.last_len < P.max_chain_gap) {
-                        P.next[S + c.last] = o;
-                        c.last = o;
-                        c.last_rbeg = rb;
-                        c.last_qbeg = sd.qbeg;
-                        c.last_len = sd.len;
-                        c.n += 1;
-                        chn[id] = c;
-                        make = false;
-                    }
+                const int mg = merge_test(P, c, rb, sd.qbeg, sd.len);
+                if (mg == MERGE_APPEND) {
+                    P.next[S + c.last] = o;
+                    chain_append(c, o, rb, sd.qbeg, sd.len);
+                    chn[id] = c;
                 }
-                if (make && c.pos == rb) dup = true;
+                make = mg == MERGE_NEW;
+                if (make && c.pos == rb) cdup = true;
             }
+            code[o] = make ? CODE_NEW : CODE_SKIP;
             if (make) {
-                ChainRec c;
-                c.pos = rb;
-                c.last_rbeg = rb;
-                c.first_qbeg = sd.qbeg;
-                c.last_qbeg = sd.qbeg;
-                c.last_len = sd.len;
-                c.n = 1;
-                c.first = c.last = o;
-                chn[cs + n_ch] = c;
-                // insert after L; the slots up to cs + n_ch are already read
-                for (int q = (int)n_ch; q > L + 1; --q) key[cs + q] = key[cs + q - 1];
-                key[cs + L + 1] = ((uint64_t)rb << CL_OBITS) | n_ch;
-                ++n_ch;
+                chn[o] = ChainRec{rb, rb, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
+                ++n_mine;
+                if (!cdup) {
+                    // insert after L; the slots up to cs + n_ch are already read
+                    for (int q = (int)n_ch; q > L + 1; --q) key[cs + q] = key[cs + q - 1];
+                    key[cs + L + 1] = ((uint64_t)rb << CL_OBITS) | o;
+                    ++n_ch;
+                }
             }
         }
+        dup = dup || cdup;
         uint32_t tot;
         const uint32_t base = wave_excl_scan(n_ch, lane, tot);
-        for (uint32_t j = 0; j < n_ch; ++j) ord[n_tot + base + j] = cs + (uint32_t)(key[cs + j] & CL_OMASK);
+        for (uint32_t j = 0; j < n_ch; ++j) ord[n_tot + base + j] = (uint32_t)(key[cs + j] & CL_OMASK);
         n_tot += tot;
     }
     n_out = (int)n_tot;
+    for (int off = 32; off > 0; off >>= 1) n_mine += __shfl_xor(n_mine, off);
+    n_cand = n_mine;
     return __ballot(dup) == 0;
+}
+
+// The kbtree pass of a read whose clusters made an equal chain key: which of
+// two equal keys kb_intervalp returns, and where kb_putp puts a new one,
+// depend on the node layout (software/kbtree.h:150-166, 193-207), so the
+// tree is rebuilt in seed order, kb_putp for every chain as it is created.
+// Chains of clean clusters, and the seeds of a dup cluster up to its first
+// equal key, are as the cluster pass decided them (exact: no equal keys
+// there yet); the later seeds of a dup cluster (CODE_REPLAY) are decided
+// here against the tree, as mem_insert_seed does.  Lane 0 walks the tree;
+// the wave loads codes and seeds 64 at a time.
+template <class N>
+__device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane) {
+    const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
+    const SeedRec* seed = P.seed + S;
+    ChainRec* chn = P.chn + S;
+    uint32_t root = 0, n_nodes = 1, n_ch = 0;
+    if (lane == 0) node_init(pool, 1);
+    for (uint32_t base = 0; base < ns; base += 64) {
+        const uint32_t o = base + (uint32_t)lane;
+        const uint32_t cd = o < ns ? code[o] : CODE_SKIP;
+        SeedRec sd{0, 0, 0};
+        if (cd != CODE_SKIP) sd = seed[o];
+        uint64_t m = __ballot(cd != CODE_SKIP);
+        while (m) {
+            const int t = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t ct = rlu(cd, t);
+            const int64_t rb = rl64(sd.rbeg, t);
+            const int32_t qb = rl32(sd.qbeg, t), ln = rl32(sd.len, t);
+            const uint32_t ot = base + (uint32_t)t;
+            if (lane == 0) {
+                bool make = true;
+                if (ct == CODE_REPLAY && n_ch) {
+                    const int lw = tree_lower(pool, root, rb);
+                    if (lw >= 0) {
+                        ChainRec c = chn[lw];
+                        const int mg = merge_test(P, c, rb, qb, ln);
+                        if (mg == MERGE_APPEND) {
+                            P.next[S + c.last] = ot;
+                            chain_append(c, ot, rb, qb, ln);
+                            chn[lw] = c;
+                        }
+                        make = mg == MERGE_NEW;
+                    }
+                }
+                if (make) {
+                    if (ct == CODE_REPLAY) chn[ot] = ChainRec{rb, rb, qb, qb, ln, 1, ot, ot};
+                    tree_insert(pool, root, n_nodes, ot, rb);
+                    ++n_ch;
+                }
+            }
+        }
+    }
+    int n = 0;
+    if (lane == 0 && n_ch) n = tree_inorder(pool, root, P.ord + S);
+    return __shfl(n, 0, 64);
+}
+
+// ---------------------------------------------------------------------------
+// ks_introsort(mem_flt) by a wave (software/ksort.h:176-224), the result of
+// flt_sort.  Segments are disjoint and each one's depth budget is fixed by
+// its depth in the recursion, so the order they are cut in does not matter:
+// segments longer than sort_lane_max are cut by the whole wave, one Hoare
+// partition at a time; shorter ones get a lane each and the serial loop.  In
+// a partition the serial scans swap the k-th left stopper (w <= pivot, from
+// the left) with the k-th right stopper (w >= pivot, from the right) while
+// the first lies left of the second -- neither scan revisits a position --
+// and the pivot goes to the first unpaired left stopper or the last paired
+// right stopper, whichever comes first.  The closing insertion sort over the
+// whole array is stable and leaves it sorted, so its result is the stable
+// sort by weight (descending) of what the partitions left: a bitonic sort of
+// (weight, position) keys and a permute.
+// ---------------------------------------------------------------------------
+
+// the serial loop from segment [s, t] with depth budget d, without the
+// closing insertion sort
+__device__ void flt_sort_seg_serial(FltRec* a, size_t s, size_t t, int d) {
+    size_t sl[64], sr[64];
+    int sd[64];
+    int top = 0;
+    for (;;) {
+        if (s < t) {
+            if (--d == 0) {
+                flt_combsort(a + s, t - s + 1);
+                t = s;
+                continue;
+            }
+            size_t i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            if (flt_lt(a[k], a[i])) {
+                if (flt_lt(a[k], a[j])) k = j;
+            } else {
+                k = flt_lt(a[j], a[i]) ? i : j;
+            }
+            const FltRec rp = a[k];
+            if (k != t) flt_swap(a, k, t);
+            for (;;) {
+                do ++i;
+                while (flt_lt(a[i], rp));
+                do --j;
+                while (i <= j && flt_lt(rp, a[j]));
+                if (j <= i) break;
+                flt_swap(a, i, j);
+            }
+            flt_swap(a, i, t);
+            if (i - s > t - i) {
+                if (i - s > 16) {
+                    sl[top] = s;
+                    sr[top] = i - 1;
+                    sd[top] = d;
+                    ++top;
+                }
+                s = t - i > 16 ? i + 1 : t;
+            } else {
+                if (t - i > 16) {
+                    sl[top] = i + 1;
+                    sr[top] = t;
+                    sd[top] = d;
+                    ++top;
+                }
+                t = i - s > 16 ? i - 1 : s;
+            }
+        } else {
+            if (top == 0) return;
+            --top;
+            s = sl[top];
+            t = sr[top];
+            d = sd[top];
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_sync_mem() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// one partition of a[s..t] (s < t) as ks_introsort makes it; returns the
+// pivot's final position.  tl / tr: the stopper positions by rank
+__device__ uint32_t flt_partition_wave(FltRec* a, uint32_t s, uint32_t t, uint32_t* tl, uint32_t* tr, int lane) {
+    uint32_t k = s + ((t - s) >> 1) + 1;
+    {
+        const int wi = a[s].w, wj = a[t].w, wk = a[k].w;  // flt_lt(x, y) = x.w > y.w
+        if (wk > wi) {
+            if (wk > wj) k = t;
+        } else {
+            k = wj > wi ? s : t;
+        }
+    }
+    const int pw = a[k].w;
+    if (k != t) {
+        if (lane == 0) flt_swap(a, k, t);
+        wave_sync_mem();
+    }
+    uint32_t tot_r = 0;
+    for (uint32_t b = s; b < t; b += 64) {
+        const uint32_t p = b + (uint32_t)lane;
+        tot_r += (uint32_t)__builtin_popcountll(__ballot(p < t && a[p].w >= pw));
+    }
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t run_l = 0, run_r = 0, K = 0;
+    for (uint32_t b = s; b <= t; b += 64) {
+        const uint32_t p = b + (uint32_t)lane;
+        const int w = p <= t ? a[p].w : 0;
+        const bool is_l = p > s && p <= t && w <= pw;
+        const bool is_r = p < t && w >= pw;
+        const uint64_t ml = __ballot(is_l), mr = __ballot(is_r);
+        const uint32_t rl = run_l + (uint32_t)__builtin_popcountll(ml & below);
+        // right stoppers after p (p's rank from the right when it is one)
+        const uint32_t after = tot_r - run_r - (uint32_t)__builtin_popcountll(mr & (below | (1ull << lane)));
+        if (is_l) tl[rl] = p;
+        if (is_r) tr[after] = p;
+        K += (uint32_t)__builtin_popcountll(__ballot(is_l && after > rl));
+        run_l += (uint32_t)__builtin_popcountll(ml);
+        run_r += (uint32_t)__builtin_popcountll(mr);
+    }
+    wave_sync_mem();
+    // the K swapped pairs touch 2K distinct positions
+    for (uint32_t q0 = 0; q0 < K; q0 += 64) {
+        const uint32_t q = q0 + (uint32_t)lane;
+        if (q < K) {
+            const uint32_t pl = tl[q], pr = tr[q];
+            const FltRec x = a[pl], y = a[pr];
+            a[pl] = y;
+            a[pr] = x;
+        }
+    }
+    wave_sync_mem();
+    uint32_t i = tl[K];  // t is a left stopper that is never swapped
+    if (K > 0) {
+        const uint32_t r = tr[K - 1];
+        i = r < i ? r : i;
+    }
+    if (lane == 0) flt_swap(a, i, t);
+    wave_sync_mem();
+    return i;
+}
+
+__device__ void wave_bitonic32(uint32_t* key, uint32_t npad, int lane) {
+    for (uint32_t k = 2; k <= npad; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = lane; t < (npad >> 1); t += 64) {
+                const uint32_t i = 2 * t - (t & (j - 1));
+                const uint32_t l = i + j;
+                const uint32_t x = key[i], y = key[l];
+                if ((x > y) == ((i & k) == 0)) {
+                    key[i] = y;
+                    key[l] = x;
+                }
+            }
+            wave_sync_mem();
+        }
+    }
+}
+
+// the whole ks_introsort(mem_flt) for n < 2^16 chains of weights in
+// [0, 2^16); small: 3 words per lane-cut segment, stk: 3 words per wave-cut
+// segment (at most 64 pending); keys: npad words; tmp: n records
+__device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t* tl, uint32_t* tr, uint32_t* keys,
+                              FltRec* tmp, uint32_t* small, uint32_t* stk, int lane) {
+    if (n < 2) return;
+    if (n == 2) {
+        if (lane == 0 && flt_lt(a[1], a[0])) flt_swap(a, 0, 1);
+        wave_sync_mem();
+        return;
+    }
+    int d = 2;
+    while ((1ull << d) < n) ++d;
+    d <<= 1;
+    uint32_t top = 0, n_small = 0;
+    auto add = [&](uint32_t s, uint32_t t, int dd) {
+        uint32_t* dst;
+        if (t - s + 1 > lane_max && top < 64) dst = stk + 3 * top++;
+        else dst = small + 3 * n_small++;
+        if (lane == 0) {
+            dst[0] = s;
+            dst[1] = t;
+            dst[2] = (uint32_t)dd;
+        }
+    };
+    add(0, n - 1, d);
+    wave_sync_mem();
+    while (top > 0) {
+        --top;
+        const uint32_t s = stk[3 * top], t = stk[3 * top + 1];
+        int dd = (int)stk[3 * top + 2];
+        wave_sync_mem();
+        if (--dd == 0) {
+            if (lane == 0) flt_combsort(a + s, t - s + 1);
+        } else {
+            const uint32_t i = flt_partition_wave(a, s, t, tl, tr, lane);
+            if (i - s > 16) add(s, i - 1, dd);
+            if (t - i > 16) add(i + 1, t, dd);
+        }
+        wave_sync_mem();
+    }
+    for (uint32_t q = lane; q < n_small; q += 64)
+        flt_sort_seg_serial(a, small[3 * q], small[3 * q + 1], (int)small[3 * q + 2]);
+    wave_sync_mem();
+    // the closing insertion sort: a stable sort by weight, descending
+    uint32_t npad = 2;
+    while (npad < n) npad <<= 1;
+    for (uint32_t p = lane; p < npad; p += 64)
+        keys[p] = p < n ? ((uint32_t)(0xFFFF - a[p].w) << 16) | p : 0xFFFFFFFFu;
+    wave_sync_mem();
+    wave_bitonic32(keys, npad, lane);
+    for (uint32_t r = lane; r < n; r += 64) tmp[r] = a[keys[r] & 0xFFFFu];
+    wave_sync_mem();
+    for (uint32_t r = lane; r < n; r += 64) a[r] = tmp[r];
+    wave_sync_mem();
 }
 
 }  // namespace
@@ -1065,6 +1359,7 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_item;
     __shared__ int64_t s_dups[256];
+    __shared__ uint32_t s_stk[3 * 64];
     const int lane = threadIdx.x;
     const uint32_t n_giant = P.heavy_ctr[0], n_all = n_giant + P.heavy_ctr[1];
     for (;;) {
@@ -1103,14 +1398,27 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             while (npad < E - S) npad <<= 1;
             if (E - S < (1ull << CL_OBITS) && (uint64_t)npad * 8 <= P.lds_bytes) {
                 int n = 0;
-                done = insert_read_clusters(P, S, E, reinterpret_cast<uint64_t*>(lds_raw), lane, n);
-                if (done && lane == 0) {
+                uint32_t n_cand = 0;
+                const bool clean =
+                    insert_read_clusters(P, S, E, reinterpret_cast<uint64_t*>(lds_raw), lane, n, n_cand);
+                if (!clean) {
+                    // an equal chain key: rebuild the tree in seed order
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    __syncthreads();
+                    if (n_cand / (BT_T - 1) + 8 <= P.lds_bytes / sizeof(LNode))
+                        n = replay_tree(P, S, (uint32_t)(E - S), reinterpret_cast<LNode*>(lds_raw), lane);
+                    else
+                        n = replay_tree(P, S, (uint32_t)(E - S), P.node + (S / 7 + 3ull * (uint64_t)r), lane);
+                }
+                if (lane == 0) {
                     s_n = n;
                     if (dbg) {
                         dbg[3] = __builtin_readcyclecounter();
                         dbg[4] = n;
+                        dbg[10] = clean ? 0 : 1;
                     }
                 }
+                done = true;
                 __syncthreads();
             }
         }
@@ -1170,7 +1478,32 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             }
             __syncthreads();
             if (dbg && lane == 0) dbg[5] = __builtin_readcyclecounter();
-            if (lane == 0) {
+            int wmin = INT32_MAX, wmax = INT32_MIN;
+            for (int i = lane; i < n; i += 64) {
+                const int w = in_lds ? la[i].w : ga[i].w;
+                wmin = w < wmin ? w : wmin;
+                wmax = w > wmax ? w : wmax;
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const int a0 = __shfl_xor(wmin, off), a1 = __shfl_xor(wmax, off);
+                wmin = a0 < wmin ? a0 : wmin;
+                wmax = a1 > wmax ? a1 : wmax;
+            }
+            if (P.wave_sort && n < 0x10000 && wmin >= 0 && wmax < 0x10000) {
+                // scratch: stopper lists and keys in LDS after the records
+                // while they fit, else (and the permute's copy always) in the
+                // read's kbtree node pool, free once the chains are listed
+                uint32_t npad = 2;
+                while (npad < (uint32_t)n) npad <<= 1;
+                const uint64_t need = (uint64_t)n * 8 + (uint64_t)npad * 4;
+                uint8_t* gs = reinterpret_cast<uint8_t*>(P.node + (S / 7 + 3ull * (uint64_t)r));
+                uint32_t* tl;
+                if (in_lds && (uint64_t)n * sizeof(FltRec) + need <= P.lds_bytes) tl = reinterpret_cast<uint32_t*>(la + n);
+                else if (!in_lds && need <= P.lds_bytes) tl = reinterpret_cast<uint32_t*>(lds_raw);
+                else tl = reinterpret_cast<uint32_t*>(gs + (uint64_t)n * sizeof(FltRec));
+                flt_sort_wave(in_lds ? la : ga, (uint32_t)n, P.sort_lane_max, tl, tl + n, tl + 2 * n,
+                              reinterpret_cast<FltRec*>(gs), ord2, s_stk, lane);
+            } else if (lane == 0) {
                 if (in_lds) flt_sort(la, (size_t)n);
                 else flt_sort(ga, (size_t)n);
             }

@@ -733,7 +733,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     HIP_TRY(b->d_node.ensure(b->tot_occ / 7 + 3ull * (uint64_t)n + 8));
     HIP_TRY(b->d_ord.ensure(no));
     HIP_TRY(b->d_ord2.ensure(no));
-    HIP_TRY(b->d_flt.ensure(opt->filter ? no : 1));
+    HIP_TRY(b->d_flt.ensure(no));  // also the heavy path's per-seed codes
     HIP_TRY(b->d_n_out.ensure(std::max(n, 1)));
     HIP_TRY(b->d_ns_out.ensure(std::max(n, 1)));
     HIP_TRY(b->d_chain_off.ensure(n + 1));
@@ -777,6 +777,9 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     if (const char* v = getenv("SMEM_CHAIN_LDS")) P.lds_bytes = (uint32_t)std::max(1024, atoi(v));
     if (const char* v = getenv("SMEM_CHAIN_HEAVY_MIN")) P.heavy_min = (uint32_t)std::max(0, atoi(v));
     P.cluster = getenv("SMEM_CHAIN_TREE_ONLY") ? 0 : 1;
+    P.wave_sort = getenv("SMEM_CHAIN_SERIAL_SORT") ? 0 : 1;
+    P.sort_lane_max = 256;
+    if (const char* v = getenv("SMEM_CHAIN_SORT_LANE_MAX")) P.sort_lane_max = (uint32_t)std::max(17, atoi(v));
     if (getenv("SMEM_CHAIN_DBG")) {
         HIP_TRY(b->d_dbg.ensure(256 * 16));
         HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 256 * 16 * sizeof(uint64_t), b->st));

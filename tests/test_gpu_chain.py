@@ -150,8 +150,12 @@ def test_chain_strand_bridging_and_empty(gpu_device):
 
 @pytest.mark.parametrize("env", [dict(SMEM_CHAIN_HEAVY_MIN="0"), dict(SMEM_CHAIN_HEAVY_MIN="100000"),
                                  dict(SMEM_CHAIN_LDS="2048"), dict(SMEM_CHAIN_TREE_ONLY="1"),
-                                 dict(SMEM_CHAIN_TREE_ONLY="1", SMEM_CHAIN_HEAVY_MIN="0")],
-                         ids=["all-wave", "all-lane", "lds-overflow", "tree-only", "tree-only-all-wave"])
+                                 dict(SMEM_CHAIN_TREE_ONLY="1", SMEM_CHAIN_HEAVY_MIN="0"),
+                                 dict(SMEM_CHAIN_SERIAL_SORT="1"),
+                                 dict(SMEM_CHAIN_SORT_LANE_MAX="17", SMEM_CHAIN_HEAVY_MIN="0"),
+                                 dict(SMEM_CHAIN_SORT_LANE_MAX="17", SMEM_CHAIN_LDS="4096")],
+                         ids=["all-wave", "all-lane", "lds-overflow", "tree-only", "tree-only-all-wave",
+                              "serial-sort", "wave-cut-sort", "wave-cut-sort-hbm"])
 def test_chain_paths_agree(gpu_device, monkeypatch, env):
     """The lane-per-read path, the wave-per-read paths (position clusters,
     and the chain tree they fall back to on equal chain keys) and the wave
@@ -178,6 +182,50 @@ def test_chain_paths_agree(gpu_device, monkeypatch, env):
             res = b.fetch()
             assert res.to_smch() == _oracle_chains(res, reads.n, l_pac, 19, 10000, filter=filt, w=5,
                                                    max_chain_gap=40)
+        b.close()
+    finally:
+        gpu.close()
+
+
+@pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_HEAVY_MIN="0"), dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_LDS="4096")],
+                         ids=["default", "all-wave", "all-wave-hbm-tree"])
+def test_chain_equal_keys_replay(gpu_device, monkeypatch, env):
+    """Reads X + Y + X whose two copies of X match one locus: test_and_merge
+    rejects the far query offset, so two chains share a pos, and the
+    position-cluster path hands the read to the kbtree replay (which of two
+    equal keys the tree returns depends on its node layout).  Chains ==
+    the restatement's, with and without the filter."""
+    import smemgpu
+    from smemgpu import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.make_genome(300_000, seed=91, repeat_frac=0.3, n_families=3, n_chrom=1)
+    G = g.codes
+    rng = np.random.default_rng(92)
+    parts = []
+    for r in range(600):
+        p = int(rng.integers(0, G.size - 500))
+        q = int(rng.integers(0, G.size - 500))
+        x = G[p:p + int(rng.integers(25, 70))]
+        parts.append(np.concatenate([x, G[q:q + int(rng.integers(101, 160))], x]).astype(np.uint8))
+    base = synth.make_reads(G, 600, 150, seed=93, sub_rate=0.01)
+    codes = np.concatenate(parts + [base.codes]).astype(np.uint8)
+    lens = [x.size for x in parts] + list(np.diff(base.offs))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    n = offs.size - 1
+    idx, sa = smemgpu.Index.build_sa(G, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        b = gpu.batch(n, codes.size, int(np.max(lens)))
+        b.set_reads(codes, offs)
+        b.run()
+        b.sa(19, 10000)
+        l_pac = idx.seq_len // 2
+        for filt in (0, 1):
+            b.chain(l_pac, filter=bool(filt))
+            res = b.fetch()
+            assert res.to_smch() == _oracle_chains(res, n, l_pac, 19, 10000, filter=filt)
         b.close()
     finally:
         gpu.close()
