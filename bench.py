@@ -107,44 +107,58 @@ def make_reads(args, rank, genome_codes=None):
                             sub_rate=args.sub, n_rate=0.001)
 
 
-def cpu_baseline(args, idx, idx_path, reads, cores):
-    """Time the CPU seeding loop on a bounded sample of the same reads."""
+def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores):
+    """The CPU leg of the bench (rank 0 only) -- the one place bench.py runs
+    anything under oracle/, as the checker and the CPU baseline, never in the
+    measured path:
+      * SURVEY.md §8(d) algorithmic bytes/read, counted by the restatement on
+        a sample of the benchmark's own reads (64 B per distinct
+        reference-layout Occ bucket of each bwt_extend + read + 32 B per
+        interval), and the same over the 32-B Occ64 buckets this build reads;
+      * parity of that sample at full index size: the GPU's smem_next2 lists
+        for those reads == the restatement's, bit for bit;
+      * the CPU baseline: the compiled reference (oracle/_ref) -- or the
+        restatement when it is absent -- timed on a bounded prefix of the
+        same reads."""
     from oracle import oracle
     from smemgpu import synth
     oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
-    # calibrate on a small slice, then size the sample for ~cpu_seconds
-    cal = reads.subset(np.arange(min(reads.n, 2000)))
-    t, _ = oracle.seed_timed(oi, cal.codes, cal.offs, threads=cores)
-    rate = cal.n / max(t, 1e-6)
-    n = int(min(reads.n, max(cal.n, rate * args.cpu_seconds)))
-    sample = reads.subset(np.arange(n))
-    kind = "port"
-    if oracle.ref_available():
-        with tempfile.TemporaryDirectory() as d:
-            p = os.path.join(d, "s.smrd")
-            synth.write_smrd(p, sample)
-            r = oracle.ref_bench(idx_path, p, cores, n)
-            secs, kind = r["seconds"], "reference"
-    else:
-        secs, _ = oracle.seed_timed(oi, sample.codes, sample.offs, threads=cores)
-    oi.close()
-    return {"value": round(n / secs, 1), "unit": "reads/s", "cores": cores, "kind": kind,
-            "sample": f"first {n} of the benchmark's {args.read_len} bp reads on rank 0, {secs:.1f} s wall, "
-                      f"{cores} pthreads"}
-
-
-def algorithmic_bytes(args, idx, reads):
-    """SURVEY.md §8(d) bytes/read (64 B per distinct reference-layout Occ bucket
-    of each bwt_extend + read + 32 B per interval), and the same with the
-    32-B Occ64 buckets this build reads, counted by the oracle on a sample."""
-    from oracle import oracle
-    oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
     n = min(reads.n, args.stats_sample)
     s = reads.subset(np.arange(n))
-    per, st = oracle.seed_stats(oi, s.codes, s.offs, threads=min(16, os.cpu_count() or 1))
-    oi.close()
+    want, per, st = oracle.seed(oi, s.codes, s.offs, threads=min(16, os.cpu_count() or 1))
+    bpr = float(per["bytes"].mean())
     b64 = (32.0 * st["n_bkt64"] + st["n_bases"] + 32.0 * st["n_intv"]) / max(n, 1)
-    return float(per["bytes"].mean()), b64, st, n
+    b = gpu.batch(s.n, int(s.codes.size), int(s.lens.max()))
+    try:
+        b.set_reads(s.codes, s.offs)
+        b.run(opt)
+        got = b.fetch().to_smgo()
+    finally:
+        b.close()
+    parity = {"reads": n, "intervals": int(st["n_intv"]), "bit_exact": got == want,
+              "against": "C restatement of the seeding loop (oracle/, pinned to the compiled reference's streams)"}
+    cpu = None
+    if args.cpu_seconds > 0:
+        # calibrate on a small slice, then size the sample for ~cpu_seconds
+        cal = reads.subset(np.arange(min(reads.n, 2000)))
+        t, _ = oracle.seed_timed(oi, cal.codes, cal.offs, threads=cores)
+        rate = cal.n / max(t, 1e-6)
+        m = int(min(reads.n, max(cal.n, rate * args.cpu_seconds)))
+        sample = reads.subset(np.arange(m))
+        kind = "port"
+        if oracle.ref_available():
+            with tempfile.TemporaryDirectory() as d:
+                p = os.path.join(d, "s.smrd")
+                synth.write_smrd(p, sample)
+                r = oracle.ref_bench(idx_path, p, cores, m)
+                secs, kind = r["seconds"], "reference"
+        else:
+            secs, _ = oracle.seed_timed(oi, sample.codes, sample.offs, threads=cores)
+        cpu = {"value": round(m / secs, 1), "unit": "reads/s", "cores": cores, "kind": kind,
+               "sample": f"first {m} of the benchmark's {args.read_len} bp reads on rank 0, {secs:.1f} s wall, "
+                         f"{cores} pthreads"}
+    oi.close()
+    return bpr, b64, st, n, parity, cpu
 
 
 def traffic_for(args, path: str):
@@ -341,15 +355,12 @@ def main():
     chain_rep = chain_report(batch, opt, idx.seq_len // 2) if rank == 0 else None
 
     if rank == 0:
-        bpr, bpr64, ostats, n_counted = algorithmic_bytes(args, idx, reads)
+        cores = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
+        bpr, bpr64, ostats, n_counted, parity, cpu = cpu_leg(args, gpu, opt, idx, idx_path, reads, cores)
         k_ms = float(np.mean(kernel_ms))
         a_ms = float(np.mean(alone_ms))
         achieved = bpr * reads.n / (k_ms * 1e-3) / 1e9
         traffic = traffic_for(args, args.traffic_json)
-        cores = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
-        cpu = None
-        if args.cpu_seconds > 0:
-            cpu = cpu_baseline(args, idx, idx_path, reads, cores)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -395,6 +406,7 @@ def main():
                 "extends_per_read": round(ostats["n_ext"] / max(n_counted, 1), 1),
             },
             "cpu_baseline": cpu,
+            "parity_sample": parity,
             "compact_ms": round(compact_alone, 3),
             "pcie_inclusive_reads_per_s": round(pcie, 1),
             "sa_lookup": sa_rep,
