@@ -24,6 +24,7 @@
 #include "smem_gpu.h"
 #include "smem_kernels.h"
 #include "chain_kernels.h"
+#include "ksw_kernels.h"
 
 using smem::CallRec;
 using smem::Intv;
@@ -857,6 +858,86 @@ int smem_batch_debug(const smem_batch_t* b, uint64_t* out, uint64_t n_words) {
     const uint64_t n = std::min<uint64_t>(n_words, b->d_dbg.n);
     if (hipMemcpy(out, b->d_dbg.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return SMEM_E_DEVICE;
     return (int)n;
+}
+
+void smem_ksw_opt_default(smem_ksw_opt_t* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    // bwa_fill_scmat(1, 4) (software/bwa.c:84-93), gaps of mem_opt_init (software/bwamem.c:50-52)
+    for (int i = 0; i < 4; ++i) {
+        for (int j = 0; j < 4; ++j) o->mat[i * 5 + j] = (int8_t)(i == j ? 1 : -4);
+        o->mat[i * 5 + 4] = -1;
+    }
+    for (int j = 0; j < 5; ++j) o->mat[20 + j] = -1;
+    o->o_del = o->o_ins = 6;
+    o->e_del = o->e_ins = 1;
+}
+
+static_assert(sizeof(smem_ksw_task_t) == sizeof(smem::KswTask), "task layout");
+static_assert(sizeof(smem_ksw_result_t) == sizeof(smem::KswResult), "result layout");
+
+int smem_ksw_extend(smem_gpu_t* g, int n, const smem_ksw_task_t* tasks, const uint8_t* q, uint64_t q_bytes,
+                    const uint8_t* t, uint64_t t_bytes, const smem_ksw_opt_t* opt, smem_ksw_result_t* out,
+                    double* kernel_ms) {
+    g_err[0] = 0;
+    if (!g || n < 0 || !opt || (n > 0 && (!tasks || !out))) return fail(SMEM_E_ARG, "smem_ksw_extend: bad arguments");
+    if (opt->e_del < 1 || opt->e_ins < 1 || opt->o_del < 0 || opt->o_ins < 0)
+        return fail(SMEM_E_ARG, "smem_ksw_extend: gap penalties need e >= 1, o >= 0");
+    for (int i = 0; i < n; ++i) {
+        const smem_ksw_task_t& k = tasks[i];
+        if (k.qlen < 1 || k.qlen > 64 * smem::KSW_COLS_PER_LANE - 1 || k.tlen < 0 || k.q_off + (uint64_t)k.qlen > q_bytes ||
+            k.t_off + (uint64_t)k.tlen > t_bytes)
+            return fail(SMEM_E_ARG, "smem_ksw_extend: task outside 1 <= qlen <= 255 or its pools");
+    }
+    if (kernel_ms) *kernel_ms = 0.0;
+    if (n == 0) return SMEM_OK;
+    HIP_TRY(hipSetDevice(g->device));
+    DevBuf<smem::KswTask> dt;
+    DevBuf<smem::KswResult> dr;
+    DevBuf<uint8_t> dq, dtg;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    struct Guard {
+        DevBuf<smem::KswTask>& a; DevBuf<smem::KswResult>& b; DevBuf<uint8_t>& c; DevBuf<uint8_t>& d;
+        hipStream_t& s; hipEvent_t* e;
+        ~Guard() {
+            a.release(); b.release(); c.release(); d.release();
+            if (e[0]) (void)hipEventDestroy(e[0]);
+            if (e[1]) (void)hipEventDestroy(e[1]);
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } guard{dt, dr, dq, dtg, st, ev};
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&ev[0]));
+    HIP_TRY(hipEventCreate(&ev[1]));
+    HIP_TRY(dt.ensure(n));
+    HIP_TRY(dr.ensure(n));
+    HIP_TRY(dq.ensure(q_bytes + 64));
+    HIP_TRY(dtg.ensure(t_bytes + 64));
+    HIP_TRY(hipMemcpyAsync(dt.p, tasks, sizeof(smem::KswTask) * n, hipMemcpyHostToDevice, st));
+    if (q_bytes) HIP_TRY(hipMemcpyAsync(dq.p, q, q_bytes, hipMemcpyHostToDevice, st));
+    if (t_bytes) HIP_TRY(hipMemcpyAsync(dtg.p, t, t_bytes, hipMemcpyHostToDevice, st));
+    smem::KswParams K;
+    std::memset(&K, 0, sizeof(K));
+    K.task = dt.p;
+    K.n = n;
+    K.q = dq.p;
+    K.t = dtg.p;
+    std::memcpy(K.mat, opt->mat, 25);
+    K.o_del = opt->o_del;
+    K.e_del = opt->e_del;
+    K.o_ins = opt->o_ins;
+    K.e_ins = opt->e_ins;
+    K.out = dr.p;
+    HIP_TRY(hipEventRecord(ev[0], st));
+    HIP_TRY(smem_launch_ksw(&K, g->n_cu, st));
+    HIP_TRY(hipEventRecord(ev[1], st));
+    HIP_TRY(hipMemcpyAsync(out, dr.p, sizeof(smem::KswResult) * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    if (kernel_ms) *kernel_ms = ms;
+    return SMEM_OK;
 }
 
 int smem_batch_stats(const smem_batch_t* b, smem_batch_stats_t* st) {

@@ -29,6 +29,7 @@ EXPORTED = [
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
     "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results", "smem_bwt_build_gpu_large",
+    "smem_ksw_opt_default", "smem_ksw_extend",
 ]
 
 
@@ -59,6 +60,12 @@ class BatchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
                 ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int),
                 ("sa_ms", C.c_double), ("n_occ", C.c_uint64), ("chain_ms", C.c_double), ("n_chains", C.c_uint64)]
+
+
+class KswOptT(C.Structure):
+    """smem_ksw_opt_t"""
+    _fields_ = [("mat", C.c_int8 * 25), ("pad", C.c_int8 * 3), ("o_del", C.c_int32), ("e_del", C.c_int32),
+                ("o_ins", C.c_int32), ("e_ins", C.c_int32)]
 
 
 class ChainOptT(C.Structure):
@@ -99,6 +106,10 @@ def load() -> C.CDLL:
     lib.smem_gpu_load_sa.argtypes = [C.c_void_p, P(SaT)]
     lib.smem_batch_sa.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.smem_batch_sa_results.argtypes = [C.c_void_p, P(P(C.c_uint64)), P(P(C.c_uint64)), P(C.c_uint64)]
+    lib.smem_ksw_opt_default.argtypes = [P(KswOptT)]
+    lib.smem_ksw_opt_default.restype = None
+    lib.smem_ksw_extend.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                    P(KswOptT), C.c_void_p, P(C.c_double)]
     lib.smem_chain_opt_default.argtypes = [P(ChainOptT)]
     lib.smem_chain_opt_default.restype = None
     lib.smem_batch_chain.argtypes = [C.c_void_p, C.c_int64, P(ChainOptT)]
@@ -351,6 +362,24 @@ class Gpu:
 
     def batch(self, max_reads: int, max_bases: int, max_len: int) -> "Batch":
         return Batch(self, max_reads, max_bases, max_len)
+
+    def ksw_extend(self, kb) -> tuple:
+        """ksw_extend2 (software/ksw.c:379) of every task of a synth.KswBatch on
+        this device: (results as synth.KSW_RESULT, kernel ms)."""
+        from . import synth
+        lib = load()
+        tasks = np.ascontiguousarray(kb.tasks, dtype=synth.KSW_TASK)
+        q = np.ascontiguousarray(kb.q, dtype=np.uint8)
+        t = np.ascontiguousarray(kb.t, dtype=np.uint8)
+        o = KswOptT()
+        for i, v in enumerate(np.asarray(kb.mat, dtype=np.int8)):
+            o.mat[i] = int(v)
+        o.o_del, o.e_del, o.o_ins, o.e_ins = kb.o_del, kb.e_del, kb.o_ins, kb.e_ins
+        out = np.zeros(max(tasks.size, 1), dtype=synth.KSW_RESULT)
+        ms = C.c_double()
+        _check(lib.smem_ksw_extend(self._h, tasks.size, tasks.ctypes.data, q.ctypes.data, q.size, t.ctypes.data,
+                                   t.size, C.byref(o), out.ctypes.data, C.byref(ms)), "smem_ksw_extend")
+        return out[:tasks.size], ms.value
 
     def close(self) -> None:
         if self._h:

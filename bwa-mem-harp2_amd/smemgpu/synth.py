@@ -306,3 +306,147 @@ def write_smch(per_read) -> bytes:
             parts.append(struct.pack("<qI", int(cpos), seeds.size))
             parts.append(seeds.tobytes())
     return b"".join(parts)
+
+
+# ---- SW extension tasks (ksw_extend2, software/ksw.c:379) ------------------
+KSW_TASK = np.dtype([("q_off", "<u8"), ("t_off", "<u8"), ("qlen", "<i4"), ("tlen", "<i4"), ("w", "<i4"),
+                     ("end_bonus", "<i4"), ("zdrop", "<i4"), ("h0", "<i4")])   # smem_ksw_task_t, 40 B
+KSW_RESULT = np.dtype([(k, "<i4") for k in ("score", "qle", "tle", "gtle", "gscore", "max_off")])
+
+
+def bwa_scmat(a: int = 1, b: int = 4) -> np.ndarray:
+    """The m = 5 scoring matrix bwa_fill_scmat builds (software/bwa.c:84-93)."""
+    m = np.full((5, 5), -1, dtype=np.int8)
+    for i in range(4):
+        for j in range(4):
+            m[i, j] = a if i == j else -b
+    return m.reshape(-1)
+
+
+@dataclass
+class KswBatch:
+    tasks: np.ndarray   # KSW_TASK
+    q: np.ndarray       # uint8 codes 0..4
+    t: np.ndarray
+    mat: np.ndarray     # int8[25]
+    o_del: int = 6
+    e_del: int = 1
+    o_ins: int = 6
+    e_ins: int = 1
+
+
+def _mutated_copy(src: np.ndarray, rng, sub: float, indel: float) -> np.ndarray:
+    out = []
+    i = 0
+    while i < src.size:
+        r = rng.random()
+        if r < indel / 2:            # insertion in the copy
+            out.append(int(rng.integers(0, 4)))
+            continue
+        if r < indel:                # deletion from the copy
+            i += 1
+            continue
+        c = int(src[i])
+        if rng.random() < sub:
+            c = (c + int(rng.integers(1, 4))) & 3
+        out.append(c)
+        i += 1
+    return np.array(out, dtype=np.uint8)
+
+
+def make_ksw_tasks(genome_codes: np.ndarray, n: int, seed: int = 1, max_qlen: int = 255) -> KswBatch:
+    """Extension problems shaped like mem_chain2aln's (software/bwamem.c:1120-1170):
+    from a seed inside a read sampled with substitutions and indels, the
+    left extension (reversed prefix vs the reversed reference before the seed)
+    and the right one (suffix vs the reference after it), the reference
+    window padded by up to a band; plus unrelated sequences, N bases, tiny
+    and empty problems, narrow / doubled bands, z-drop off."""
+    rng = np.random.default_rng(seed)
+    G = genome_codes
+    tasks = np.zeros(n, dtype=KSW_TASK)
+    qs, ts = [], []
+    qo = to = 0
+    for k in range(n):
+        kind = rng.random()
+        w = 100 if rng.random() < 0.8 else (200 if rng.random() < 0.5 else int(rng.integers(1, 21)))
+        zdrop = 100 if rng.random() < 0.9 else (0 if rng.random() < 0.5 else int(rng.integers(1, 30)))
+        end_bonus = 5 if rng.random() < 0.9 else int(rng.integers(0, 20))
+        if kind < 0.04:     # tiny / empty
+            qlen = int(rng.integers(1, 6))
+            q = rng.integers(0, 5, size=qlen).astype(np.uint8)
+            t = rng.integers(0, 5, size=int(rng.integers(0, 6))).astype(np.uint8)
+            h0 = int(rng.integers(0, 40))
+        elif kind < 0.12:   # unrelated
+            qlen = int(rng.integers(1, max_qlen + 1))
+            q = rng.integers(0, 4, size=qlen).astype(np.uint8)
+            t = rng.integers(0, 4, size=int(rng.integers(0, qlen + 120))).astype(np.uint8)
+            h0 = int(rng.integers(0, 80))
+        else:
+            L = int(rng.choice([100, 150, 250]))
+            pos = int(rng.integers(300, G.size - L - 600))
+            ref = G[pos - 250:pos + L + 250]
+            read = _mutated_copy(G[pos:pos + L], rng, float(rng.choice([0.0, 0.02, 0.05])), 0.004)
+            if rng.random() < 0.1:
+                read[rng.random(read.size) < 0.02] = 4
+            if read.size < 30:
+                read = G[pos:pos + L].copy()
+            sl = int(rng.integers(19, min(60, read.size - 1)))
+            q0 = int(rng.integers(0, read.size - sl + 1))
+            pad = int(rng.integers(0, 110))
+            if rng.random() < 0.5:  # left extension: reversed prefix, reversed reference before the seed
+                q = read[:q0][::-1].copy()
+                r0 = 250 + q0
+                t = ref[max(0, r0 - q0 - pad):r0][::-1].copy()
+                h0 = sl
+            else:                    # right extension: suffix after the seed
+                q = read[q0 + sl:].copy()
+                r0 = 250 + q0 + sl
+                t = ref[r0:r0 + q.size + pad].copy()
+                h0 = int(rng.integers(sl, sl + 120))
+            if q.size == 0:
+                q = read[:1].copy()
+            q = q[:max_qlen]
+            qlen = q.size
+        tasks[k] = (qo, to, qlen, t.size, w, end_bonus, zdrop, h0)
+        qs.append(q)
+        ts.append(t)
+        qo += q.size
+        to += t.size
+    qpool = np.concatenate(qs).astype(np.uint8) if qs else np.zeros(0, np.uint8)
+    tpool = np.concatenate(ts).astype(np.uint8) if ts else np.zeros(0, np.uint8)
+    return KswBatch(tasks, qpool, tpool, bwa_scmat())
+
+
+def write_smkt(path: str, b: KswBatch) -> None:
+    with open(path, "wb") as fh:
+        fh.write(b"SMKT0001")
+        fh.write(struct.pack("<QQQ", b.tasks.size, b.q.size, b.t.size))
+        fh.write(np.asarray(b.mat, dtype=np.int8).tobytes() + b"\0\0\0")
+        fh.write(struct.pack("<4i", b.o_del, b.e_del, b.o_ins, b.e_ins))
+        fh.write(b.tasks.astype(KSW_TASK).tobytes())
+        fh.write(b.q.astype(np.uint8).tobytes())
+        fh.write(b.t.astype(np.uint8).tobytes())
+
+
+def read_smkt(data: bytes) -> KswBatch:
+    if data[:8] != b"SMKT0001":
+        raise ValueError("not an SMKT file")
+    n, qb, tb = struct.unpack_from("<QQQ", data, 8)
+    o = 32
+    mat = np.frombuffer(data, dtype=np.int8, count=25, offset=o).copy()
+    o += 28
+    o_del, e_del, o_ins, e_ins = struct.unpack_from("<4i", data, o)
+    o += 16
+    tasks = np.frombuffer(data, dtype=KSW_TASK, count=n, offset=o).copy()
+    o += n * KSW_TASK.itemsize
+    q = np.frombuffer(data, dtype=np.uint8, count=qb, offset=o).copy()
+    o += qb
+    t = np.frombuffer(data, dtype=np.uint8, count=tb, offset=o).copy()
+    return KswBatch(tasks, q, t, mat, o_del, e_del, o_ins, e_ins)
+
+
+def read_smkr(data: bytes) -> np.ndarray:
+    if data[:8] != b"SMKR0001":
+        raise ValueError("not an SMKR file")
+    (n,) = struct.unpack_from("<Q", data, 8)
+    return np.frombuffer(data, dtype=KSW_RESULT, count=n, offset=16).copy()

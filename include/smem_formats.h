@@ -34,6 +34,18 @@
  *   per read:  uint32_t n_chains
  *              per chain: int64_t pos ; uint32_t n ;
  *                         n x { int64_t rbeg ; int32_t qbeg ; int32_t len }  (mem_seed_t)
+ *
+ * SW extension tasks file ("SMKT0001") — ksw_extend2 calls
+ * (software/ksw.c:379) with m = 5:
+ *   char     magic[8]      = "SMKT0001"
+ *   uint64_t n_tasks, q_bytes, t_bytes
+ *   int8_t   mat[25] ; int8_t pad[3] ; int32_t o_del, e_del, o_ins, e_ins
+ *   n_tasks x { uint64_t q_off, t_off ; int32_t qlen, tlen, w, end_bonus, zdrop, h0 }
+ *   uint8_t  q[q_bytes] ; uint8_t t[t_bytes]        codes 0..4
+ * SW extension results file ("SMKR0001"):
+ *   char     magic[8]      = "SMKR0001"
+ *   uint64_t n_tasks
+ *   n_tasks x { int32_t score (the return value), qle, tle, gtle, gscore, max_off }
  */
 #ifndef SMEM_FORMATS_H
 #define SMEM_FORMATS_H
@@ -47,6 +59,8 @@
 #define SMGO_MAGIC "SMGO0001"
 #define SMSA_MAGIC "SMSA0001"
 #define SMCH_MAGIC "SMCH0001"
+#define SMKT_MAGIC "SMKT0001"
+#define SMKR_MAGIC "SMKR0001"
 
 typedef struct {
 	uint64_t n_reads, n_bases;

@@ -204,6 +204,35 @@ int  smem_batch_chain(smem_batch_t *b, int64_t l_pac, const smem_chain_opt_t *op
 int  smem_batch_chain_results(const smem_batch_t *b, const smem_chain_t **chains, const uint64_t **chain_off,
                               const smem_seed_t **seeds, uint64_t *n_chains, uint64_t *n_seeds);
 
+/* --------------------------------------------------- SW extension */
+/* one ksw_extend2 call (software/ksw.c:379) as mem_chain2aln makes it
+ * (software/bwamem.c:1136, 1164): query / target are offsets into the code
+ * pools (0..4; the left extension's reversed sequences as the caller builds
+ * them), m = 5 */
+typedef struct {
+	uint64_t q_off, t_off;
+	int32_t qlen, tlen;       /* 1 <= qlen <= 255, tlen >= 0 */
+	int32_t w, end_bonus, zdrop, h0;
+} smem_ksw_task_t;
+/* the return value and the five out-parameters of ksw_extend2 */
+typedef struct {
+	int32_t score, qle, tle, gtle, gscore, max_off;
+} smem_ksw_result_t;
+typedef struct {
+	int8_t mat[25], pad[3];   /* bwa_fill_scmat (software/bwa.c:84-93) */
+	int32_t o_del, e_del, o_ins, e_ins;
+} smem_ksw_opt_t;
+/* mem_opt_init's scoring (software/bwamem.c:50-52): a 1, b 4, gaps 6 + 1 */
+void smem_ksw_opt_default(smem_ksw_opt_t *opt);
+/* ksw_extend2 of every task on the GPU, results in task order: the same
+ * values the reference returns.  Host buffers in and out; kernel_ms (may be
+ * NULL) gets the kernel's HIP-event time.  SMEM_E_ARG for a task outside the
+ * limits above or gap penalties with e < 1 or o < 0 (the caller extends
+ * those on the CPU, as the reference's reject path would). */
+int  smem_ksw_extend(smem_gpu_t *gpu, int n, const smem_ksw_task_t *tasks, const uint8_t *q, uint64_t q_bytes,
+                     const uint8_t *t, uint64_t t_bytes, const smem_ksw_opt_t *opt, smem_ksw_result_t *out,
+                     double *kernel_ms);
+
 /* ---------------------------------------------------------- telemetry */
 typedef struct {
 	double kernel_ms;        /* seeding kernel(s), HIP events on the batch stream */

@@ -46,6 +46,11 @@ class ChainOptT(C.Structure):
                 ("drop_ratio", C.c_float), ("filter", C.c_int)]
 
 
+class KswOptT(C.Structure):
+    _fields_ = [("mat", C.c_int8 * 25), ("pad", C.c_int8 * 3), ("o_del", C.c_int32), ("e_del", C.c_int32),
+                ("o_ins", C.c_int32), ("e_ins", C.c_int32)]
+
+
 _lib = None
 
 
@@ -81,6 +86,8 @@ def load() -> C.CDLL:
         lib.orc_sa_lookup.restype = C.c_uint64
         lib.orc_sa_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int]
         lib.orc_sa_batch.restype = None
+        lib.orc_ksw_batch.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(KswOptT), C.c_void_p]
+        lib.orc_ksw_batch.restype = C.c_int
         lib.orc_chain.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(ChainOptT), C.c_int,
                                   C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64)]
         _lib = lib
@@ -297,3 +304,32 @@ def chain(seeds, seed_off, l_pac: int, w=100, max_chain_gap=10000, min_seed_len=
     data = C.string_at(out, out_len.value)
     lib.orc_free(out)
     return data
+
+
+# ---- SW extension (ksw_oracle.c) -------------------------------------------
+def ksw_opt(batch) -> KswOptT:
+    o = KswOptT()
+    for i, v in enumerate(np.asarray(batch.mat, dtype=np.int8)):
+        o.mat[i] = int(v)
+    o.o_del, o.e_del, o.o_ins, o.e_ins = batch.o_del, batch.e_del, batch.o_ins, batch.e_ins
+    return o
+
+
+def ksw(batch) -> np.ndarray:
+    """The restated ksw_extend2 on every task of a synth.KswBatch."""
+    from smemgpu import synth
+    lib = load()
+    tasks = np.ascontiguousarray(batch.tasks, dtype=synth.KSW_TASK)
+    q = np.ascontiguousarray(batch.q, dtype=np.uint8)
+    t = np.ascontiguousarray(batch.t, dtype=np.uint8)
+    out = np.zeros(max(tasks.size, 1), dtype=synth.KSW_RESULT)
+    o = ksw_opt(batch)
+    rc = lib.orc_ksw_batch(tasks.size, tasks.ctypes.data, q.ctypes.data, t.ctypes.data, C.byref(o), out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("orc_ksw_batch failed")
+    return out[:tasks.size]
+
+
+def ref_ksw(smkt: str, out: str) -> None:
+    """The compiled reference's own ksw_extend2 on every task of an SMKT file."""
+    subprocess.run([REF, "ksw", smkt, out], check=True)

@@ -298,6 +298,48 @@ static int cmd_chain(int argc, char **argv)
 	return 0;
 }
 
+/* ksw <tasks.smkt> <out.smkr>: the reference's own ksw_extend2 on every task */
+extern int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m, const int8_t *mat,
+		int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle,
+		int *_gtle, int *_gscore, int *_max_off);
+
+typedef struct { uint64_t q_off, t_off; int32_t qlen, tlen, w, end_bonus, zdrop, h0; } ksw_task_t;
+
+static int cmd_ksw(int argc, char **argv)
+{
+	char magic[8];
+	uint64_t n, qb, tb, i;
+	int8_t mat[28];
+	int32_t pen[4];
+	ksw_task_t *T;
+	uint8_t *q, *t;
+	FILE *fp, *out;
+	if (argc < 3) { fprintf(stderr, "usage: ksw <tasks.smkt> <out.smkr>\n"); return 1; }
+	fp = fopen(argv[1], "rb");
+	if (!fp) return 1;
+	if (fread(magic, 1, 8, fp) != 8 || memcmp(magic, SMKT_MAGIC, 8) != 0) return 1;
+	if (fread(&n, 8, 1, fp) != 1 || fread(&qb, 8, 1, fp) != 1 || fread(&tb, 8, 1, fp) != 1) return 1;
+	if (fread(mat, 1, 28, fp) != 28 || fread(pen, 4, 4, fp) != 4) return 1;
+	T = malloc(sizeof(ksw_task_t) * (n ? n : 1));
+	q = malloc(qb ? qb : 1);
+	t = malloc(tb ? tb : 1);
+	if (fread(T, sizeof(ksw_task_t), n, fp) != n || fread(q, 1, qb, fp) != qb || fread(t, 1, tb, fp) != tb) return 1;
+	fclose(fp);
+	out = fopen(argv[2], "wb");
+	if (!out) return 1;
+	fwrite(SMKR_MAGIC, 1, 8, out);
+	fwrite(&n, 8, 1, out);
+	for (i = 0; i < n; ++i) {
+		int32_t r[6];
+		r[0] = ksw_extend2(T[i].qlen, q + T[i].q_off, T[i].tlen, t + T[i].t_off, 5, mat, pen[0], pen[1], pen[2], pen[3],
+				T[i].w, T[i].end_bonus, T[i].zdrop, T[i].h0, &r[1], &r[2], &r[3], &r[4], &r[5]);
+		fwrite(r, 4, 6, out);
+	}
+	fclose(out);
+	free(T); free(q); free(t);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	if (argc < 2) {
@@ -314,6 +356,7 @@ int main(int argc, char **argv)
 	if (strcmp(argv[1], "bench") == 0) return cmd_bench(argc - 1, argv + 1);
 	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
 	if (strcmp(argv[1], "chain") == 0) return cmd_chain(argc - 1, argv + 1);
+	if (strcmp(argv[1], "ksw") == 0) return cmd_ksw(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

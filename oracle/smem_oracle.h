@@ -118,4 +118,19 @@ int orc_chain(int64_t n_reads, const orc_seed_t *seeds, const uint64_t *seed_off
 #ifdef __cplusplus
 }
 #endif
+/* ---- SW extension (ksw_oracle.c): ksw_extend2, software/ksw.c:379-476 ---- */
+typedef struct {
+	uint64_t q_off, t_off;          /* into the query / target code pools (0..4) */
+	int32_t qlen, tlen, w, end_bonus, zdrop, h0;
+} orc_ksw_task_t;                   /* the layout of smem_ksw_task_t */
+typedef struct { int32_t score, qle, tle, gtle, gscore, max_off; } orc_ksw_result_t;
+typedef struct {
+	int8_t mat[25], pad[3];          /* m = 5 */
+	int32_t o_del, e_del, o_ins, e_ins;
+} orc_ksw_opt_t;
+int orc_ksw_extend(const orc_ksw_task_t *t, const uint8_t *query, const uint8_t *target, const orc_ksw_opt_t *o,
+		orc_ksw_result_t *res);
+int orc_ksw_batch(int64_t n, const orc_ksw_task_t *tasks, const uint8_t *q, const uint8_t *t, const orc_ksw_opt_t *o,
+		orc_ksw_result_t *out);
+
 #endif

@@ -21,9 +21,13 @@ reference code itself:
   manifest.json       cases, options, sha256 of the uncompressed streams
 
   g2.*, g2_<case>*     the same for a repeat-dense genome (make_g2)
+  ksw.smkt.gz         5000 SW extension problems (include/smem_formats.h) shaped like
+                      mem_chain2aln's left/right extensions on g1 (software/bwamem.c:1120-1170)
+  ksw.smkr.gz         the reference's own ksw_extend2 on each (software/ksw.c:379)
 
     python tests/golden/make_golden.py --chains-only   # (re)make only the g1 .smch files
     python tests/golden/make_golden.py --g2-only       # (re)make only the g2 set
+    python tests/golden/make_golden.py --ksw-only      # (re)make only the ksw set
 """
 import gzip
 import hashlib
@@ -246,11 +250,33 @@ def main():
         shutil.rmtree(tmp)
 
 
+def make_ksw():
+    if not oracle.ref_available():
+        oracle.build(ref=True)
+    tmp = tempfile.mkdtemp()
+    try:
+        with gzip.open(os.path.join(HERE, "g1.fa.gz"), "rb") as fh:
+            from tests import golden_data
+            g = golden_data.fasta_codes(fh.read())
+        b = synth.make_ksw_tasks(g, 5000, seed=121)
+        p = os.path.join(tmp, "ksw.smkt")
+        synth.write_smkt(p, b)
+        oracle.ref_ksw(p, os.path.join(tmp, "ksw.smkr"))
+        for name in ("ksw.smkt", "ksw.smkr"):
+            with open(os.path.join(tmp, name), "rb") as fh:
+                gz_write(os.path.join(HERE, name + ".gz"), fh.read())
+    finally:
+        shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
-    if "--chains-only" in sys.argv:
+    if "--ksw-only" in sys.argv:
+        make_ksw()
+    elif "--chains-only" in sys.argv:
         chains_only()
     elif "--g2-only" in sys.argv:
         make_g2()
     else:
         main()
         make_g2()
+        make_ksw()

@@ -238,3 +238,31 @@ def test_oracle_g2_streams_match_reference(tmp_path):
         assert np.array_equal(osa.lookup(oi, k), exp)
     osa.close()
     oi.close()
+
+
+def test_ksw_oracle_matches_reference_golden():
+    """The restated ksw_extend2 (oracle/ksw_oracle.c) == the compiled reference's
+    own ksw_extend2 (software/ksw.c:379) on 5000 extension problems."""
+    from smemgpu import synth
+    from tests import golden_data
+    b = synth.read_smkt(golden_data.gz("ksw.smkt.gz"))
+    want = synth.read_smkr(golden_data.gz("ksw.smkr.gz"))
+    assert b.tasks.size == want.size == 5000
+    assert np.array_equal(oracle.ksw(b), want)
+
+
+def test_ksw_oracle_matches_reference_live(tmp_path):
+    """Fresh problems under other scoring (a=2 b=3, o_del 5 e_del 2, o_ins 4
+    e_ins 1), checked against the reference binary when it is built."""
+    from smemgpu import synth
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    g = synth.make_genome(100_000, seed=131, n_chrom=1)
+    b = synth.make_ksw_tasks(g.codes, 1500, seed=132)
+    b.mat = synth.bwa_scmat(2, 3)
+    b.o_del, b.e_del, b.o_ins, b.e_ins = 5, 2, 4, 1
+    p = str(tmp_path / "t.smkt")
+    synth.write_smkt(p, b)
+    oracle.ref_ksw(p, str(tmp_path / "r.smkr"))
+    want = synth.read_smkr(open(tmp_path / "r.smkr", "rb").read())
+    assert np.array_equal(oracle.ksw(b), want)
