@@ -107,7 +107,7 @@ def make_reads(args, rank, genome_codes=None):
                             sub_rate=args.sub, n_rate=0.001)
 
 
-def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores):
+def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
     """The CPU leg of the bench (rank 0 only) -- the one place bench.py runs
     anything under oracle/, as the checker and the CPU baseline, never in the
     measured path:
@@ -119,7 +119,8 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores):
         for those reads == the restatement's, bit for bit;
       * the CPU baseline: the compiled reference (oracle/_ref) -- or the
         restatement when it is absent -- timed on a bounded prefix of the
-        same reads."""
+        same reads;
+      * with sw_tasks, the SW stage's CPU baseline (sw_cpu)."""
     from oracle import oracle
     from smemgpu import synth
     oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
@@ -158,7 +159,8 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores):
                "sample": f"first {m} of the benchmark's {args.read_len} bp reads on rank 0, {secs:.1f} s wall, "
                          f"{cores} pthreads"}
     oi.close()
-    return bpr, b64, st, n, parity, cpu
+    sw = sw_cpu(sw_tasks) if (sw_tasks is not None and args.cpu_seconds > 0) else None
+    return bpr, b64, st, n, parity, cpu, sw
 
 
 def traffic_for(args, path: str):
@@ -278,6 +280,44 @@ def chain_report(batch, opt, l_pac: int, reps: int = 3) -> dict:
             "what": "mem_chain (kbtree of chains, test_and_merge) + mem_chain_flt, w 100, max_chain_gap 10000"}
 
 
+def sw_report(gpu, genome_codes, n_unique: int = 20000, tile: int = 10, reps: int = 3):
+    """SW extension: ksw_extend2 on the GPU over
+    problems shaped like mem_chain2aln's left/right extensions, drawn from the
+    bench genome (n_unique distinct problems, the batch tiled `tile` times);
+    reported beside the SMEM metric.  Returns (report, the distinct problems)."""
+    from smemgpu import synth
+    kb = synth.make_ksw_tasks(genome_codes, n_unique, seed=771)
+    big = synth.KswBatch(np.tile(kb.tasks, tile), kb.q, kb.t, kb.mat)
+    best = float("inf")
+    for _ in range(reps):
+        _, ms = gpu.ksw_extend(big)
+        best = min(best, ms)
+    cells = int(np.sum(kb.tasks["qlen"].astype(np.int64) * kb.tasks["tlen"])) * tile
+    return {"tasks": int(big.tasks.size), "kernel_ms": round(best, 3),
+            "tasks_per_s": round(big.tasks.size / (best * 1e-3), 1),
+            "what": "ksw_extend2 (software/ksw.c:379), one wave per problem; synthetic mem_chain2aln-shaped "
+                    "left/right extensions of 100-250 bp reads (2-5% subs, 0.4% indels), w 100 (some 200 / narrow), "
+                    "zdrop 100, end_bonus 5", "qlen_x_tlen_cells_upper_bound": cells}, kb
+
+
+def sw_cpu(kb) -> dict:
+    """The compiled reference's own ksw_extend2 (oracle/_ref ref_harness ksw,
+    one thread) on the same distinct problems: the SW stage's CPU baseline
+    (run from cpu_leg)."""
+    from oracle import oracle
+    from smemgpu import synth
+    if not oracle.ref_available():
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "t.smkt")
+        synth.write_smkt(p, kb)
+        t = time.perf_counter()
+        oracle.ref_ksw(p, os.path.join(d, "r.smkr"))
+        secs = time.perf_counter() - t
+    return {"value": round(kb.tasks.size / secs, 1), "unit": "tasks/s", "cores": 1, "kind": "reference",
+            "sample": f"{kb.tasks.size} problems, {secs:.2f} s incl. file I/O"}
+
+
 def main():
     args = parse()
     import torch
@@ -288,7 +328,11 @@ def main():
     barrier = d.barrier
 
     idx, idx_path, sa = get_index(args, rank, world, barrier, d.gpu)
-    reads = make_reads(args, rank)
+    genome_codes = None
+    if rank == 0:
+        from smemgpu import synth
+        genome_codes = synth.make_genome(int(args.genome_mbp * 1e6), seed=args.seed, n_chrom=24).codes
+    reads = make_reads(args, rank, genome_codes)
     gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu)
     gpu.load_sa(sa)
     # one batch object (own HIP stream, own buffers) per host worker, each
@@ -353,10 +397,15 @@ def main():
     pcie = pcie_inclusive(batch, reads, opt) if rank == 0 else None
     sa_rep = sa_lookup(batch, opt) if rank == 0 else None
     chain_rep = chain_report(batch, opt, idx.seq_len // 2) if rank == 0 else None
+    sw_rep, sw_tasks = sw_report(gpu, genome_codes) if rank == 0 else (None, None)
+    del genome_codes
 
     if rank == 0:
         cores = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
-        bpr, bpr64, ostats, n_counted, parity, cpu = cpu_leg(args, gpu, opt, idx, idx_path, reads, cores)
+        bpr, bpr64, ostats, n_counted, parity, cpu, sw_cpu_rep = cpu_leg(args, gpu, opt, idx, idx_path, reads, cores,
+                                                                          sw_tasks)
+        if sw_rep is not None:
+            sw_rep["cpu_baseline"] = sw_cpu_rep
         k_ms = float(np.mean(kernel_ms))
         a_ms = float(np.mean(alone_ms))
         achieved = bpr * reads.n / (k_ms * 1e-3) / 1e9
@@ -411,6 +460,7 @@ def main():
             "pcie_inclusive_reads_per_s": round(pcie, 1),
             "sa_lookup": sa_rep,
             "chaining": chain_rep,
+            "sw_extension": sw_rep,
             "overflow_reads": st["n_overflow"],
         }
         print(json.dumps(out), flush=True)
