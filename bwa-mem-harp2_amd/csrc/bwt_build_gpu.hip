@@ -391,38 +391,65 @@ __global__ void __launch_bounds__(256) bin_hist(const uint8_t* __restrict__ T, u
     }
 }
 
-// positions whose bin is in [blo, bhi), with their K0-symbol key; order of
-// the output is arbitrary (it is sorted next)
-__global__ void __launch_bounds__(256) bin_gather(const uint8_t* __restrict__ T, uint64_t n, uint64_t blo,
-                                                  uint64_t bhi, uint64_t* __restrict__ key, uint64_t* __restrict__ pos,
-                                                  unsigned long long* __restrict__ cnt) {
-    constexpr int PER = 16;
-    const uint64_t p0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * PER;
-    uint64_t b = 0;
-    if (p0 < n)
-        for (int d = 0; d < PB - 1; ++d) b = (b << 3) | sym3(T, n, p0 + d);
-    for (int k = 0; k < PER; ++k) {
-        const uint64_t p = p0 + k;
-        bool hit = false;
-        if (p < n) {
-            b = ((b << 3) | sym3(T, n, p + PB - 1)) & ((1ull << BIN_BITS) - 1);
-            hit = b >= blo && b < bhi;
+// Counting sort of all suffixes by bin into the SA array (one pass; the
+// order inside a bin is arbitrary, the super-bucket sort fixes it).  Block b
+// takes positions [b SC, (b + 1) SC): an LDS histogram of its full-length
+// prefixes, one global reservation per (block, bin), then the positions.
+constexpr int SC = 1 << 18;  // positions per block
+__global__ void __launch_bounds__(256) bin_scatter(const uint8_t* __restrict__ T, uint64_t n,
+                                                   unsigned long long* __restrict__ cursor, uint64_t* __restrict__ sa) {
+    constexpr int NC = 1 << (2 * PB);
+    __shared__ uint32_t cnt[NC];
+    __shared__ uint64_t base[NC];
+    for (int i = threadIdx.x; i < NC; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    constexpr int PER = SC / 256;
+    const uint64_t p0 = (uint64_t)blockIdx.x * SC + (uint64_t)threadIdx.x * PER;
+    const uint64_t last = n >= PB ? n - PB : 0;  // positions <= last have all PB symbols
+    auto walk = [&](auto&& f) {
+        if (n < PB || p0 > last) return;
+        uint32_t code = 0;
+        for (int d = 0; d < PB - 1; ++d) code = (code << 2) | T[p0 + d];
+        for (int k = 0; k < PER && p0 + k <= last; ++k) {
+            code = ((code << 2) | T[p0 + k + PB - 1]) & (NC - 1);
+            f(code, p0 + k);
         }
-        const unsigned long long m = __ballot(hit);
-        if (!m) continue;
-        const int lane = threadIdx.x & 63;
-        const int leader = __ffsll((long long)m) - 1;
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(cnt, (unsigned long long)__popcll(m));
-        base = __shfl(base, leader);
-        if (hit) {
-            const uint64_t slot = base + __popcll(m & ((1ull << lane) - 1));
-            uint64_t kk = b;
-            for (int d = PB; d < K0; ++d) kk = (kk << 3) | sym3(T, n, p + d);
-            key[slot] = kk;
-            pos[slot] = p;
+    };
+    walk([&](uint32_t c, uint64_t) { atomicAdd(&cnt[c], 1u); });
+    __syncthreads();
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+        const uint32_t v = cnt[c];
+        if (v) {
+            uint64_t b = 0;
+            for (int d = PB - 1; d >= 0; --d) b = (b << 3) | (((c >> (2 * d)) & 3) + 1);
+            base[c] = atomicAdd(&cursor[b], (unsigned long long)v);
         }
+        cnt[c] = 0;
     }
+    __syncthreads();
+    walk([&](uint32_t c, uint64_t p) { sa[base[c] + atomicAdd(&cnt[c], 1u)] = p; });
+}
+
+// the PB - 1 suffixes too short for a full prefix
+__global__ void bin_scatter_tail(const uint8_t* __restrict__ T, uint64_t n, unsigned long long* __restrict__ cursor,
+                                 uint64_t* __restrict__ sa) {
+    const uint64_t p = (n >= PB ? n - PB + 1 : 0) + threadIdx.x;
+    if (p >= n) return;
+    uint64_t b = 0;
+    for (int d = 0; d < PB; ++d) b = (b << 3) | sym3(T, n, p + d);
+    sa[atomicAdd(&cursor[b], 1ull)] = p;
+}
+
+// a super-bucket's positions (SA rows [base, base + m)) with their K0-symbol keys
+__global__ void sb_load(const uint8_t* __restrict__ T, uint64_t n, const uint64_t* __restrict__ sa, uint64_t base,
+                        uint64_t m, uint64_t* __restrict__ key, uint64_t* __restrict__ pos) {
+    const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint64_t p = sa[base + j];
+    uint64_t k = 0;
+    for (int d = 0; d < K0; ++d) k = (k << 3) | sym3(T, n, p + d);
+    key[j] = k;
+    pos[j] = p;
 }
 
 // after the super-bucket sort: SA range, group heads (key changes)
@@ -523,7 +550,10 @@ static int build_gpu_large(int device, const uint8_t* fwd, uint64_t n_fwd, int s
                     (unsigned long long)n);
             return SMEM_E_INTERNAL;
         }
-        uint64_t cap = std::max(std::min(SB_MAX, n), big);
+        // (test hook: SMEM_BUILD_SB_MAX shrinks the super-buckets)
+        uint64_t sb_max = SB_MAX;
+        if (const char* v = getenv("SMEM_BUILD_SB_MAX")) sb_max = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
+        uint64_t cap = std::max(std::min(sb_max, n), big);
         if (cap >= (1ull << 31)) return SMEM_E_CAPACITY;
 
         Buf bK0, bK1, bV0, bV1, bG, bFlag, bTmp, bU0, bU1;
@@ -552,15 +582,28 @@ static int build_gpu_large(int device, const uint8_t* fwd, uint64_t n_fwd, int s
         uint64_t u_cap = std::max<uint64_t>(cap, 1 << 20), n_u = 0;
         GB_TRY(hipMalloc(&bU0.p, u_cap * 8));
 
-        // A. super-buckets, in bin (= SA) order
+        // A. every suffix to its bin's SA range (counting sort), then the
+        // super-buckets, in bin (= SA) order
+        {
+            uint64_t* start = (uint64_t*)malloc(n_bins * 8);
+            if (!start) return SMEM_E_NOMEM;
+            uint64_t acc = 0;
+            for (uint64_t b = 0; b < n_bins; ++b) start[b] = acc, acc += hist[b];
+            const hipError_t e = hipMemcpyAsync(bHist.p, start, n_bins * 8, hipMemcpyHostToDevice, st);
+            const hipError_t e2 = hipStreamSynchronize(st);
+            free(start);
+            GB_TRY(e);
+            GB_TRY(e2);
+            bin_scatter<<<(unsigned)((n + SC - 1) / SC), 256, 0, st>>>(T, n, (unsigned long long*)bHist.p, sa);
+            bin_scatter_tail<<<1, 64, 0, st>>>(T, n, (unsigned long long*)bHist.p, sa);
+            GB_TRY(hipGetLastError());
+        }
         uint64_t base = 0;
         for (uint64_t blo = 0; blo < n_bins;) {
             uint64_t bhi = blo, m = 0;
             while (bhi < n_bins && (m + hist[bhi] <= cap)) m += hist[bhi++];
             if (m == 0) { blo = bhi; continue; }
-            GB_TRY(hipMemsetAsync(d_cnt, 0, 8, st));
-            bin_gather<<<blocks((n + 15) / 16), 256, 0, st>>>(T, n, blo, bhi, (uint64_t*)bK0.p, (uint64_t*)bV0.p,
-                                                              d_cnt);
+            sb_load<<<blocks(m), 256, 0, st>>>(T, n, sa, base, m, (uint64_t*)bK0.p, (uint64_t*)bV0.p);
             hipcub::DoubleBuffer<uint64_t> k((uint64_t*)bK0.p, (uint64_t*)bK1.p), v((uint64_t*)bV0.p, (uint64_t*)bV1.p);
             size_t tb = tmp_bytes;
             GB_TRY(hipcub::DeviceRadixSort::SortPairs(bTmp.p, tb, k, v, (int)m, 0, 3 * K0, st));

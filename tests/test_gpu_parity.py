@@ -235,6 +235,21 @@ def test_gpu_large_builder_matches_cpu(gpu_device, kind, n_bp):
     assert np.array_equal(a_idx.words, c.words)
 
 
+@pytest.mark.parametrize("sb_max", ["1000", "65536"])
+def test_gpu_large_builder_many_superbuckets(gpu_device, monkeypatch, sb_max):
+    """The bucketed builder with its super-buckets shrunk (the human-size
+    genome has ~25 of 2^28 suffixes): every bin's range is sorted on its own
+    and the ranks / unresolved list are carried across them."""
+    import smemgpu
+    from smemgpu import synth
+    monkeypatch.setenv("SMEM_BUILD_SB_MAX", sb_max)
+    g = synth.make_genome(1_500_000, seed=61, n_chrom=1).codes
+    a_idx, a_sa = smemgpu.Index.build_sa(g, sa_intv=32)
+    b_idx, b_sa = smemgpu.Index.build_sa(g, sa_intv=32, gpu=True, device=gpu_device, large=True)
+    assert a_idx.primary == b_idx.primary and np.array_equal(a_idx.words, b_idx.words)
+    assert np.array_equal(a_sa.samples, b_sa.samples)
+
+
 def test_gpu_index_builder_golden(gpu_device):
     import smemgpu
     from tests import golden_data
