@@ -106,6 +106,7 @@ struct smem_gpu {
     int variant = 2;  // see smem_gpu_set_kernel_variant
     uint32_t* d_bwt = nullptr;      // reference layout (variants 3, 4)
     uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
+    uint32_t* d_occ192 = nullptr;   // Occ192 layout (variant 10)
     uint64_t* d_sa = nullptr;       // sampled SA (smem_gpu_load_sa), n_sa + 1 words
     uint64_t n_sa = 0;
     uint32_t sa_shift = 0;
@@ -246,6 +247,8 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
     if (e != hipSuccess) {
         (void)hipFree(g->d_bwt);
         if (g->d_occ64) (void)hipFree(g->d_occ64);
+    if (g->d_occ192) (void)hipFree(g->d_occ192);
+        if (g->d_occ192) (void)hipFree(g->d_occ192);
         delete g;
         return fail(SMEM_E_DEVICE, "smem_gpu_init: Occ64 layout", e);
     }
@@ -260,7 +263,23 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 8) || variant == 9)) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 10))) return SMEM_E_ARG;
+    if (variant == 10 && !g->d_occ192) {
+        // the Occ192 layout (variant 10 only), built from Occ64 on first use
+        std::lock_guard<std::mutex> lk(g->mu);
+        HIP_TRY(hipSetDevice(g->device));
+        const uint64_t n_blocks = 2 * ((g->bwt_size + 15) / 16), n_lines = (n_blocks + 2) / 3;
+        uint32_t* p = nullptr;
+        HIP_TRY(hipMalloc(&p, (n_lines * 16 + 16) * sizeof(uint32_t)));
+        hipError_t e = hipMemset(p + n_lines * 16, 0, 16 * sizeof(uint32_t));
+        if (e == hipSuccess) e = smem_launch_occ192(g->d_occ64, n_blocks, p, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            return fail(SMEM_E_DEVICE, "smem_gpu_set_kernel_variant: Occ192 layout", e);
+        }
+        g->d_occ192 = p;
+    }
     g->variant = variant == 0 ? 2 : variant;
     return SMEM_OK;
 }
@@ -302,6 +321,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     g->per_thread.clear();
     if (g->d_bwt) (void)hipFree(g->d_bwt);
     if (g->d_occ64) (void)hipFree(g->d_occ64);
+    if (g->d_occ192) (void)hipFree(g->d_occ192);
     if (g->d_sa) (void)hipFree(g->d_sa);
     delete g;
 }
@@ -416,6 +436,7 @@ static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& 
     P.s_calls = b->d_sz_calls.p;
     P.bwt = b->g->d_bwt;
     P.occ64 = b->g->d_occ64;
+    P.occ192 = b->g->d_occ192;
     P.primary = b->g->primary;
     std::memcpy(P.L2, b->g->L2, sizeof(P.L2));
     P.codes = b->d_codes.p;

@@ -23,6 +23,7 @@ struct CallRec {
 struct SeedParams {
     const uint32_t* bwt;       // interleaved BWT + Occ, resident in HBM (reference layout)
     const uint32_t* occ64;     // the same index as 32-B buckets per 64 symbols (smem_launch_occ64)
+    const uint32_t* occ192;    // the same index as 64-B lines of 192 symbols (smem_launch_occ192; variant 10)
     uint64_t primary;
     uint64_t L2[5];
     const uint8_t* codes;      // reads, concatenated nt4 codes (+32 B pad)
@@ -94,6 +95,7 @@ extern "C" {
 hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st);
 // reference interleaved words (n_ref_buckets x 64 B) -> 2 * n_ref_buckets 32-B buckets
 hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32_t* out, hipStream_t st);
+hipError_t smem_launch_occ192(const uint32_t* occ64, uint64_t n_blocks, uint32_t* out, hipStream_t st);
 hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int write, hipStream_t st);
 hipError_t smem_launch_fill_i32(int32_t* p, int32_t v, int n, hipStream_t st);
 hipError_t smem_launch_ovf_slot(const int32_t* items, int n_ovf, int32_t* ovf_slot, hipStream_t st);

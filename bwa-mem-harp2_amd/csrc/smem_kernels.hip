@@ -281,15 +281,51 @@ __device__ __forceinline__ void count_cgt4(const uint4& v, uint32_t pos, uint32_
     G = sHi - sT;
 }
 
-// bwt_extend for the child c only (as extend_counts) on Occ64 buckets
+// ---- Occ192: 64-B lines of 192 BWT symbols (a third fewer index bytes than
+// Occ64, and more k / l pairs in one line).  Chunk 0: Occ(C), Occ(G), Occ(T)
+// before the line's second 64-symbol block (34 bits: low 32 in words 0-2,
+// bits 32-33 in word 3 bits 0-5) and the C / G / T counts of that block
+// (7 bits each, word 3 bits 6-26).  Chunks 1-3: the line's three blocks of
+// 64 symbols, as Occ64's symbol words.  A rank in block r of a line reads
+// chunk 0 and chunk 1 + r (still two 16-B loads): r = 0 subtracts the
+// block's symbols after the position, r = 1 adds those up to it, r = 2 adds
+// the middle block's counts as well.  Slot tags stay the 64-symbol block.
+__device__ __forceinline__ void rank192(const Bucket32& v, uint64_t kk, uint64_t& tC, uint64_t& tG, uint64_t& tT) {
+    const uint32_t b = (uint32_t)(kk >> 6), r = b - 3u * (b / 3u), p = (uint32_t)(kk & 63);
+    uint32_t C, G, T;
+    count_cgt4(v.sym, p, C, G, T);
+    const uint64_t c0 = occ_cgt(v.cnt, 0), g0 = occ_cgt(v.cnt, 1), t0 = occ_cgt(v.cnt, 2);
+    if (r == 0) {
+        uint32_t C6, G6, T6;
+        count_cgt4(v.sym, 63, C6, G6, T6);
+        tC = c0 - (C6 - C);
+        tG = g0 - (G6 - G);
+        tT = t0 - (T6 - T);
+    } else {
+        const uint32_t w = r == 2 ? v.cnt.w : 0u;
+        tC = c0 + ((w >> 6) & 127u) + C;
+        tG = g0 + ((w >> 13) & 127u) + G;
+        tT = t0 + ((w >> 20) & 127u) + T;
+    }
+}
+
+// bwt_extend for the child c only (as extend_counts) on Occ64 buckets (or
+// Occ192 lines)
+template <bool L192 = false>
 __device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a, uint64_t b, uint64_t s, int c,
                                                 uint64_t kk, uint64_t ll, const Bucket32& vk, const Bucket32& vl,
                                                 uint64_t& na, uint64_t& nb, uint64_t& ns) {
-    uint32_t Ck, Gk, Tk, Cl, Gl, Tl;
-    count_cgt4(vk.sym, (uint32_t)(kk & 63), Ck, Gk, Tk);
-    count_cgt4(vl.sym, (uint32_t)(ll & 63), Cl, Gl, Tl);
-    const uint64_t tk1 = occ_cgt(vk.cnt, 0) + Ck, tk2 = occ_cgt(vk.cnt, 1) + Gk, tk3 = occ_cgt(vk.cnt, 2) + Tk;
-    const uint64_t tl1 = occ_cgt(vl.cnt, 0) + Cl, tl2 = occ_cgt(vl.cnt, 1) + Gl, tl3 = occ_cgt(vl.cnt, 2) + Tl;
+    uint64_t tk1, tk2, tk3, tl1, tl2, tl3;
+    if constexpr (L192) {
+        rank192(vk, kk, tk1, tk2, tk3);
+        rank192(vl, ll, tl1, tl2, tl3);
+    } else {
+        uint32_t Ck, Gk, Tk, Cl, Gl, Tl;
+        count_cgt4(vk.sym, (uint32_t)(kk & 63), Ck, Gk, Tk);
+        count_cgt4(vl.sym, (uint32_t)(ll & 63), Cl, Gl, Tl);
+        tk1 = occ_cgt(vk.cnt, 0) + Ck, tk2 = occ_cgt(vk.cnt, 1) + Gk, tk3 = occ_cgt(vk.cnt, 2) + Tk;
+        tl1 = occ_cgt(vl.cnt, 0) + Cl, tl2 = occ_cgt(vl.cnt, 1) + Gl, tl3 = occ_cgt(vl.cnt, 2) + Tl;
+    }
     const uint64_t tk0 = kk + 1 - tk1 - tk2 - tk3, tl0 = ll + 1 - tl1 - tl2 - tl3;
     const uint64_t d0 = tl0 - tk0, d1 = tl1 - tk1, d2 = tl2 - tk2, d3 = tl3 - tk3;
     const uint64_t L2c = sel4(c, P.L2[0], P.L2[1], P.L2[2], P.L2[3]);
@@ -306,7 +342,21 @@ __device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a,
 // bucket again (nested intervals of one backward step: 30 % of the buckets
 // on the bench workload), and those are not fetched again.  Every lane DMAs
 // its own buckets, one 16-B chunk per instruction (at most 4 instructions).
-template <class WL>
+// the two 16-B chunks of 64-symbol block b: Occ64 bucket b, or Occ192 line b / 3
+template <bool L192>
+__device__ __forceinline__ void block_chunks(const uint32_t* __restrict__ occ, uint32_t b, const uint32_t*& c0,
+                                             const uint32_t*& c1) {
+    if constexpr (L192) {
+        const uint32_t line = b / 3u;
+        c0 = boff(occ, line, 0);
+        c1 = boff(occ, line, 4u * (1u + b - 3u * line));
+    } else {
+        c0 = boff(occ, b >> 1, (b & 1) * 8);
+        c1 = boff(occ, b >> 1, (b & 1) * 8 + 4);
+    }
+}
+
+template <class WL, bool L192 = false>
 __device__ __forceinline__ void fetch_occ64_issue(const uint32_t* __restrict__ occ, WL* W, uint64_t kk, uint64_t ll,
                                                   uint32_t& t0, uint32_t& t1, int& ks, int& ls) {
     const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
@@ -321,13 +371,17 @@ __device__ __forceinline__ void fetch_occ64_issue(const uint32_t* __restrict__ o
     const bool f1 = (kmiss && ks == 1) || (lmiss && ls == 1);
     const uint32_t b0 = (kmiss && ks == 0) ? bk : bl, b1 = (kmiss && ks == 1) ? bk : bl;
     if (f0) {
-        __builtin_amdgcn_global_load_lds(boff(occ, b0 >> 1, (b0 & 1) * 8), LDS_PTR(&W->img[0][0]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(boff(occ, b0 >> 1, (b0 & 1) * 8 + 4), LDS_PTR(&W->img[1][0]), 16, 0, 0);
+        const uint32_t *a0, *a1;
+        block_chunks<L192>(occ, b0, a0, a1);
+        __builtin_amdgcn_global_load_lds(a0, LDS_PTR(&W->img[0][0]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(a1, LDS_PTR(&W->img[1][0]), 16, 0, 0);
         t0 = b0;
     }
     if (f1) {
-        __builtin_amdgcn_global_load_lds(boff(occ, b1 >> 1, (b1 & 1) * 8), LDS_PTR(&W->img[2][0]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(boff(occ, b1 >> 1, (b1 & 1) * 8 + 4), LDS_PTR(&W->img[3][0]), 16, 0, 0);
+        const uint32_t *a0, *a1;
+        block_chunks<L192>(occ, b1, a0, a1);
+        __builtin_amdgcn_global_load_lds(a0, LDS_PTR(&W->img[2][0]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(a1, LDS_PTR(&W->img[3][0]), 16, 0, 0);
         t1 = b1;
     }
 }
@@ -368,7 +422,7 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 // STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
-template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false>
+template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -641,7 +695,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         if constexpr (FETCH == FETCH_OCC64 && EARLY) {
                             // issue its bucket fetch now: it overlaps the rest of the pass
                             const uint64_t k = ik0 - 1, l = k + ik2;
-                            fetch_occ64_issue(P.occ64, W, k - (k >= P.primary), l - (l >= P.primary), tag0, tag1,
+                            fetch_occ64_issue<WaveLds, L192>(L192 ? P.occ192 : P.occ64, W, k - (k >= P.primary), l - (l >= P.primary), tag0, tag1,
                                               fks, fls);
                             early = true;
                         }
@@ -853,7 +907,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         Bucket32 wk, wl;
         if constexpr (FETCH == FETCH_OCC64) {
             // lanes whose fetch was not issued early in BWD_RES issue it now
-            if (want && !early) fetch_occ64_issue(P.occ64, W, kk, ll, tag0, tag1, fks, fls);
+            if (want && !early)
+                fetch_occ64_issue<WaveLds, L192>(L192 ? P.occ192 : P.occ64, W, kk, ll, tag0, tag1, fks, fls);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             fetch_occ64_read(W, fks, fls, wk, wl);
         } else {
@@ -874,7 +929,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         }
         if (want) {
             if constexpr (FETCH == FETCH_OCC64)
-                extend_counts64(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
+                extend_counts64<L192>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
             else
                 extend_counts(P, ra, rb, rs, rc, kk, ll, vk, vl, na, nb, ns);
         }
@@ -992,6 +1047,7 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 8: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 10: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
@@ -1055,6 +1111,47 @@ __global__ __launch_bounds__(256) void occ64_kernel(const uint32_t* __restrict__
     o[1] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
 }
 }  // namespace smem
+
+namespace smem {
+// Occ64 -> Occ192 (see rank192); one thread per 64-B line of 192 symbols
+__global__ __launch_bounds__(256) void occ192_kernel(const uint32_t* __restrict__ occ64, uint64_t n_blocks,
+                                                      uint64_t n_lines, uint32_t* __restrict__ out) {
+    const uint64_t L = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= n_lines) return;
+    const uint4* o = reinterpret_cast<const uint4*>(occ64);  // block b: o[2b] counts, o[2b + 1] symbols
+    const uint64_t b0 = 3 * L;
+    uint4 sym[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sym[i] = b0 + i < n_blocks ? o[2 * (b0 + i) + 1] : make_uint4(0, 0, 0, 0);
+    uint64_t c, g, t;
+    if (b0 + 1 < n_blocks) {
+        const uint4 cnt = o[2 * (b0 + 1)];
+        c = occ_cgt(cnt, 0), g = occ_cgt(cnt, 1), t = occ_cgt(cnt, 2);
+    } else {  // the line's first block is the last one: counts through its end
+        const uint4 cnt = o[2 * b0];
+        uint32_t C, G, T;
+        count_cgt4(sym[0], 63, C, G, T);
+        c = occ_cgt(cnt, 0) + C, g = occ_cgt(cnt, 1) + G, t = occ_cgt(cnt, 2) + T;
+    }
+    uint32_t dC, dG, dT;
+    count_cgt4(sym[1], 63, dC, dG, dT);
+    uint4* w = reinterpret_cast<uint4*>(out) + 4 * L;
+    w[0] = make_uint4((uint32_t)c, (uint32_t)g, (uint32_t)t,
+                      (uint32_t)(c >> 32) | (uint32_t)(g >> 32) << 2 | (uint32_t)(t >> 32) << 4 | dC << 6 | dG << 13 |
+                          dT << 20);
+    w[1] = sym[0];
+    w[2] = sym[1];
+    w[3] = sym[2];
+}
+}  // namespace smem
+
+extern "C" hipError_t smem_launch_occ192(const uint32_t* occ64, uint64_t n_blocks, uint32_t* out, hipStream_t st) {
+    const uint64_t n_lines = (n_blocks + 2) / 3;
+    if (n_lines == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::occ192_kernel, dim3((unsigned)((n_lines + 255) / 256)), dim3(256), 0, st, occ64, n_blocks,
+                       n_lines, out);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32_t* out, hipStream_t st) {
     const uint64_t n = 2 * n_ref_buckets;

@@ -260,7 +260,8 @@ int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
  * cooperative fetch, lists in global memory; 4 reference layout, per-lane
  * fetch; 5 as 2 with 12 list entries in LDS (2 blocks per CU); 6 as 2 with
  * lists in global memory; 9 the default with per-wave cycle stamps
- * (smem_batch_debug) */
+ * (smem_batch_debug); 10 the default on the Occ192 layout (64-B lines of
+ * 192 symbols, built on first use: exact, 7 % slower at human size) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
 /* variant 9 (stamped diagnostic build): copy the per-wave cycle split
  * {advance, fetch, compute, iterations, active lanes, t0, t1, 0} of the last
