@@ -195,11 +195,18 @@ class Dist:
         n_dev = torch.cuda.device_count()
         self.gpu = self.local % n_dev if n_dev > 0 else 0
         if self.world > 1:
-            backend = backend or os.environ.get("SMEM_DIST_BACKEND") or ("nccl" if n_dev > 0 else "gloo")
+            # RCCL when every rank has a GPU of its own; gloo on CPU for a
+            # rehearsal with more ranks than GPUs (RCCL refuses two ranks on
+            # one device) -- only a barrier and two scalars go through it
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
+            default = "nccl" if n_dev >= local_world and n_dev > 0 else "gloo"
+            backend = backend or os.environ.get("SMEM_DIST_BACKEND") or default
             if backend == "nccl":
                 torch.cuda.set_device(self.gpu)
                 self.device = "cuda"
-            dist.init_process_group(backend)
+                dist.init_process_group(backend, device_id=torch.device("cuda", self.gpu))
+            else:
+                dist.init_process_group(backend)
 
     def barrier(self):
         if self.world > 1:
