@@ -1401,6 +1401,10 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 uint32_t n_cand = 0;
                 const bool clean =
                     insert_read_clusters(P, S, E, reinterpret_cast<uint64_t*>(lds_raw), lane, n, n_cand);
+                if (dbg && lane == 0) {
+                    dbg[11] = __builtin_readcyclecounter();
+                    dbg[12] = n_cand;
+                }
                 if (!clean) {
                     // an equal chain key: rebuild the tree in seed order
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

@@ -26,17 +26,22 @@ constexpr int NEG = -(1 << 28);
 
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 
-__device__ __forceinline__ int wave_max(int v) {
-    for (int off = 32; off > 0; off >>= 1) v = imax(v, __shfl_xor(v, off));
+// Cross-lane steps by DPP (no LDS round trip): an inclusive prefix max over
+// the 64 lanes (row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15
+// and 31 across rows; lanes a step does not reach keep NEG), and the
+// whole-wave shift by one lane (wave_shr 1, lane 0 takes `first`).
+__device__ __forceinline__ int scan_max(int v) {
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
 
-__device__ __forceinline__ int scan_max(int v, int lane) {
-    for (int off = 1; off < 64; off <<= 1) {
-        const int t = __shfl_up(v, off, 64);
-        if (lane >= off) v = imax(v, t);
-    }
-    return v;
+__device__ __forceinline__ int wave_shr1(int v, int first) {
+    return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
 
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -57,6 +62,7 @@ __global__ __launch_bounds__(256) void ksw_extend_kernel(KswParams K) {
         const uint8_t* tg = K.t + T.t_off;
         const int h0 = T.h0 > 0 ? T.h0 : 0;
         const int eh1 = h0 > oe_ins ? h0 - oe_ins : 0;
+
         // columns: scores, first row (software/ksw.c:389-396)
         uint32_t sc[KC];
         int sc4[KC], hp[KC], ee[KC];
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(256) void ksw_extend_kernel(KswParams K) {
             if (end > qlen) end = qlen;
             // H of the row: D, then F by a prefix max across the columns
             int H[KC];
-            int carry = NEG, best = -1, bestj = -1;
+            int carry = NEG, key = NEG;
 #pragma unroll
             for (int c = 0; c < KC; ++c) {
                 const int j = 64 * c + lane;
@@ -104,24 +110,23 @@ __global__ __launch_bounds__(256) void ksw_extend_kernel(KswParams K) {
                 const bool valid = j >= beg && j < end;
                 const int s = tc < 4 ? (int)(int8_t)(sc[c] >> (8 * tc)) : sc4[c];
                 const int d = imax(hp[c] + s, ee[c]);
-                const int incl = scan_max(valid ? d + j * K.e_ins : NEG, lane);
-                int excl = __shfl_up(incl, 1, 64);
-                if (lane == 0) excl = NEG;
-                excl = imax(excl, carry);
+                const int incl = scan_max(valid ? d + j * K.e_ins : NEG);
+                const int excl = imax(wave_shr1(incl, NEG), carry);
                 carry = imax(carry, rl(incl, 63));
                 const int f = imax(0, excl - oe_ins - (j - 1) * K.e_ins);
                 const int h = imax(d, f);
                 if (valid) {
                     H[c] = h;
-                    if (h >= best) best = h, bestj = j;  // ascending j per lane
+                    key = imax(key, h << 8 | j);  // ascending j: ties keep the last column
                 }
             }
             // row maximum m (0 when the band is empty) and its last column
             const bool nonempty = beg < end;
             int m = 0, mj = -1;
             if (nonempty) {
-                m = wave_max(best);
-                mj = wave_max(best == m ? bestj : -1);
+                const int kmax = rl(scan_max(key), 63);
+                m = kmax >> 8;
+                mj = kmax & 255;
             }
             // the column array for the next row: E updated, H shifted one
             // column right (column beg takes the row's first-column value)
@@ -129,8 +134,11 @@ __global__ __launch_bounds__(256) void ksw_extend_kernel(KswParams K) {
 #pragma unroll
             for (int c = 0; c < KC; ++c) {
                 const int j = 64 * c + lane;
-                int up = __shfl_up(H[c], 1, 64);
-                if (lane == 0) up = prev_last;
+                if (64 * c >= end || 64 * c + 63 < beg) {  // outside the band (uniform)
+                    prev_last = 0;
+                    continue;
+                }
+                const int up = wave_shr1(H[c], prev_last);
                 prev_last = rl(H[c], 63);
                 if (j >= beg && j < end) {
                     ee[c] = imax(ee[c] - K.e_del, imax(H[c] - oe_del, 0));
@@ -169,13 +177,11 @@ __global__ __launch_bounds__(256) void ksw_extend_kernel(KswParams K) {
 #pragma unroll
             for (int c = 0; c < KC; ++c) {
                 const int j = 64 * c + lane;
-                if (hp[c] == 0) {
-                    if (j >= beg && j <= mj) zlo = imax(zlo, j);
-                    if (j >= mj + 2 && j <= end) zhi = j < zhi ? j : zhi;
-                }
+                const uint64_t lo = __ballot(hp[c] == 0 && j >= beg && j <= mj);
+                const uint64_t hi = __ballot(hp[c] == 0 && j >= mj + 2 && j <= end);
+                if (lo) zlo = 64 * c + 63 - __builtin_clzll(lo);
+                if (hi && zhi == 0x7fffffff) zhi = 64 * c + __builtin_ctzll(hi);
             }
-            zlo = wave_max(zlo);
-            zhi = -wave_max(-zhi);
             beg = zlo >= 0 ? zlo + 1 : beg;
             end = zhi != 0x7fffffff ? zhi : end + 1;
         }
