@@ -1,0 +1,334 @@
+// Chains -> alignment regions on gfx950: the loop of
+// mem_align1_core over a read's chains (software/bwamem.c:1452-1460), each
+// chain through mem_chain2aln_short (software/bwamem.c:805-852, ksw_align2)
+// and, when that declines, mem_chain2aln (software/bwamem.c:1040-1188, two
+// ksw_extend2 calls per extended seed), over the chains smem_batch_chain left
+// in HBM and the .pac resident beside the index.
+//
+// One wave per read: a read's regions depend on each other (every seed is
+// first tested for containment in the regions made before it, from this and
+// earlier chains), so the wave walks its chains and seeds in the reference's
+// order and spreads the work inside each step over its 64 lanes:
+//   * the per-seed scans (reference span, containment in earlier regions,
+//     overlap with longer seeds, seed coverage) run one region or seed per
+//     lane and end in a ballot or a reduction;
+//   * the seed order (ks_introsort_64 of len << 32 | index, distinct keys) is
+//     each key's rank among the chain's keys, by lanes;
+//   * every ksw_extend2 / ksw_align2 runs on the whole wave (ksw_device.h),
+//     the reference fetched from the 2-bit .pac per row (bns_get_seq).
+// Reads up to 256 bp go to aln_kernel<4> (query columns in 4 registers per
+// lane), longer ones (up to 1024 bp) to aln_kernel<16>.
+#include <algorithm>
+
+#include "aln_kernels.h"
+#include "ksw_device.h"
+
+namespace smem {
+namespace {
+
+__device__ __forceinline__ int pac_at(const uint8_t* pac, int64_t l) {
+    return pac[l >> 2] >> ((~l & 3) << 1) & 3;  // _get_pac (software/bntseq.h)
+}
+
+// symbol p of the forward-reverse text (bns_get_seq, software/bntseq.c:355-376,
+// over a span that does not bridge the strands)
+__device__ __forceinline__ int ref_at(const AlnParams& P, int64_t p) {
+    return p < P.l_pac ? pac_at(P.pac, p) : 3 - pac_at(P.pac, (P.l_pac << 1) - 1 - p);
+}
+
+// cal_max_gap (software/bwamem.c:854-861)
+__device__ __forceinline__ int max_gap(const AlnParams& P, int qlen) {
+    const int l_del = (int)((double)(qlen * P.a - P.o_del) / P.e_del + 1.);
+    const int l_ins = (int)((double)(qlen * P.a - P.o_ins) / P.e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < P.w << 1 ? l : P.w << 1;
+}
+
+__device__ __forceinline__ int64_t wmin64(int64_t v) {
+    for (int o = 32; o; o >>= 1) {
+        const int64_t t = __shfl_xor(v, o);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int64_t wmax64(int64_t v) {
+    for (int o = 32; o; o >>= 1) {
+        const int64_t t = __shfl_xor(v, o);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int wsum(int v) {
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32;
+}
+
+// mem_chain2aln_short (software/bwamem.c:805-852): 0 when it wrote region
+// *out, 1 when it declines (then mem_chain2aln runs)
+__device__ int chain_short(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n, AlnReg* out,
+                           int lane) {
+    int64_t qb = L, qe = 0, rb = P.l_pac << 1, re = 0;
+    int cov = 0;
+    for (int i = lane; i < n; i += 64) {
+        const SeedRec s = S[i];
+        qb = s.qbeg < qb ? s.qbeg : qb;
+        qe = s.qbeg + s.len > qe ? s.qbeg + s.len : qe;
+        rb = s.rbeg < rb ? s.rbeg : rb;
+        re = s.rbeg + s.len > re ? s.rbeg + s.len : re;
+        cov += s.len;
+    }
+    cov = wsum(cov);
+    qb = wmin64(qb) - 50, qe = wmax64(qe) + 50;  // MEM_SHORT_EXT
+    rb = wmin64(rb) - 50, re = wmax64(re) + 50;
+    if (qb <= 10 || qe >= L - 10) return 1;
+    rb = rb > 0 ? rb : 0;
+    re = re < P.l_pac << 1 ? re : P.l_pac << 1;
+    if (rb < P.l_pac && P.l_pac < re) {
+        if (S[0].rbeg < P.l_pac) re = P.l_pac;
+        else rb = P.l_pac;
+    }
+    if ((re - rb) - (qe - qb) > 50 || (qe - qb) - (re - rb) > 50) return 1;
+    if (qe - qb >= P.w * 4 || re - rb >= P.w * 4) return 1;
+    if (qe - qb >= 200 || re - rb >= 200) return 1;  // MEM_SHORT_LEN
+    const int ql = (int)(qe - qb), tl = (int)(re - rb);
+    const int xtra = kswd::SW_XSUBO | kswd::SW_XSTART | (ql * P.a < 250 ? kswd::SW_XBYTE : 0) | (P.min_seed_len * P.a);
+    const uint8_t* qw = query + qb;
+    const int64_t r0 = rb;
+    const kswd::SwAlign x = kswd::sw_align_wave(
+        ql, [&](int q) { return (int)qw[q]; }, tl, [&](int i) { return ref_at(P, r0 + i); }, P.mat, P.o_del, P.e_del,
+        P.o_ins, P.e_ins, xtra, P.sw_shift, P.top);
+    if (x.tb < 25 || x.te > tl - 25) return 1;
+    if (lane == 0) {
+        AlnReg a;
+        a.rb = rb + x.tb, a.re = rb + x.te + 1;
+        a.qb = (int)qb + x.qb, a.qe = (int)qb + x.qe + 1;
+        a.score = x.score, a.truesc = 0, a.sub = 0, a.csub = x.score2, a.sub_n = 0, a.w = 0, a.seedcov = cov;
+        a.secondary = 0, a.hash = 0;
+        *out = a;
+    }
+    return 0;
+}
+
+// mem_chain2aln (software/bwamem.c:1040-1188); regs[0 .. nreg) are the read's
+// regions so far, srt the chain's n-word scratch
+template <int KC>
+__device__ void chain_full(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n, uint64_t* srt,
+                           AlnReg* regs, int& nreg, int lane) {
+    // the span of reference any extension may reach (software/bwamem.c:1050-1065)
+    int64_t r0 = P.l_pac << 1, r1 = 0;
+    for (int i = lane; i < n; i += 64) {
+        const SeedRec t = S[i];
+        const int64_t b = t.rbeg - (t.qbeg + max_gap(P, t.qbeg));
+        const int64_t e = t.rbeg + t.len + ((L - t.qbeg - t.len) + max_gap(P, L - t.qbeg - t.len));
+        r0 = b < r0 ? b : r0;
+        r1 = e > r1 ? e : r1;
+    }
+    r0 = wmin64(r0), r1 = wmax64(r1);
+    r0 = r0 > 0 ? r0 : 0;
+    r1 = r1 < P.l_pac << 1 ? r1 : P.l_pac << 1;
+    if (r0 < P.l_pac && P.l_pac < r1) {
+        if (S[0].rbeg < P.l_pac) r1 = P.l_pac;
+        else r0 = P.l_pac;
+    }
+    // seeds ascending by (len, index): each key lands at its rank
+    for (int ib = 0; ib < n; ib += 64) {
+        const int i = ib + lane;
+        const uint64_t ki = i < n ? ((uint64_t)(uint32_t)S[i].len << 32 | (uint32_t)i) : ~0ull;
+        int rank = 0;
+        for (int jb = 0; jb < n; jb += 64) {
+            const int j = jb + lane;
+            const uint64_t kj = j < n ? ((uint64_t)(uint32_t)S[j].len << 32 | (uint32_t)j) : ~0ull;
+            const int m = n - jb < 64 ? n - jb : 64;
+            for (int t = 0; t < m; ++t) rank += rl64(kj, t) < ki;
+        }
+        if (i < n) srt[rank] = ki;
+    }
+    __threadfence_block();
+    for (int k = n - 1; k >= 0; --k) {
+        const SeedRec s = S[(uint32_t)srt[k]];
+        // is the seed (almost) contained in a region made before? (software/bwamem.c:1079-1094)
+        bool hit = false;
+        for (int ib = 0; ib < nreg && !hit; ib += 64) {
+            const int i = ib + lane;
+            bool ok = false;
+            if (i < nreg) {
+                const AlnReg p = regs[i];
+                if (!(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe)) {
+                    int qd = s.qbeg - p.qb;
+                    int64_t rd = s.rbeg - p.rb;
+                    int g = max_gap(P, (int)(qd < rd ? qd : rd));
+                    int w = g < P.w ? g : P.w;
+                    if (qd - rd < w && rd - qd < w) ok = true;
+                    qd = p.qe - (s.qbeg + s.len);
+                    rd = p.re - (s.rbeg + s.len);
+                    g = max_gap(P, (int)(qd < rd ? qd : rd));
+                    w = g < P.w ? g : P.w;
+                    if (qd - rd < w && rd - qd < w) ok = true;
+                }
+            }
+            hit = __ballot(ok) != 0;
+        }
+        if (hit) {  // extend only if a long overlapping seed disagrees (software/bwamem.c:1098-1109)
+            bool brk = false;
+            for (int ib = k + 1; ib < n && !brk; ib += 64) {
+                const int i = ib + lane;
+                bool ok = false;
+                if (i < n) {
+                    const uint64_t v = srt[i];
+                    if (v != 0) {
+                        const SeedRec t = S[(uint32_t)v];
+                        if (!(t.len < s.len * .95)) {
+                            if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
+                                (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg)
+                                ok = true;
+                            if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
+                                (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg)
+                                ok = true;
+                        }
+                    }
+                }
+                brk = __ballot(ok) != 0;
+            }
+            if (!brk) {
+                if (lane == 0) srt[k] = 0;  // not extended
+                __threadfence_block();
+                continue;
+            }
+        }
+        int aw0 = P.w, aw1 = P.w, score = -1, truesc = -1, aqb, aqe;
+        int64_t arb, are;
+        if (s.qbeg) {  // left: the reversed query against the reversed reference
+            const int64_t tmp = s.rbeg - r0;
+            KswResult x{};
+            for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY
+                const int prev = score;
+                aw0 = P.w << t;
+                x = kswd::extend_wave<KC>(
+                    kswd::ExtIn{s.qbeg, (int)tmp, aw0, P.pen_clip5, P.zdrop, s.len * P.a},
+                    [&](int j) { return (int)query[s.qbeg - 1 - j]; }, [&](int i) { return ref_at(P, s.rbeg - 1 - i); },
+                    P.mat, P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
+                score = x.score;
+                if (score == prev || x.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+            }
+            if (x.gscore <= 0 || x.gscore <= score - P.pen_clip5) {  // local extension
+                aqb = s.qbeg - x.qle, arb = s.rbeg - x.tle;
+                truesc = score;
+            } else {  // to the query start
+                aqb = 0, arb = s.rbeg - x.gtle;
+                truesc = x.gscore;
+            }
+        } else {
+            score = truesc = s.len * P.a;
+            aqb = 0, arb = s.rbeg;
+        }
+        if (s.qbeg + s.len != L) {  // right
+            const int qe = s.qbeg + s.len, sc0 = score;
+            const int64_t rs = s.rbeg + s.len;
+            KswResult x{};
+            for (int t = 0; t < 2; ++t) {
+                const int prev = score;
+                aw1 = P.w << t;
+                x = kswd::extend_wave<KC>(kswd::ExtIn{L - qe, (int)(r1 - rs), aw1, P.pen_clip3, P.zdrop, sc0},
+                                          [&](int j) { return (int)query[qe + j]; },
+                                          [&](int i) { return ref_at(P, rs + i); }, P.mat, P.o_del, P.e_del, P.o_ins,
+                                          P.e_ins, P.top);
+                score = x.score;
+                if (score == prev || x.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+            }
+            if (x.gscore <= 0 || x.gscore <= score - P.pen_clip3) {
+                aqe = qe + x.qle, are = rs + x.tle;
+                truesc += score - sc0;
+            } else {
+                aqe = L, are = rs + x.gtle;
+                truesc += x.gscore - sc0;
+            }
+        } else {
+            aqe = L, are = s.rbeg + s.len;
+        }
+        int cov = 0;  // seeds inside the region (software/bwamem.c:1180-1184)
+        for (int i = lane; i < n; i += 64) {
+            const SeedRec t = S[i];
+            if (t.qbeg >= aqb && t.qbeg + t.len <= aqe && t.rbeg >= arb && t.rbeg + t.len <= are) cov += t.len;
+        }
+        cov = wsum(cov);
+        if (lane == 0) {
+            AlnReg a;
+            a.rb = arb, a.re = are, a.qb = aqb, a.qe = aqe;
+            a.score = score, a.truesc = truesc, a.sub = 0, a.csub = 0, a.sub_n = 0;
+            a.w = aw0 > aw1 ? aw0 : aw1, a.seedcov = cov, a.secondary = 0, a.hash = 0;
+            regs[nreg] = a;
+        }
+        ++nreg;
+        __threadfence_block();
+    }
+}
+
+template <int KC>
+__global__ __launch_bounds__(256) void aln_kernel(AlnParams P) {
+    const int lane = threadIdx.x & 63;
+    constexpr uint32_t CLAIM = 4;  // reads per work-queue claim
+    for (;;) {
+        uint32_t r0 = 0;
+        if (lane == 0) r0 = atomicAdd(&P.ctr[KC > 4 ? 1 : 0], CLAIM);
+        r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0);
+        if (r0 >= (uint32_t)P.n_reads) break;
+        const uint32_t r1 = r0 + CLAIM < (uint32_t)P.n_reads ? r0 + CLAIM : (uint32_t)P.n_reads;
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint64_t q0 = P.offs[r];
+            const int L = (int)(P.offs[r + 1] - q0);
+            if ((L > 256) != (KC > 4)) continue;  // the other instantiation's read
+            const uint8_t* query = P.codes + q0;
+            const uint64_t c0 = P.chain_off[r], c1 = P.chain_off[r + 1];
+            AlnReg* regs = P.raw + P.seed_off[r];
+            int nreg = 0;
+            for (uint64_t c = c0; c < c1; ++c) {
+                const OutChain ch = P.chains[c];
+                if (ch.n <= 0) continue;  // mem_chain2aln_short returns -1, nothing is made
+                const SeedRec* S = P.seeds + ch.seed_off;
+                if (chain_short(P, query, L, S, ch.n, regs + nreg, lane) == 0) {
+                    ++nreg;
+                    __threadfence_block();
+                } else {
+                    chain_full<KC>(P, query, L, S, ch.n, P.srt + ch.seed_off, regs, nreg, lane);
+                }
+            }
+            if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
+        }
+    }
+}
+
+// regions compacted per read (one thread per read)
+__global__ __launch_bounds__(256) void aln_write_kernel(AlnParams P) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= P.n_reads) return;
+    const uint64_t n = P.n_regs[r];
+    const AlnReg* src = P.raw + P.seed_off[r];
+    AlnReg* dst = P.out + P.reg_off[r];
+    for (uint64_t i = 0; i < n; ++i) dst[i] = src[i];
+}
+
+}  // namespace
+}  // namespace smem
+
+extern "C" hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
+    if (P->n_reads <= 0) return hipSuccess;
+    // up to 8 blocks of 4 waves per CU, every wave claiming reads from the queue
+    const int waves = (P->n_reads + 3) / 4;
+    const int blocks = std::max(1, std::min(n_cu * 8, (waves + 3) / 4));
+    hipLaunchKernelGGL(smem::aln_kernel<4>, dim3(blocks), dim3(256), 0, st, *P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !long_reads) return e;
+    hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(std::max(1, std::min(n_cu * 2, blocks))), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st) {
+    if (P->n_reads <= 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::aln_write_kernel, dim3((P->n_reads + 255) / 256), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -25,6 +26,7 @@
 #include "smem_kernels.h"
 #include "chain_kernels.h"
 #include "ksw_kernels.h"
+#include "aln_kernels.h"
 
 using smem::CallRec;
 using smem::Intv;
@@ -955,6 +957,145 @@ int smem_ksw_extend(smem_gpu_t* g, int n, const smem_ksw_task_t* tasks, const ui
     HIP_TRY(hipEventRecord(ev[1], st));
     HIP_TRY(hipMemcpyAsync(out, dr.p, sizeof(smem::KswResult) * n, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    if (kernel_ms) *kernel_ms = ms;
+    return SMEM_OK;
+}
+
+void smem_aln_opt_default(smem_aln_opt_t* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    smem_ksw_opt_default(&o->sc);
+    // mem_opt_init (software/bwamem.c:47-70)
+    o->a = 1, o->w = 100, o->zdrop = 100, o->pen_clip5 = o->pen_clip3 = 5, o->min_seed_len = 19;
+}
+
+static_assert(sizeof(smem_alnreg_t) == sizeof(smem::AlnReg), "region layout");
+static_assert(sizeof(smem_chain_t) == sizeof(smem::OutChain), "chain layout");
+static_assert(sizeof(smem_seed_t) == sizeof(smem::SeedRec), "seed layout");
+
+int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint64_t* offs, const smem_chain_t* chains,
+                   const uint64_t* chain_off, const smem_seed_t* seeds, uint64_t n_seeds, const uint8_t* pac,
+                   int64_t l_pac, const smem_aln_opt_t* opt, smem_alnreg_t* regs, uint64_t* reg_off,
+                   double* kernel_ms) {
+    g_err[0] = 0;
+    if (!g || n_reads < 0 || !opt || !reg_off || (n_reads > 0 && (!codes || !offs || !chain_off)) || l_pac <= 0 || !pac)
+        return fail(SMEM_E_ARG, "smem_chain2aln: bad arguments");
+    if (opt->sc.e_del < 1 || opt->sc.e_ins < 1 || opt->sc.o_del < 0 || opt->sc.o_ins < 0 || opt->a < 1 || opt->w < 0)
+        return fail(SMEM_E_ARG, "smem_chain2aln: scoring needs e >= 1, o >= 0, a >= 1, w >= 0");
+    if (kernel_ms) *kernel_ms = 0.0;
+    reg_off[0] = 0;
+    if (n_reads == 0) return SMEM_OK;
+    // per-read region capacity = its chains' seeds; the host checks every
+    // shape the kernel indexes with before anything is launched
+    const uint64_t n_chains = chain_off[n_reads];
+    std::vector<uint64_t> cap(n_reads + 1, 0);
+    bool long_reads = false;
+    for (int r = 0; r < n_reads; ++r) {
+        if (offs[r + 1] < offs[r] || offs[r + 1] - offs[r] > 1024 || chain_off[r + 1] < chain_off[r])
+            return fail(SMEM_E_ARG, "smem_chain2aln: read longer than 1024 bp or offsets not ascending");
+        long_reads |= offs[r + 1] - offs[r] > 256;
+        uint64_t c = 0;
+        for (uint64_t k = chain_off[r]; k < chain_off[r + 1]; ++k) {
+            const smem_chain_t& ch = chains[k];
+            if (ch.n < 0 || ch.seed_off + (uint64_t)ch.n > n_seeds)
+                return fail(SMEM_E_ARG, "smem_chain2aln: chain seeds outside seeds[]");
+            for (int i = 0; i < ch.n; ++i) {
+                const smem_seed_t& s = seeds[ch.seed_off + i];
+                if (s.qbeg < 0 || s.len <= 0 || (uint64_t)s.qbeg + s.len > offs[r + 1] - offs[r] || s.rbeg < 0 ||
+                    s.rbeg + s.len > 2 * l_pac)
+                    return fail(SMEM_E_ARG, "smem_chain2aln: seed outside its read or the text");
+            }
+            c += (uint64_t)ch.n;
+        }
+        cap[r + 1] = cap[r] + c;
+    }
+    const uint64_t n_bases = offs[n_reads], n_cap = cap[n_reads];
+    if (n_cap > 0 && !regs) return fail(SMEM_E_ARG, "smem_chain2aln: no region buffer");
+    HIP_TRY(hipSetDevice(g->device));
+    DevBuf<uint8_t> dcodes, dpac;
+    DevBuf<uint64_t> doffs, dchoff, dseedoff, dsrt, dnregs, dregoff;
+    DevBuf<smem::OutChain> dch;
+    DevBuf<smem::SeedRec> dseeds;
+    DevBuf<smem::AlnReg> draw, dout;
+    DevBuf<uint32_t> dctr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    struct Guard {
+        std::vector<std::function<void()>> f;
+        ~Guard() {
+            for (auto& x : f) x();
+        }
+    } guard;
+    guard.f.push_back([&] {
+        dcodes.release(); dpac.release(); doffs.release(); dchoff.release(); dseedoff.release(); dsrt.release();
+        dnregs.release(); dregoff.release(); dch.release(); dseeds.release(); draw.release(); dout.release();
+        dctr.release();
+        if (ev[0]) (void)hipEventDestroy(ev[0]);
+        if (ev[1]) (void)hipEventDestroy(ev[1]);
+        if (st) (void)hipStreamDestroy(st);
+    });
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&ev[0]));
+    HIP_TRY(hipEventCreate(&ev[1]));
+    const uint64_t pac_bytes = (uint64_t)(l_pac + 3) / 4;
+    HIP_TRY(dcodes.ensure(n_bases + 64));
+    HIP_TRY(dpac.ensure(pac_bytes + 64));
+    HIP_TRY(doffs.ensure(n_reads + 1));
+    HIP_TRY(dchoff.ensure(n_reads + 1));
+    HIP_TRY(dseedoff.ensure(n_reads + 1));
+    HIP_TRY(dsrt.ensure(n_seeds + 1));
+    HIP_TRY(dnregs.ensure(n_reads));
+    HIP_TRY(dregoff.ensure(n_reads + 1));
+    HIP_TRY(dch.ensure(n_chains + 1));
+    HIP_TRY(dseeds.ensure(n_seeds + 1));
+    HIP_TRY(draw.ensure(n_cap + 1));
+    HIP_TRY(dout.ensure(n_cap + 1));
+    HIP_TRY(dctr.ensure(2));
+    if (n_bases) HIP_TRY(hipMemcpyAsync(dcodes.p, codes, n_bases, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dpac.p, pac, pac_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(doffs.p, offs, 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dchoff.p, chain_off, 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dseedoff.p, cap.data(), 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
+    if (n_chains) HIP_TRY(hipMemcpyAsync(dch.p, chains, sizeof(smem::OutChain) * n_chains, hipMemcpyHostToDevice, st));
+    if (n_seeds) HIP_TRY(hipMemcpyAsync(dseeds.p, seeds, sizeof(smem::SeedRec) * n_seeds, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(dctr.p, 0, 8, st));
+    smem::AlnParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.codes = dcodes.p, P.offs = doffs.p, P.chains = dch.p, P.chain_off = dchoff.p, P.seeds = dseeds.p;
+    P.seed_off = dseedoff.p, P.pac = dpac.p, P.l_pac = l_pac, P.n_reads = n_reads;
+    std::memcpy(P.mat, opt->sc.mat, 25);
+    P.o_del = opt->sc.o_del, P.e_del = opt->sc.e_del, P.o_ins = opt->sc.o_ins, P.e_ins = opt->sc.e_ins;
+    P.a = opt->a, P.w = opt->w, P.zdrop = opt->zdrop, P.pen_clip5 = opt->pen_clip5, P.pen_clip3 = opt->pen_clip3;
+    P.min_seed_len = opt->min_seed_len;
+    {  // ksw_qinit's bias and largest score (software/ksw.c:78-85)
+        uint8_t sh = 127, md = 0;
+        for (int k = 0; k < 25; ++k) {
+            if (opt->sc.mat[k] < (int8_t)sh) sh = (uint8_t)opt->sc.mat[k];
+            if (opt->sc.mat[k] > (int8_t)md) md = (uint8_t)opt->sc.mat[k];
+        }
+        P.top = md, P.sw_shift = (uint8_t)(256 - sh);
+    }
+    P.srt = dsrt.p, P.raw = draw.p, P.n_regs = dnregs.p, P.ctr = dctr.p;
+    HIP_TRY(hipEventRecord(ev[0], st));
+    HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
+    HIP_TRY(hipEventRecord(ev[1], st));
+    std::vector<uint64_t> nr(n_reads);
+    HIP_TRY(hipMemcpyAsync(nr.data(), dnregs.p, 8 * n_reads, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int r = 0; r < n_reads; ++r) {
+        if (nr[r] > cap[r + 1] - cap[r]) return fail(SMEM_E_INTERNAL, "smem_chain2aln: region count past capacity");
+        reg_off[r + 1] = reg_off[r] + nr[r];
+    }
+    const uint64_t n_out = reg_off[n_reads];
+    if (n_out) {
+        HIP_TRY(hipMemcpyAsync(dregoff.p, reg_off, 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
+        P.reg_off = dregoff.p, P.out = dout.p;
+        HIP_TRY(smem_launch_aln_write(&P, st));
+        HIP_TRY(hipMemcpyAsync(regs, dout.p, sizeof(smem::AlnReg) * n_out, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
     if (kernel_ms) *kernel_ms = ms;

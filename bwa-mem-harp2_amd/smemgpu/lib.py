@@ -29,7 +29,7 @@ EXPORTED = [
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
     "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results", "smem_bwt_build_gpu_large",
-    "smem_ksw_opt_default", "smem_ksw_extend",
+    "smem_ksw_opt_default", "smem_ksw_extend", "smem_aln_opt_default", "smem_chain2aln",
 ]
 
 
@@ -110,6 +110,11 @@ def load() -> C.CDLL:
     lib.smem_ksw_opt_default.restype = None
     lib.smem_ksw_extend.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                     P(KswOptT), C.c_void_p, P(C.c_double)]
+    lib.smem_aln_opt_default.argtypes = [C.c_void_p]
+    lib.smem_aln_opt_default.restype = None
+    lib.smem_chain2aln.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_uint64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   P(C.c_double)]
     lib.smem_chain_opt_default.argtypes = [P(ChainOptT)]
     lib.smem_chain_opt_default.restype = None
     lib.smem_batch_chain.argtypes = [C.c_void_p, C.c_int64, P(ChainOptT)]
@@ -380,6 +385,28 @@ class Gpu:
         _check(lib.smem_ksw_extend(self._h, tasks.size, tasks.ctypes.data, q.ctypes.data, q.size, t.ctypes.data,
                                    t.size, C.byref(o), out.ctypes.data, C.byref(ms)), "smem_ksw_extend")
         return out[:tasks.size], ms.value
+
+    def chain2aln(self, pac, l_pac: int, codes, offs, chains, chain_off, seeds, opt) -> tuple:
+        """mem_chain2aln_short / mem_chain2aln of every chain of every read
+        (software/bwamem.c:1452-1460) on this device.  opt is a ctypes struct
+        laid out as smem_aln_opt_t.  Returns (regions as 64-byte smem_alnreg_t
+        records, reg_off[n_reads + 1], kernel ms)."""
+        lib = load()
+        pac = np.ascontiguousarray(pac, dtype=np.uint8)
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        chain_off = np.ascontiguousarray(chain_off, dtype=np.uint64)
+        chains = np.ascontiguousarray(chains, dtype=CHAIN_DT)
+        seeds = np.ascontiguousarray(seeds, dtype=SEED_DT)
+        n = offs.size - 1
+        cap = int(chains["n"].sum()) if chains.size else 0
+        regs = np.zeros(max(cap, 1) * 64, dtype=np.uint8)
+        reg_off = np.zeros(n + 1, dtype=np.uint64)
+        ms = C.c_double()
+        _check(lib.smem_chain2aln(self._h, n, codes.ctypes.data, offs.ctypes.data, chains.ctypes.data,
+                                  chain_off.ctypes.data, seeds.ctypes.data, seeds.size, pac.ctypes.data, l_pac,
+                                  C.byref(opt), regs.ctypes.data, reg_off.ctypes.data, C.byref(ms)), "smem_chain2aln")
+        return regs[:int(reg_off[-1]) * 64], reg_off, ms.value
 
     def close(self) -> None:
         if self._h:

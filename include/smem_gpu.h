@@ -233,6 +233,39 @@ int  smem_ksw_extend(smem_gpu_t *gpu, int n, const smem_ksw_task_t *tasks, const
                      const uint8_t *t, uint64_t t_bytes, const smem_ksw_opt_t *opt, smem_ksw_result_t *out,
                      double *kernel_ms);
 
+/* ------------------------------------------- chains -> alignment regions */
+/* mem_alnreg_t (software/bwamem.h:62-74); hash / sub / sub_n / secondary are
+ * left 0 here, as mem_chain2aln leaves them (mem_mark_primary sets them later) */
+typedef struct {
+	int64_t rb, re;
+	int32_t qb, qe, score, truesc, sub, csub, sub_n, w, seedcov, secondary;
+	uint64_t hash;
+} smem_alnreg_t;
+/* the mem_opt_t fields mem_chain2aln reads (software/bwamem.h:33-45) */
+typedef struct {
+	smem_ksw_opt_t sc;        /* matrix and gap penalties */
+	int a;                    /* match score, 1 */
+	int w;                    /* band width, 100 */
+	int zdrop;                /* 100 */
+	int pen_clip5, pen_clip3; /* 5, 5 */
+	int min_seed_len;         /* 19 */
+} smem_aln_opt_t;
+void smem_aln_opt_default(smem_aln_opt_t *opt);
+/* The loop of mem_align1_core over every read's chains (software/bwamem.c:1452-1460):
+ * mem_chain2aln_short, then mem_chain2aln when it declines (software/bwamem.c:805-852,
+ * 1040-1188), on the GPU, one wave per read.  Replaces the host-side calls at
+ * software/bwamem.c:1421-1422 / 1457-1458.  Inputs are host buffers in the layout
+ * smem_batch_chain_results returns (chains[chain_off[r] .. chain_off[r+1]) of read r,
+ * seeds[n_seeds] indexed by smem_chain_t.seed_off) plus the reads (nt4 codes, offs[n+1])
+ * and the 2-bit forward-strand .pac (software/bntseq.c:303-309, l_pac bases).
+ * regs must hold one region per chain seed (sum of chains' n); reg_off[n_reads + 1]
+ * gets each read's regions, in the order the reference appends them.  Reads longer
+ * than 1024 bp give SMEM_E_ARG. */
+int  smem_chain2aln(smem_gpu_t *gpu, int n_reads, const uint8_t *codes, const uint64_t *offs,
+                    const smem_chain_t *chains, const uint64_t *chain_off, const smem_seed_t *seeds, uint64_t n_seeds,
+                    const uint8_t *pac, int64_t l_pac, const smem_aln_opt_t *opt, smem_alnreg_t *regs,
+                    uint64_t *reg_off, double *kernel_ms);
+
 /* ---------------------------------------------------------- telemetry */
 typedef struct {
 	double kernel_ms;        /* seeding kernel(s), HIP events on the batch stream */

@@ -90,6 +90,9 @@ def load() -> C.CDLL:
         lib.orc_ksw_batch.restype = C.c_int
         lib.orc_chain.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(ChainOptT), C.c_int,
                                   C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64)]
+        lib.orc_aln_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p]
+        lib.orc_aln_batch.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -333,3 +336,52 @@ def ksw(batch) -> np.ndarray:
 def ref_ksw(smkt: str, out: str) -> None:
     """The compiled reference's own ksw_extend2 on every task of an SMKT file."""
     subprocess.run([REF, "ksw", smkt, out], check=True)
+
+
+# ---- chains -> regions (aln_oracle.c) --------------------------------------
+class AlnOptT(C.Structure):
+    """orc_aln_opt_t (= smem_aln_opt_t)"""
+    _fields_ = [("mat", C.c_int8 * 25), ("pad", C.c_int8 * 3), ("o_del", C.c_int32), ("e_del", C.c_int32),
+                ("o_ins", C.c_int32), ("e_ins", C.c_int32), ("a", C.c_int32), ("w", C.c_int32), ("zdrop", C.c_int32),
+                ("pen_clip5", C.c_int32), ("pen_clip3", C.c_int32), ("min_seed_len", C.c_int32)]
+
+
+def aln_opt(w=100, min_seed_len=19, a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1, zdrop=100, pen_clip5=5,
+            pen_clip3=5) -> AlnOptT:
+    """mem_opt_init's scoring (software/bwamem.c:47-70), bwa_fill_scmat (software/bwa.c:84-93)"""
+    o = AlnOptT()
+    for i in range(4):
+        for j in range(4):
+            o.mat[i * 5 + j] = a if i == j else -b
+        o.mat[i * 5 + 4] = -1
+    for j in range(5):
+        o.mat[20 + j] = -1
+    o.o_del, o.e_del, o.o_ins, o.e_ins, o.a, o.w, o.zdrop = o_del, e_del, o_ins, e_ins, a, w, zdrop
+    o.pen_clip5, o.pen_clip3, o.min_seed_len = pen_clip5, pen_clip3, min_seed_len
+    return o
+
+
+def aln(pac, l_pac: int, codes, offs, chains, chain_off, seeds, opt: AlnOptT):
+    """The restated mem_chain2aln_short / mem_chain2aln loop over every read's
+    chains: (regions as golden_data.ALNREG_DT, reg_off[n_reads + 1])."""
+    from tests.golden_data import ALNREG_DT
+    lib = load()
+    pac = np.ascontiguousarray(pac, dtype=np.uint8)
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    chain_off = np.ascontiguousarray(chain_off, dtype=np.uint64)
+    chains = np.ascontiguousarray(chains)
+    seeds = np.ascontiguousarray(seeds)
+    n = offs.size - 1
+    reg_off = np.zeros(n + 1, dtype=np.uint64)
+    p = C.c_void_p()
+    rc = lib.orc_aln_batch(C.byref(opt), l_pac, pac.ctypes.data, n, codes.ctypes.data, offs.ctypes.data,
+                           chains.ctypes.data, chain_off.ctypes.data, seeds.ctypes.data, C.byref(p),
+                           reg_off.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("orc_aln_batch failed")
+    k = int(reg_off[-1])
+    out = np.frombuffer((C.c_uint8 * (k * 64)).from_address(p.value), dtype=ALNREG_DT).copy() if k else \
+        np.zeros(0, dtype=ALNREG_DT)
+    lib.orc_free(p)
+    return out, reg_off

@@ -28,6 +28,13 @@
  *       when filter != 0, mem_chain_flt() (software/bwamem.c:629) as
  *       mem_align1_core calls them (software/bwamem.c:1448-1449); chains
  *       written as SMCH (include/smem_formats.h).
+ *   aln   <in.bwt> <in.sa> <in.pac> <reads.smrd> <out.smrg> <k> <r> <s> <start_width> <max_occ> <w>
+ *         <max_chain_gap> <mask_level> <drop_ratio>
+ *       mem_chain + mem_chain_flt as for chain (filter on), then per chain
+ *       mem_chain2aln_short and, when it declines, mem_chain2aln
+ *       (software/bwamem.c:1452-1460); every read's regions written as SMRG:
+ *       "SMRG0001", u64 n_reads, per read u32 n then n x {i64 rb, re;
+ *       i32 qb, qe, score, truesc, sub, csub, sub_n, w, seedcov, secondary}.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -298,6 +305,77 @@ static int cmd_chain(int argc, char **argv)
 	return 0;
 }
 
+extern int mem_chain2aln_short(const mem_opt_t *opt, int64_t l_pac, const uint8_t *pac, int l_query,
+		const uint8_t *query, const h_chain_t *c, mem_alnreg_v *av);
+extern void mem_chain2aln(const mem_opt_t *opt, int64_t l_pac, const uint8_t *pac, int l_query, const uint8_t *query,
+		const h_chain_t *c, mem_alnreg_v *av);
+
+static int cmd_aln(int argc, char **argv)
+{
+	bwt_t *bwt;
+	smrd_reads_t r;
+	mem_opt_t *opt;
+	FILE *out, *fp;
+	uint64_t i;
+	int64_t l_pac;
+	uint8_t *pac;
+	if (argc < 15) {
+		fprintf(stderr, "usage: aln <bwt> <sa> <pac> <reads> <out> <k> <r> <s> <sw> <max_occ> <w> <gap> <mask> <drop>\n");
+		return 1;
+	}
+	opt = mem_opt_init();
+	opt->min_seed_len = atoi(argv[6]);
+	opt->split_factor = (float)atof(argv[7]);
+	opt->split_width = atoi(argv[8]);
+	if (atoi(argv[9]) == 2) opt->flag |= MEM_F_NO_EXACT;
+	opt->max_occ = atoi(argv[10]);
+	opt->w = atoi(argv[11]);
+	opt->max_chain_gap = atoi(argv[12]);
+	opt->mask_level = (float)atof(argv[13]);
+	opt->chain_drop_ratio = (float)atof(argv[14]);
+	bwt = bwt_restore_bwt(argv[1]);
+	bwt_restore_sa(argv[2], bwt);
+	l_pac = (int64_t)(bwt->seq_len >> 1);
+	pac = calloc(l_pac / 4 + 1, 1);
+	fp = fopen(argv[3], "rb");
+	if (!fp || fread(pac, 1, (l_pac + 3) / 4, fp) != (size_t)((l_pac + 3) / 4)) return 1;
+	fclose(fp);
+	if (smrd_load(argv[4], &r) != 0) return 1;
+	out = fopen(argv[5], "wb");
+	if (!out) return 1;
+	fwrite("SMRG0001", 1, 8, out);
+	fwrite(&r.n_reads, 8, 1, out);
+	for (i = 0; i < r.n_reads; ++i) {
+		const uint8_t *q = r.codes + r.off[i];
+		h_chain_v c = mem_chain(opt, bwt, l_pac, r.len[i], q);
+		mem_alnreg_v av = { 0, 0, 0 };
+		uint32_t j, n;
+		c.n = mem_chain_flt(opt, (int)c.n, c.a);
+		for (j = 0; j < c.n; ++j)   /* software/bwamem.c:1452-1460 */
+			if (mem_chain2aln_short(opt, l_pac, pac, r.len[i], q, &c.a[j], &av) > 0)
+				mem_chain2aln(opt, l_pac, pac, r.len[i], q, &c.a[j], &av);
+		n = (uint32_t)av.n;
+		fwrite(&n, 4, 1, out);
+		for (j = 0; j < n; ++j) {
+			const mem_alnreg_t *a = &av.a[j];
+			int32_t v[10] = { a->qb, a->qe, a->score, a->truesc, a->sub, a->csub, a->sub_n, a->w, a->seedcov,
+				a->secondary };
+			fwrite(&a->rb, 8, 1, out);
+			fwrite(&a->re, 8, 1, out);
+			fwrite(v, 4, 10, out);
+		}
+		free(av.a);
+		for (j = 0; j < c.m && j < c.n; ++j) free(c.a[j].seeds);
+		free(c.a);
+	}
+	fclose(out);
+	smrd_free(&r);
+	free(pac);
+	free(opt);
+	bwt_destroy(bwt);
+	return 0;
+}
+
 /* ksw <tasks.smkt> <out.smkr>: the reference's own ksw_extend2 on every task */
 extern int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m, const int8_t *mat,
 		int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle,
@@ -357,6 +435,7 @@ int main(int argc, char **argv)
 	if (strcmp(argv[1], "sa") == 0) return cmd_sa(argc - 1, argv + 1);
 	if (strcmp(argv[1], "chain") == 0) return cmd_chain(argc - 1, argv + 1);
 	if (strcmp(argv[1], "ksw") == 0) return cmd_ksw(argc - 1, argv + 1);
+	if (strcmp(argv[1], "aln") == 0) return cmd_aln(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

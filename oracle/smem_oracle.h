@@ -133,4 +133,24 @@ int orc_ksw_extend(const orc_ksw_task_t *t, const uint8_t *query, const uint8_t 
 int orc_ksw_batch(int64_t n, const orc_ksw_task_t *tasks, const uint8_t *q, const uint8_t *t, const orc_ksw_opt_t *o,
 		orc_ksw_result_t *out);
 
+/* ---- chains -> alignment regions (aln_oracle.c): mem_chain2aln_short /
+ * mem_chain2aln, software/bwamem.c:805-852, 1040-1188 ---- */
+typedef struct {
+	int8_t mat[25], pad[3];
+	int32_t o_del, e_del, o_ins, e_ins;
+	int32_t a, w, zdrop, pen_clip5, pen_clip3, min_seed_len;
+} orc_aln_opt_t;                     /* the layout of smem_aln_opt_t */
+typedef struct {
+	int64_t rb, re;
+	int32_t qb, qe, score, truesc, sub, csub, sub_n, w, seedcov, secondary;
+	uint64_t hash;
+} orc_alnreg_t;                      /* mem_alnreg_t, the layout of smem_alnreg_t */
+typedef struct { int64_t pos; uint64_t seed_off; int32_t n, pad; } orc_aln_chain_t;   /* smem_chain_t */
+void orc_sw_shift_top(const int8_t *mat, int *shift, int *top);
+int orc_aln_read(const orc_aln_opt_t *o, int64_t l_pac, const uint8_t *pac, int l_query, const uint8_t *query,
+		int n_chains, const orc_aln_chain_t *chains, const orc_seed_t *seeds, orc_alnreg_t **out);
+int orc_aln_batch(const orc_aln_opt_t *o, int64_t l_pac, const uint8_t *pac, int64_t n_reads, const uint8_t *codes,
+		const uint64_t *offs, const orc_aln_chain_t *chains, const uint64_t *chain_off, const orc_seed_t *seeds,
+		orc_alnreg_t **regs, uint64_t *reg_off);
+
 #endif

@@ -269,9 +269,62 @@ def make_ksw():
         shutil.rmtree(tmp)
 
 
+# chains -> regions (mem_chain2aln_short / mem_chain2aln, software/bwamem.c:805-852,
+# 1040-1188): the reference's own regions for every read of a seeding case,
+# over the chains the matching filtered SMCH fixture holds
+ALN_CASES = [("g1", "default", "std"), ("g1", "k14s20", "tight"), ("g2", "default", "std"), ("g2", "k14s20", "std")]
+
+
+def make_aln():
+    if not oracle.ref_available():
+        oracle.build(ref=True)
+    tmp = tempfile.mkdtemp()
+    try:
+        with open(os.path.join(HERE, "manifest.json")) as fh:
+            manifest = json.load(fh)
+        copts = {c["name"]: c for c in CHAIN_OPTS}
+        for g in ("g1", "g2"):
+            with gzip.open(os.path.join(HERE, g + ".fa.gz"), "rb") as fh, open(os.path.join(tmp, g + ".fa"), "wb") as o:
+                o.write(fh.read())
+            oracle.ref_index(os.path.join(tmp, g + ".fa"), os.path.join(tmp, g))
+            with open(os.path.join(tmp, g + ".pac"), "rb") as fh:
+                gz_write(os.path.join(HERE, g + ".pac.gz"), fh.read())
+            rd = "r1.smrd" if g == "g1" else "r2.smrd"
+            with gzip.open(os.path.join(HERE, rd + ".gz"), "rb") as fh, open(os.path.join(tmp, rd), "wb") as o:
+                o.write(fh.read())
+        out_cases = []
+        for g, cname, oname in ALN_CASES:
+            cases = manifest["cases"] if g == "g1" else manifest["g2"]["cases"]
+            case = next(c for c in cases if c["name"] == cname)
+            reads = synth.read_smrd(os.path.join(tmp, "r1.smrd" if g == "g1" else "r2.smrd"))
+            sub = os.path.join(tmp, "sub.smrd")
+            synth.write_smrd(sub, reads.subset(np.arange(case["n_reads"])))
+            o, co = case["opt"], copts[oname]
+            out = os.path.join(tmp, "a.smrg")
+            subprocess.run([oracle.REF, "aln", os.path.join(tmp, g + ".bwt"), os.path.join(tmp, g + ".sa"),
+                            os.path.join(tmp, g + ".pac"), sub, out, str(o["min_seed_len"]), str(o["split_factor"]),
+                            str(o["split_width"]), str(o["start_width"]), str(MAX_OCC), str(co["w"]),
+                            str(co["max_chain_gap"]), str(co["mask_level"]), str(co["drop_ratio"])], check=True)
+            with open(out, "rb") as fh:
+                data = fh.read()
+            fn = f"{g}_{cname}_{oname}.smrg.gz"
+            gz_write(os.path.join(HERE, fn), data)
+            chain = next(c for c in case["chains"] if c["name"] == oname and c["filter"] == 1)
+            out_cases.append(dict(genome=g, case=cname, chain_file=chain["file"], file=fn, w=co["w"],
+                                  min_seed_len=o["min_seed_len"], sha256=hashlib.sha256(data).hexdigest()))
+        manifest["aln"] = out_cases
+        with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+            json.dump(manifest, fh, indent=1)
+    finally:
+        shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
-    if "--ksw-only" in sys.argv:
+    if "--aln-only" in sys.argv:
+        make_aln()
+    elif "--ksw-only" in sys.argv:
         make_ksw()
+        make_aln()
     elif "--chains-only" in sys.argv:
         chains_only()
     elif "--g2-only" in sys.argv:

@@ -133,3 +133,72 @@ def files(genome: str, d: str):
             fh.write(_gz(name + ".gz"))
         out[name.split(".")[-1]] = p
     return out
+
+
+# ---- chains -> regions (mem_chain2aln) fixtures ----------------------------
+ALNREG_DT = np.dtype([("rb", "<i8"), ("re", "<i8"), ("qb", "<i4"), ("qe", "<i4"), ("score", "<i4"),
+                      ("truesc", "<i4"), ("sub", "<i4"), ("csub", "<i4"), ("sub_n", "<i4"), ("w", "<i4"),
+                      ("seedcov", "<i4"), ("secondary", "<i4"), ("hash", "<u8")])   # smem_alnreg_t, 64 B
+_SMRG_REC = np.dtype([("rb", "<i8"), ("re", "<i8"), ("qb", "<i4"), ("qe", "<i4"), ("score", "<i4"),
+                      ("truesc", "<i4"), ("sub", "<i4"), ("csub", "<i4"), ("sub_n", "<i4"), ("w", "<i4"),
+                      ("seedcov", "<i4"), ("secondary", "<i4")])
+
+
+def aln_fixtures():
+    """every (genome, seeding case, chain file, region file) the reference's
+    mem_chain2aln loop produced (tests/golden/make_golden.py make_aln)"""
+    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+        return json.load(fh).get("aln", [])
+
+
+def pac(genome: str) -> np.ndarray:
+    """the 2-bit forward strand bwa_index wrote (software/bntseq.c:303-309)"""
+    n = (l_pac(genome) + 3) // 4
+    return np.frombuffer(_gz(f"{genome}.pac.gz"), dtype=np.uint8)[:n].copy()
+
+
+def smch_parse(data: bytes):
+    """SMCH stream -> (chains as smemgpu CHAIN_DT, chain_off[n+1], seeds as SEED_DT)"""
+    import struct
+    from smemgpu.lib import CHAIN_DT, SEED_DT
+    assert data[:8] == b"SMCH0001"
+    n_reads = struct.unpack_from("<Q", data, 8)[0]
+    p, chains, seeds, off = 16, [], [], [0]
+    for _ in range(n_reads):
+        nc = struct.unpack_from("<I", data, p)[0]
+        p += 4
+        for _ in range(nc):
+            pos, n = struct.unpack_from("<qI", data, p)
+            p += 12
+            chains.append((pos, len(seeds), n, 0))
+            for _ in range(n):
+                seeds.append(struct.unpack_from("<qii", data, p))
+                p += 16
+        off.append(len(chains))
+    return (np.array(chains, dtype=CHAIN_DT), np.array(off, dtype=np.uint64), np.array(seeds, dtype=SEED_DT))
+
+
+def smrg_parse(data: bytes):
+    """SMRG stream -> (regions as ALNREG_DT, reg_off[n+1])"""
+    import struct
+    assert data[:8] == b"SMRG0001"
+    n_reads = struct.unpack_from("<Q", data, 8)[0]
+    p, parts, off = 16, [], [0]
+    for _ in range(n_reads):
+        n = struct.unpack_from("<I", data, p)[0]
+        p += 4
+        parts.append(np.frombuffer(data, dtype=_SMRG_REC, count=n, offset=p))
+        p += n * _SMRG_REC.itemsize
+        off.append(off[-1] + n)
+    regs = np.zeros(off[-1], dtype=ALNREG_DT)
+    if off[-1]:
+        cat = np.concatenate(parts)
+        for f in _SMRG_REC.names:
+            regs[f] = cat[f]
+    return regs, np.array(off, dtype=np.uint64)
+
+
+def smrg(fix) -> bytes:
+    data = _gz(fix["file"])
+    assert hashlib.sha256(data).hexdigest() == fix["sha256"], "fixture corrupted"
+    return data

@@ -1,0 +1,146 @@
+"""Chains -> alignment regions: the loop of
+mem_align1_core over every read's chains (software/bwamem.c:1452-1460),
+mem_chain2aln_short (software/bwamem.c:805-852, ksw_align2) and, when it
+declines, mem_chain2aln (software/bwamem.c:1040-1188, ksw_extend2 both ways).
+
+Bar: bit-exact — per read, every region's rb / re / qb / qe / score / truesc /
+csub / w / seedcov in the reference's order.  The restatement
+(oracle/aln_oracle.c) is pinned to the compiled reference's own regions
+(tests/golden/*.smrg.gz, `ref_harness aln`) over the reference's own
+filtered chains (the matching *.smch.gz); the GPU path (smem_chain2aln,
+through the C ABI) is checked against the same fixtures and against the
+restatement on larger repeat-rich genomes with chains from the GPU chain stage.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests import golden_data
+
+FIX = golden_data.aln_fixtures()
+FIELDS = ["rb", "re", "qb", "qe", "score", "truesc", "sub", "csub", "sub_n", "w", "seedcov", "secondary"]
+
+
+def _reads(g, n):
+    from smemgpu import synth
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        p = golden_data.files(g, d)
+        return synth.read_smrd(p["smrd"]).subset(np.arange(n))
+
+
+def _case_inputs(fix):
+    cases = golden_data.genome_cases(fix["genome"])
+    case = next(c for c in cases if c["name"] == fix["case"])
+    chain = next(c for c in case["chains"] if c["file"] == fix["chain_file"])
+    chains, chain_off, seeds = golden_data.smch_parse(golden_data.smch(chain))
+    reads = _reads(fix["genome"], case["n_reads"])
+    assert chain_off.size == reads.n + 1
+    return reads, chains, chain_off, seeds
+
+
+def _assert_same(got, got_off, want, want_off):
+    assert np.array_equal(np.asarray(got_off, dtype=np.uint64), np.asarray(want_off, dtype=np.uint64))
+    for f in FIELDS:
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert bad.size == 0, f"field {f}: {bad.size} regions differ, first {bad[:5]}"
+
+
+def test_aln_fixtures_present():
+    assert len(FIX) >= 4
+    assert {f["genome"] for f in FIX} == {"g1", "g2"}
+
+
+@pytest.mark.parametrize("fix", FIX, ids=[f["file"].split(".")[0] for f in FIX])
+def test_aln_oracle_vs_reference(fix):
+    """restatement == the reference's mem_chain2aln loop, region for region"""
+    reads, chains, chain_off, seeds = _case_inputs(fix)
+    want, want_off = golden_data.smrg_parse(golden_data.smrg(fix))
+    assert want.size > 0
+    got, got_off = oracle.aln(golden_data.pac(fix["genome"]), golden_data.l_pac(fix["genome"]), reads.codes,
+                              reads.offs, chains, chain_off, seeds,
+                              oracle.aln_opt(w=fix["w"], min_seed_len=fix["min_seed_len"]))
+    _assert_same(got, got_off, want, want_off)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fix", FIX, ids=[f["file"].split(".")[0] for f in FIX])
+def test_aln_gpu_vs_reference(gpu_device, fix):
+    import smemgpu
+    from smemgpu import synth
+    reads, chains, chain_off, seeds = _case_inputs(fix)
+    want, want_off = golden_data.smrg_parse(golden_data.smrg(fix))
+    idx = smemgpu.Index.read(golden_data.files(fix["genome"], _tmpdir())["bwt"])
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        raw, off, ms = gpu.chain2aln(golden_data.pac(fix["genome"]), golden_data.l_pac(fix["genome"]), reads.codes,
+                                     reads.offs, chains, chain_off, seeds,
+                                     oracle.aln_opt(w=fix["w"], min_seed_len=fix["min_seed_len"]))
+    finally:
+        gpu.close()
+    got = np.frombuffer(raw.tobytes(), dtype=golden_data.ALNREG_DT)
+    _assert_same(got, off, want, want_off)
+    del synth
+
+
+def _tmpdir():
+    import tempfile
+    return tempfile.mkdtemp()
+
+
+def _pack(codes):
+    """2-bit forward strand as bns_fasta2bntseq packs it (software/bntseq.c:303-309)"""
+    c = np.asarray(codes, dtype=np.uint8)
+    c = np.where(c > 3, 0, c).astype(np.uint8)
+    pad = (-c.size) % 4
+    c = np.concatenate([c, np.zeros(pad, dtype=np.uint8)]).reshape(-1, 4)
+    return (c[:, 0] << 6 | c[:, 1] << 4 | c[:, 2] << 2 | c[:, 3]).astype(np.uint8)
+
+
+def test_pack_matches_reference_pac():
+    """the test-side packer gives bwa_index's .pac on the golden genomes (no N)"""
+    import gzip
+    import os
+    for g in ("g1", "g2"):
+        with gzip.open(os.path.join(golden_data.GOLDEN, g + ".fa.gz"), "rb") as fh:
+            codes = golden_data.fasta_codes(fh.read())
+        assert np.array_equal(_pack(codes), golden_data.pac(g))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", [100, 20])
+def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w):
+    """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
+    kernel instantiations) with substitutions and Ns; chains from the GPU
+    chain stage; GPU regions == restatement."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(600_000, seed=91, repeat_frac=0.6, n_families=5, exact_frac=0.01, tandem_frac=0.01)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        reads = synth.concat_reads([synth.make_reads(g.codes, 2000, 150, seed=92, sub_rate=0.02),
+                                    synth.make_reads(g.codes, 1000, (70, 250), seed=93, n_rate=0.01, sub_rate=0.03),
+                                    synth.make_reads(g.codes, 600, (257, 700), seed=94, sub_rate=0.02),
+                                    synth.make_reads(g.codes, 400, 101, seed=95, random_frac=0.3)])
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        try:
+            b.set_reads(reads.codes, reads.offs)
+            b.run(smemgpu.Options())
+            b.sa(19, 10000)
+            l_pac = int(g.codes.size)
+            b.chain(l_pac, w=w)
+            res = b.fetch()
+            chains, chain_off, seeds = res.chains, res.chain_off, res.seeds
+        finally:
+            b.close()
+        opt = oracle.aln_opt(w=w)
+        pac = _pack(g.codes)
+        raw, off, ms = gpu.chain2aln(pac, l_pac, reads.codes, reads.offs, chains, chain_off, seeds, opt)
+    finally:
+        gpu.close()
+    want, want_off = oracle.aln(pac, l_pac, reads.codes, reads.offs, chains, chain_off, seeds, opt)
+    assert want.size > 1000
+    got = np.frombuffer(raw.tobytes(), dtype=golden_data.ALNREG_DT)
+    _assert_same(got, off, want, want_off)
