@@ -156,11 +156,57 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
         else:
             secs, _ = oracle.seed_timed(oi, sample.codes, sample.offs, threads=cores)
         cpu = {"value": round(m / secs, 1), "unit": "reads/s", "cores": cores, "kind": kind,
+               "host": cpu_inventory(),
+               "per_core": round(m / secs / cores, 1),
                "sample": f"first {m} of the benchmark's {args.read_len} bp reads on rank 0, {secs:.1f} s wall, "
                          f"{cores} pthreads"}
     oi.close()
     sw = sw_cpu(sw_tasks) if (sw_tasks is not None and args.cpu_seconds > 0) else None
     return bpr, b64, st, n, parity, cpu, sw
+
+
+def cpu_inventory() -> dict:
+    """The host's CPUs as this process may use them: logical CPUs, physical
+    cores (distinct (package, core) pairs of /proc/cpuinfo), the affinity
+    mask, the cgroup CPU quota, and the model.  `use` = the threads the CPU
+    baseline runs: one per physical core, capped by the affinity mask and the
+    cgroup quota (threads past the quota only time-slice)."""
+    inv = {"logical": os.cpu_count() or 1, "model": None}
+    try:
+        inv["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        inv["affinity"] = inv["logical"]
+    cores, pkg, core = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and inv["model"] is None:
+                    inv["model"] = v
+                elif k == "physical id":
+                    pkg = v
+                elif k == "core id":
+                    core = v
+                elif not k and pkg is not None:
+                    cores.add((pkg, core))
+                    pkg = core = None
+        if pkg is not None:
+            cores.add((pkg, core))
+    except OSError:
+        pass
+    inv["physical_cores"] = len(cores) or inv["logical"]
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    inv["cgroup_quota_cpus"] = quota
+    inv["use"] = max(1, min(inv["physical_cores"], inv["affinity"], quota or 1 << 30))
+    return inv
 
 
 def traffic_for(args, path: str):
@@ -408,7 +454,8 @@ def main():
     del genome_codes
 
     if rank == 0:
-        cores = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
+        inv = cpu_inventory()
+        cores = inv["use"]
         bpr, bpr64, ostats, n_counted, parity, cpu, sw_cpu_rep = cpu_leg(args, gpu, opt, idx, idx_path, reads, cores,
                                                                           sw_tasks)
         if sw_rep is not None:
@@ -469,6 +516,8 @@ def main():
             "chaining": chain_rep,
             "sw_extension": sw_rep,
             "overflow_reads": st["n_overflow"],
+            "build_id": smemgpu.build_id(),
+            "build_id_matches_sources": smemgpu.build_id() == smemgpu.source_hash(),
         }
         print(json.dumps(out), flush=True)
     for b in batches:

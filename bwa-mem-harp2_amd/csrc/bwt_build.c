@@ -10,7 +10,8 @@
  *            16 MSB-first 2-bit symbols, plus one trailing count block
  *            (software/bwtindex.c:128-150, software/bwt.h:72-73)
  *   file   = primary, L2[1..4], words   (software/bwt.c:841-850)
- * The result is byte-identical to `bwa index -a is` (tests/test_index.py).
+ * The result is byte-identical to `bwa index -a is` (tests/test_oracle.py::
+ * test_index_builder_matches_reference / test_index_builder_small_vs_reference).
  *
  * Indices are 32-bit: text length (2 x genome) must stay below 2^32 - 2.
  */

@@ -183,6 +183,11 @@ struct smem_batch {
 
 extern "C" {
 
+#ifndef SMEM_SRC_HASH
+#define SMEM_SRC_HASH "unknown"
+#endif
+const char* smem_gpu_build_id(void) { return SMEM_SRC_HASH; }
+
 const char* smem_strerror(int code) {
     if (g_err[0]) return g_err;
     switch (code) {

@@ -26,11 +26,34 @@ EXPORTED = [
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
     "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_batch_debug", "smem_strerror",
+    "smem_gpu_build_id",
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
     "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results", "smem_bwt_build_gpu_large",
     "smem_ksw_opt_default", "smem_ksw_extend", "smem_aln_opt_default", "smem_chain2aln",
 ]
+
+
+def source_hash() -> str:
+    """The content hash bwa-mem-harp2_amd/Makefile compiles into the library
+    (SRC_HASH): sha256 of csrc/*.{hip,cpp,c,h} and include/*.h, concatenated in
+    path order, first 16 hex digits."""
+    import glob
+    import hashlib
+    inc = os.path.join(os.path.dirname(PKG_DIR), "include")
+    files = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.hip")) + glob.glob(os.path.join(PKG_DIR, "csrc", "*.cpp"))
+                   + glob.glob(os.path.join(PKG_DIR, "csrc", "*.c")) + glob.glob(os.path.join(PKG_DIR, "csrc", "*.h"))
+                   + glob.glob(os.path.join(inc, "*.h")))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    """The source hash the loaded libsmemgpu.so was built from."""
+    return load().smem_gpu_build_id().decode()
 
 
 class SmemError(RuntimeError):
@@ -142,6 +165,8 @@ def load() -> C.CDLL:
         lib.smem_batch_debug.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     lib.smem_strerror.argtypes = [C.c_int]
     lib.smem_strerror.restype = C.c_char_p
+    lib.smem_gpu_build_id.argtypes = []
+    lib.smem_gpu_build_id.restype = C.c_char_p
     _lib = lib
     return lib
 

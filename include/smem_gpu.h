@@ -301,6 +301,10 @@ int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
  * run; returns the number of words copied or a negative code */
 int  smem_batch_debug(const smem_batch_t *b, uint64_t *out, uint64_t n_words);
 const char *smem_strerror(int code);
+/* content hash (16 hex digits) of the sources this library was built from
+ * (bwa-mem-harp2_amd/Makefile SRC_HASH): lets a caller prove that the .so it
+ * loaded is the build of the sources beside it */
+const char *smem_gpu_build_id(void);
 
 #ifdef __cplusplus
 }

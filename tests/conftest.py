@@ -16,14 +16,29 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 
 
+def _lib_is_current(lib: str) -> bool:
+    """The .so's compiled-in source hash equals the hash of the sources beside
+    it (a stale library pushed with the tree is rebuilt, never tested)."""
+    if not os.path.exists(lib):
+        return False
+    import subprocess
+    # in a child process: a loaded .so cannot be replaced in this one
+    code = ("import smemgpu,sys; sys.exit(0 if smemgpu.build_id() == smemgpu.source_hash() else 1)")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([PKG, ROOT]))
+    return subprocess.run([sys.executable, "-c", code], env=env).returncode == 0
+
+
 @pytest.fixture(scope="session")
 def built():
-    """Make sure the native artefacts exist (build once per session)."""
+    """Make sure the native artefacts exist and are built from the current
+    sources (build once per session)."""
     lib = os.path.join(PKG, "lib", "libsmemgpu.so")
     orc = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
-    if not (os.path.exists(lib) and os.path.exists(orc)):
+    if not (_lib_is_current(lib) and os.path.exists(orc)):
         import __graft_entry__
         __graft_entry__.build()
+    import smemgpu
+    assert smemgpu.build_id() == smemgpu.source_hash(), "libsmemgpu.so is not the build of these sources"
     return True
 
 
