@@ -1,35 +1,47 @@
 """SMEM-seeding benchmark (BASELINE.json metric) on 1..N MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5] [--genome-profile uniform|human]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Workload (BASELINE.json configs[1]): an FM index resident in HBM and 1M x
-150 bp single-end reads per GPU (2% substitutions, 0.1% N, both strands).
-human_g1k_v37 is not available offline, so the index is built from a seeded
-synthetic genome (random sequence with repeat families, exact and tandem
-repeats; smemgpu/synth.py) by this repo's own `bwa index -a is`-identical
-builder; its size is reported in `config`.
+Workload (BASELINE.json configs[1], the default --config c2): an FM index
+resident in HBM and 1M x 150 bp single-end reads per GPU (2% substitutions,
+0.1% N, both strands).  human_g1k_v37 is not available offline, so the index
+is built from a seeded synthetic genome of its size (smemgpu/synth.py:
+random sequence with repeat families, exact and tandem repeats; or, with
+--genome-profile human, a human-like ~46 % interspersed-repeat profile) by
+this repo's own `bwa index -a is`-identical builder; its size is in `config`.
 
 A step = one pass of the seeding hot path (mem_insert_seed's smem_next2 loop
 for every read, software/bwamem.c:453-460) over the resident batch: the
-seeding kernel plus result compaction, outputs left in HBM (host transfers
-excluded; DESIGN.md gives the PCIe-inclusive rate).  As the reference's
-kt_for_batch workers do, --streams host workers (default 2) each own a batch
-(all the reads) and a HIP stream and run whole steps dealt round-robin, so
-one step's tail overlaps the next step's start; K steps are timed in total.
-Reads shard across ranks with no collective in the data path (index
-replicated): scaling "weak".
+seeding kernel plus result compaction, outputs left in HBM.  As the
+reference's kt_for_batch workers do, --streams host workers (default 2) each
+own a batch (all the reads) and a HIP stream and run whole steps dealt
+round-robin, so one step's tail overlaps the next step's start; K steps are
+timed in total.  Reads shard across ranks with no collective in the data path
+(index replicated): the read stream is cut into blocks of 256k reads dealt
+round-robin to the ranks; scaling "weak".
 
-roofline: dominant kernel = seed_kernel; achieved = algorithmic bytes per
+`streaming`: the same path with host buffers -- bwa mem's chunk loop through
+smem_gpu_seed_stream (chunks staged into pinned memory, H2D, seeding, D2H of
+every interval into pinned memory, several workers overlapping) -- reported
+beside `value`, never as it.  --config c3/c4/c5 stream the north_star's
+target sizes (12.5M pairs = one GPU's shard of C3's 100M pairs, 10M x 250 bp,
+10M x 150 bp at 5 %); `value` stays the device-resident rate on a 1M-read
+batch of the same reads.
+
+roofline: dominant kernel = seed_kernel.  achieved = algorithmic bytes per
 launch (64 B x distinct Occ buckets per extend + read length
 + 32 B x intervals out, counted by the CPU oracle on a sample of the same
-reads) / the kernel's HIP-event duration measured here; achieved_occ64 is the
-same with the 32-B buckets of this build's index layout; traffic is the
-per-launch FETCH_SIZE recorded by tools/pmc_passes.sh for this workload.
+reads) / the kernel's HIP-event duration measured here; frac_occ64 does the
+same with the 32-B buckets this build actually reads.  The kernel is bound by
+random-request rate, not bytes: request_roofline compares its L2 fabric read
+requests per second (rocprofv3 TCC_EA0_RDREQ recorded by tools/traffic.py for
+this build and workload) with the random-gather ceiling measured on this GPU
+(tools/gather_ceiling.hip, profiles/r02/gather_ceiling.json).
 
 cpu_baseline: the reference's own C (oracle/_ref/ref_harness, compiled from
 the reference sources) when present, else the C restatement, timed on this
-host's cores on a bounded sample of the same reads, rank 0 only.
+host's physical cores on a bounded sample of the same reads, rank 0 only.
 """
 from __future__ import annotations
 
@@ -48,63 +60,126 @@ sys.path.insert(0, ROOT)
 
 METRIC = "SMEM reads/sec on human_g1k_v37 150bp at 1/2/4/8 MI355X; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+HUMAN_MBP = 3101.804739  # human_g1k_v37 l_pac
+BLOCK = 1 << 18          # reads per block of the read stream (shards are whole blocks)
+
+# BASELINE.json configs: per-GPU shapes
+CONFIGS = {
+    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=0,
+               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1])"),
+    "c3": dict(read_len=150, sub=0.02, k=19, pairs=True, stream_reads=25_000_000,
+               what="C3 on one GPU: its shard of 100M x 150 bp PE on 8 GPUs = 12.5M pairs, insert N(500, 50), "
+                    "mates interleaved in one chunk"),
+    "c4": dict(read_len=250, sub=0.02, k=19, pairs=False, stream_reads=10_000_000,
+               what="C4: 10M x 250 bp, min-seed-len 19 with re-seeding"),
+    "c5": dict(read_len=150, sub=0.05, k=19, pairs=False, stream_reads=10_000_000,
+               what="C5: 10M x 150 bp at 5 % substitutions"),
+}
 
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
-    p.add_argument("--read-len", type=int, default=150)
-    p.add_argument("--sub", type=float, default=0.02)
-    p.add_argument("--genome-mbp", type=float, default=3101.804739,
+    p.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    p.add_argument("--reads", type=int, default=1_000_000, help="resident reads per GPU (the metric's batch)")
+    p.add_argument("--read-len", type=int, default=None)
+    p.add_argument("--sub", type=float, default=None)
+    p.add_argument("--genome-mbp", type=float, default=HUMAN_MBP,
                    help="synthetic genome size; default = human_g1k_v37 l_pac (6.2 G symbols with its reverse complement)")
+    p.add_argument("--genome-profile", choices=["uniform", "human"], default="uniform",
+                   help="uniform: random + 2 %% repeat families; human: ~46 %% interspersed repeats + satellites")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu", help="index construction (same bytes)")
     p.add_argument("--lanes-per-cu", type=int, default=0)
     p.add_argument("--streams", type=int, default=2, help="host workers, each with its own batch and HIP stream")
+    p.add_argument("--stream-reads", type=int, default=None,
+                   help="reads per GPU pushed through the streaming path (default: the config's; c2: the resident reads)")
+    p.add_argument("--stream-chunk", type=int, default=1 << 17)
+    p.add_argument("--stream-workers", type=int, default=4)
+    p.add_argument("--stream-packed", type=int, default=1, help="1: 16-B wire entries (SMEM_STREAM_PACKED)")
+    p.add_argument("--side-stages", type=int, default=1, help="0: skip the sa / chain / sw side reports")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--stats-sample", type=int, default=20000, help="reads counted by the oracle for bytes/read")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                   help="per-launch FETCH_SIZE bytes measured by rocprofv3 --pmc for this workload")
-    return p.parse_args()
+                   help="per-launch TCC_EA0_RDREQ / FETCH_SIZE recorded by tools/traffic.py for this build + workload")
+    p.add_argument("--ceiling-json", default=os.path.join(ROOT, "profiles", "r02", "gather_ceiling.json"))
+    a = p.parse_args(argv)
+    cfg = CONFIGS[a.config]
+    a.read_len = a.read_len or cfg["read_len"]
+    a.sub = cfg["sub"] if a.sub is None else a.sub
+    a.min_seed_len = cfg["k"]
+    a.pairs = cfg["pairs"]
+    if a.stream_reads is None:
+        a.stream_reads = cfg["stream_reads"]
+    return a
 
 
-def get_index(args, rank, world, barrier, device=0):
-    import smemgpu
-    from smemgpu import synth
-    os.makedirs(args.cache, exist_ok=True)
+def genome_key(args) -> str:
     n_bp = int(args.genome_mbp * 1e6)
-    key = os.path.join(args.cache, f"genome_{n_bp}_{args.seed}.bwt")
-    skey = key[:-4] + ".sa"
-    if rank == 0 and not (os.path.exists(key) and os.path.exists(skey)):
+    prof = "" if args.genome_profile == "uniform" else "_human"
+    return os.path.join(args.cache, f"genome_{n_bp}_{args.seed}{prof}")
+
+
+def make_genome(args):
+    from smemgpu import synth
+    n_bp = int(args.genome_mbp * 1e6)
+    if args.genome_profile == "human":
+        return synth.make_genome_human_like(n_bp, seed=args.seed, n_chrom=24)
+    return synth.make_genome(n_bp, seed=args.seed, n_chrom=24)
+
+
+def get_index(args, rank, barrier, device=0):
+    """Index (+ .sa) and the genome codes, built once per host by rank 0 and
+    cached; every rank then reads them (the genome through a memory map, so
+    no rank regenerates it)."""
+    import smemgpu
+    os.makedirs(args.cache, exist_ok=True)
+    base = genome_key(args)
+    key, skey, gkey = base + ".bwt", base + ".sa", base + ".codes"
+    if rank == 0 and not all(os.path.exists(k) for k in (key, skey, gkey)):
         t = time.time()
-        g = synth.make_genome(n_bp, seed=args.seed, n_chrom=24)
+        g = make_genome(args)
         idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32, gpu=args.builder == "gpu", device=device)
         idx.write(key + ".tmp")
         sa.write(skey + ".tmp")
-        os.replace(key + ".tmp", key)
-        os.replace(skey + ".tmp", skey)
+        g.codes.tofile(gkey + ".tmp")
+        for k in (key, skey, gkey):
+            os.replace(k + ".tmp", k)
         del g
-        log(f"index built ({args.builder}): {n_bp} bp genome, {idx.words.nbytes / 1e6:.1f} MB .bwt + "
+        log(f"index built ({args.builder}, {args.genome_profile}): {idx.words.nbytes / 1e6:.1f} MB .bwt + "
             f"{sa.samples.nbytes / 1e6:.1f} MB .sa in {time.time() - t:.1f} s")
     barrier()
-    return smemgpu.Index.read(key), key, smemgpu.SA.read(skey)
+    codes = np.memmap(gkey, dtype=np.uint8, mode="r")
+    return smemgpu.Index.read(key), key, smemgpu.SA.read(skey), codes
 
 
-def make_reads(args, rank, genome_codes=None):
+def shard_blocks(n_reads: int, rank: int, world: int, block: int = BLOCK) -> list:
+    """The blocks of the read stream rank `rank` seeds: ceil(n_reads / block)
+    blocks per rank, dealt round-robin (block b goes to rank b % world)."""
+    per = (n_reads + block - 1) // block
+    return [rank + world * k for k in range(per)]
+
+
+def make_reads(args, rank, genome_codes, world: int = 1, n_reads: int | None = None, salt: int = 0):
+    """This rank's shard of the read stream: n_reads (default --reads) reads
+    in whole blocks (the last one cut), blocks dealt round-robin over the
+    ranks, so the shards reassembled in block order are the single-rank
+    stream of the same total."""
     from smemgpu import synth
-    if genome_codes is None:
-        genome_codes = synth.make_genome(int(args.genome_mbp * 1e6), seed=args.seed, n_chrom=24).codes
-    # seeds differ per rank: each GPU gets its own shard of the read set
-    return synth.make_reads(genome_codes, args.reads, args.read_len, seed=1000 + args.seed * 7919 + rank,
-                            sub_rate=args.sub, n_rate=0.001)
+    n = args.reads if n_reads is None else n_reads
+    block = getattr(args, "block", BLOCK)
+    blocks = shard_blocks(n, rank, world, block)
+    kw = dict(sub_rate=args.sub, n_rate=0.001)
+    r = synth.make_read_blocks(np.asarray(genome_codes), blocks, block, args.read_len,
+                               seed=1000 + args.seed * 7919 + salt, pairs=bool(getattr(args, "pairs", False)), **kw)
+    return r.subset(np.arange(n)) if r.n > n else r
 
 
 def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
@@ -126,7 +201,8 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
     oi = oracle.OracleIndex(words=idx.words, primary=idx.primary, L2=idx.L2)
     n = min(reads.n, args.stats_sample)
     s = reads.subset(np.arange(n))
-    want, per, st = oracle.seed(oi, s.codes, s.offs, threads=min(16, os.cpu_count() or 1))
+    want, per, st = oracle.seed(oi, s.codes, s.offs, threads=min(16, os.cpu_count() or 1),
+                                min_seed_len=opt.min_seed_len)
     bpr = float(per["bytes"].mean())
     b64 = (32.0 * st["n_bkt64"] + st["n_bases"] + 32.0 * st["n_intv"]) / max(n, 1)
     b = gpu.batch(s.n, int(s.codes.size), int(s.lens.max()))
@@ -142,7 +218,7 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
     if args.cpu_seconds > 0:
         # calibrate on a small slice, then size the sample for ~cpu_seconds
         cal = reads.subset(np.arange(min(reads.n, 2000)))
-        t, _ = oracle.seed_timed(oi, cal.codes, cal.offs, threads=cores)
+        t, _ = oracle.seed_timed(oi, cal.codes, cal.offs, threads=cores, min_seed_len=opt.min_seed_len)
         rate = cal.n / max(t, 1e-6)
         m = int(min(reads.n, max(cal.n, rate * args.cpu_seconds)))
         sample = reads.subset(np.arange(m))
@@ -151,15 +227,15 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
             with tempfile.TemporaryDirectory() as d:
                 p = os.path.join(d, "s.smrd")
                 synth.write_smrd(p, sample)
-                r = oracle.ref_bench(idx_path, p, cores, m)
+                r = oracle.ref_bench(idx_path, p, cores, m, min_seed_len=opt.min_seed_len)
                 secs, kind = r["seconds"], "reference"
         else:
-            secs, _ = oracle.seed_timed(oi, sample.codes, sample.offs, threads=cores)
+            secs, _ = oracle.seed_timed(oi, sample.codes, sample.offs, threads=cores, min_seed_len=opt.min_seed_len)
         cpu = {"value": round(m / secs, 1), "unit": "reads/s", "cores": cores, "kind": kind,
                "host": cpu_inventory(),
                "per_core": round(m / secs / cores, 1),
                "sample": f"first {m} of the benchmark's {args.read_len} bp reads on rank 0, {secs:.1f} s wall, "
-                         f"{cores} pthreads"}
+                         f"{cores} pthreads (one per physical core)"}
     oi.close()
     sw = sw_cpu(sw_tasks) if (sw_tasks is not None and args.cpu_seconds > 0) else None
     return bpr, b64, st, n, parity, cpu, sw
@@ -209,18 +285,27 @@ def cpu_inventory() -> dict:
     return inv
 
 
-def traffic_for(args, path: str):
-    """Per-launch L2 fabric read bytes (rocprofv3 FETCH_SIZE) recorded for this
-    exact workload by tools/pmc_passes.sh, or None."""
+def traffic_for(args, path: str, build_id: str):
+    """Per-launch memory-side counters of seed_kernel recorded by
+    tools/traffic.py for this exact workload AND this library build, or None."""
     if not path or not os.path.exists(path):
         return None
     with open(path) as fh:
         t = json.load(fh)
     w = t.get("workload", {})
-    if (w.get("genome_mbp"), w.get("reads"), w.get("read_len"), w.get("seed")) != (
-            args.genome_mbp, args.reads, args.read_len, args.seed):
+    want = {"genome_mbp": args.genome_mbp, "reads": args.reads, "read_len": args.read_len, "seed": args.seed,
+            "sub": args.sub, "genome_profile": args.genome_profile}
+    if any(w.get(k) != v for k, v in want.items()) or t.get("build_id") != build_id:
         return None
-    return t.get("bytes_per_launch")
+    return t
+
+
+def gather_ceiling(path: str):
+    """The random 32-B-bucket gather ceiling measured on MI355X (requests/s)."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh)
 
 
 class Dist:
@@ -284,18 +369,29 @@ def aggregate(d: Dist, elapsed: float, reads_per_rank: int, steps: int):
     return total / elapsed_max, elapsed_max
 
 
-def pcie_inclusive(batch, reads, opt, reps: int = 2) -> float:
-    """reads/s including H2D of the reads and D2H of the results (not `value`)."""
-    import torch
-    best = float("inf")
-    for _ in range(reps):
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        batch.set_reads(reads.codes, reads.offs)
-        batch.run(opt)
-        batch.fetch()
-        best = min(best, time.perf_counter() - t)
-    return reads.n / best
+def streaming_report(gpu, reads, opt, args, resident_rate: float) -> dict:
+    """bwa mem's chunk loop over host buffers (smem_gpu_seed_stream): chunks
+    staged into pinned memory, H2D, seeding + compaction, every interval D2H
+    into pinned memory; workers overlap.  One warm pass (buffer creation) is
+    not timed."""
+    chunk = min(args.stream_chunk, max(2, reads.n))
+    # warm pass: creates the pooled worker batches (device buffers, ~1 GB of
+    # pinned result memory each) outside the timed pass
+    pk = bool(args.stream_packed)
+    warm = reads.subset(np.arange(min(reads.n, chunk * args.stream_workers)))
+    gpu.seed_stream(warm.codes, warm.offs, opt, chunk_reads=chunk, workers=args.stream_workers, pairs=args.pairs,
+                    packed=pk)
+    st, _ = gpu.seed_stream(reads.codes, reads.offs, opt, chunk_reads=chunk, workers=args.stream_workers,
+                            pairs=args.pairs, packed=pk)
+    rate = st["n_reads"] / st["wall_s"]
+    return {"reads": int(st["n_reads"]), "reads_per_s": round(rate, 1), "wall_s": round(st["wall_s"], 3),
+            "chunk_reads": chunk, "workers": int(st["workers"]), "chunks": int(st["n_chunks"]),
+            "h2d_GB": round(st["h2d_bytes"] / 1e9, 3), "d2h_GB": round(st["d2h_bytes"] / 1e9, 3),
+            "intervals": int(st["n_intv"]), "packed": pk,
+            "ratio_to_resident": round(rate / resident_rate, 3) if resident_rate else None,
+            "what": "PCIe-inclusive: host reads -> pinned staging -> H2D -> seed_kernel + compaction -> D2H of every "
+                    "interval into pinned host memory (smem_gpu_seed_stream, kt_for_batch-style workers; packed: "
+                    "16-B smem_pintv_t wire entries)"}
 
 
 def sa_lookup(batch, opt, reps: int = 3) -> dict:
@@ -371,21 +467,60 @@ def sw_cpu(kb) -> dict:
             "sample": f"{kb.tasks.size} problems, {secs:.2f} s incl. file I/O"}
 
 
+def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id) -> dict:
+    achieved = bpr * reads_n / (k_ms * 1e-3) / 1e9
+    out = {
+        "bound": "hbm",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": "seed_kernel",
+        "kernel_ms": round(k_ms, 3),
+        "kernel_ms_source": "HIP events on each worker's stream around every seed_kernel launch of the timed region "
+                            "(mean); with --streams > 1 two workers' launches overlap on the GPU, so a launch lasts "
+                            "longer than ms_per_step",
+        "kernel_ms_alone": round(a_ms, 3),
+        "frac_alone": round(bpr * reads_n / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "bytes_per_read": round(bpr, 1),
+        "bytes_per_read_occ64": round(bpr64, 1),
+        "achieved_occ64": round(bpr64 * reads_n / (a_ms * 1e-3) / 1e9, 2),
+        "frac_occ64": round(bpr64 * reads_n / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "bytes_per_read_sample": n_counted,
+        "extends_per_read": round(ostats["n_ext"] / max(n_counted, 1), 1),
+        "occ64_buckets_per_read": round(ostats["n_bkt64"] / max(n_counted, 1), 1),
+    }
+    t = traffic_for(args, args.traffic_json, build_id)
+    if t:
+        rq = float(t["rdreq_per_launch"])
+        out["traffic"] = round(rq * 64.0, 1)   # one 64-B line per fabric read request (FETCH_SIZE calibration)
+        out["traffic_note"] = ("TCC_EA0_RDREQ x 64 B per launch (tools/traffic.py, " + t.get("measured", "?") +
+                               "): each random 16/32-B chunk request moves one 64-B line -- FETCH_SIZE = 64 B x "
+                               "requests, calibrated on known random 16-B and 32-B gathers (profiles/r02/probe)")
+        out["traffic_over_occ64_bytes"] = round(rq * 64.0 / (bpr64 * reads_n), 3)
+        out["dram_GBps"] = round(rq * 64.0 / (a_ms * 1e-3) / 1e9, 1)
+        c = gather_ceiling(args.ceiling_json)
+        if c:
+            rate = rq / (a_ms * 1e-3)
+            out["request_roofline"] = {
+                "requests_per_launch": int(rq), "achieved_Greq_per_s": round(rate / 1e9, 2),
+                "ceiling_Greq_per_s": c["occ64_3p1gb_Greq_per_s"], "frac": round(rate / 1e9 / c["occ64_3p1gb_Greq_per_s"], 3),
+                "ceiling_source": c["source"]}
+    return out
+
+
 def main():
     args = parse()
     import torch
     import smemgpu
 
     d = Dist()
-    rank, world, local = d.rank, d.world, d.local
+    rank, world = d.rank, d.world
     barrier = d.barrier
 
-    idx, idx_path, sa = get_index(args, rank, world, barrier, d.gpu)
-    genome_codes = None
-    if rank == 0:
-        from smemgpu import synth
-        genome_codes = synth.make_genome(int(args.genome_mbp * 1e6), seed=args.seed, n_chrom=24).codes
-    reads = make_reads(args, rank, genome_codes)
+    idx, idx_path, sa, genome_codes = get_index(args, rank, barrier, d.gpu)
+    reads = make_reads(args, rank, genome_codes, world)
     gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu)
     gpu.load_sa(sa)
     # one batch object (own HIP stream, own buffers) per host worker, each
@@ -398,10 +533,11 @@ def main():
     batch = batches[0]
     torch.cuda.synchronize()
 
-    opt = smemgpu.Options()
+    opt = smemgpu.Options(min_seed_len=args.min_seed_len)
     # warmup; launches that run alone on the GPU (no other stream's kernels
     # beside them) give kernel_ms_alone
     alone_ms = []
+    compact_alone = 0.0
     for w in range(max(args.warmup, 2)):
         batch.run(opt)
         if w > 0:
@@ -447,11 +583,24 @@ def main():
     elapsed = time.perf_counter() - t0
     st = batch.stats()
     value, elapsed_max = aggregate(d, elapsed, reads.n, args.steps)
-    pcie = pcie_inclusive(batch, reads, opt) if rank == 0 else None
-    sa_rep = sa_lookup(batch, opt) if rank == 0 else None
-    chain_rep = chain_report(batch, opt, idx.seq_len // 2) if rank == 0 else None
-    sw_rep, sw_tasks = sw_report(gpu, genome_codes) if rank == 0 else (None, None)
-    del genome_codes
+    for b in batches[1:]:
+        b.close()
+    batches = [batch]
+
+    # streaming (PCIe-inclusive) on every rank, then its aggregate; the
+    # config's target read count, or the resident reads (c2)
+    sreads = reads if args.stream_reads <= 0 else make_reads(args, rank, genome_codes, world, args.stream_reads, salt=1)
+    barrier()
+    srep = streaming_report(gpu, sreads, opt, args, value / world)
+    s_rate = d.allsum(float(srep["reads"])) / d.allmax(srep["wall_s"])
+    srep["reads_per_s_all_ranks"] = round(s_rate, 1)
+    del sreads
+
+    sa_rep = chain_rep = sw_rep = sw_tasks = None
+    if rank == 0 and args.side_stages:
+        sa_rep = sa_lookup(batch, opt)
+        chain_rep = chain_report(batch, opt, idx.seq_len // 2)
+        sw_rep, sw_tasks = sw_report(gpu, np.asarray(genome_codes))
 
     if rank == 0:
         inv = cpu_inventory()
@@ -462,8 +611,7 @@ def main():
             sw_rep["cpu_baseline"] = sw_cpu_rep
         k_ms = float(np.mean(kernel_ms))
         a_ms = float(np.mean(alone_ms))
-        achieved = bpr * reads.n / (k_ms * 1e-3) / 1e9
-        traffic = traffic_for(args, args.traffic_json)
+        cfg = CONFIGS[args.config]
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -478,40 +626,28 @@ def main():
             "dtype": "u64",
             "data": "synthetic",
             "config": {
-                "workload": f"synthetic {args.genome_mbp:g} Mbp genome index in HBM (stand-in for human_g1k_v37), "
-                            f"{reads.n} x {args.read_len} bp SE reads per GPU, {args.sub:.0%} subs, 0.1% N, "
-                            f"k=19 r=1.5 s=10",
+                "workload": f"{args.config}: synthetic {args.genome_mbp:g} Mbp genome index in HBM "
+                            f"({args.genome_profile} repeat profile; stand-in for human_g1k_v37), "
+                            f"{reads.n} x {args.read_len} bp {'PE (interleaved mates)' if args.pairs else 'SE'} reads "
+                            f"resident per GPU, {args.sub:.0%} subs, 0.1% N, k={args.min_seed_len} r=1.5 s=10",
+                "config": args.config,
+                "config_what": cfg["what"],
+                "genome_profile": args.genome_profile,
                 "reads_per_gpu": reads.n,
                 "read_len": args.read_len,
                 "genome_bp": int(args.genome_mbp * 1e6),
                 "index_bytes": int(idx.words.nbytes),
-                "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collectives; "
-                               f"{len(batches)} host workers per GPU, each running whole steps on its own stream",
+                "seed": args.seed,
+                "parallelism": f"reads sharded over {world} GPU(s) in blocks of {BLOCK} dealt round-robin, index "
+                               f"replicated, no collectives; {args.streams} host workers per GPU, each running whole "
+                               f"steps on its own stream",
                 "grid": st["grid"], "block": st["block"],
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "seed_kernel",
-                "kernel_ms": round(k_ms, 3),
-                "kernel_ms_source": "HIP events on each worker's stream around every seed_kernel launch of the "
-                                    "timed region (mean)",
-                "kernel_ms_alone": round(a_ms, 3),
-                "frac_alone": round(bpr * reads.n / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "bytes_per_read": round(bpr, 1),
-                "bytes_per_read_occ64": round(bpr64, 1),
-                "achieved_occ64": round(bpr64 * reads.n / (k_ms * 1e-3) / 1e9, 2),
-                "bytes_per_read_sample": n_counted,
-                "extends_per_read": round(ostats["n_ext"] / max(n_counted, 1), 1),
-            },
+            "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, k_ms, a_ms, smemgpu.build_id()),
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "compact_ms": round(compact_alone, 3),
-            "pcie_inclusive_reads_per_s": round(pcie, 1),
+            "streaming": srep,
             "sa_lookup": sa_rep,
             "chaining": chain_rep,
             "sw_extension": sw_rep,

@@ -12,6 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -115,6 +118,9 @@ struct smem_gpu {
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
     std::mutex mu;
     std::unordered_map<std::thread::id, smem_batch_t*> per_thread;
+    // smem_gpu_seed_stream's worker batches, kept between calls: creating one
+    // pins ~1 GB of host memory and allocates its device buffers
+    std::vector<smem_batch_t*> stream_pool;
 };
 
 struct smem_batch {
@@ -151,7 +157,10 @@ struct smem_batch {
     DevBuf<uint32_t> d_flat_calls;
     HostBuf<int32_t> h_ctr;
     HostBuf<uint64_t> h_tot;
-    // fetched results
+    // fetched results (packed: 16-B smem_pintv_t wire entries instead of h_intv)
+    bool packed = false;
+    DevBuf<uint4> d_pintv;
+    HostBuf<uint4> h_pintv;
     HostBuf<Intv> h_intv;
     HostBuf<uint32_t> h_calls;
     HostBuf<uint64_t> h_intv_off, h_call_off;
@@ -314,6 +323,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release(); b->d_heavy.release();
     b->h_chain_off.release(); b->h_out_chain.release(); b->h_out_seed.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
+    b->d_pintv.release(); b->h_pintv.release();
     b->h_intv_off.release(); b->h_call_off.release();
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -326,6 +336,8 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     (void)hipSetDevice(g->device);
     for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
     g->per_thread.clear();
+    for (auto* b : g->stream_pool) smem_batch_destroy(b);
+    g->stream_pool.clear();
     if (g->d_bwt) (void)hipFree(g->d_bwt);
     if (g->d_occ64) (void)hipFree(g->d_occ64);
     if (g->d_occ192) (void)hipFree(g->d_occ192);
@@ -597,12 +609,26 @@ int smem_batch_fetch(smem_batch_t* b) {
     if (!b || !b->ran) return fail(SMEM_E_ARG, "smem_batch_fetch: batch has not run");
     HIP_TRY(hipSetDevice(b->g->device));
     const int n = b->n_reads;
-    HIP_TRY(b->h_intv.ensure(std::max<uint64_t>(b->tot_intv, 1)));
-    HIP_TRY(b->h_calls.ensure(std::max<uint64_t>(b->tot_calls, 1)));
+    // pinned result buffers grow with headroom: a streamed batch whose next
+    // chunk holds a few more intervals must not re-pin a gigabyte
+    if (b->packed) {
+        if (b->d_pintv.n < b->tot_intv || !b->d_pintv.p)
+            HIP_TRY(b->d_pintv.ensure(std::max<uint64_t>(b->tot_intv + b->tot_intv / 4, 1)));
+        if (b->h_pintv.n < b->tot_intv || !b->h_pintv.p)
+            HIP_TRY(b->h_pintv.ensure(std::max<uint64_t>(b->tot_intv + b->tot_intv / 4, 1)));
+    } else if (b->h_intv.n < b->tot_intv || !b->h_intv.p) {
+        HIP_TRY(b->h_intv.ensure(std::max<uint64_t>(b->tot_intv + b->tot_intv / 4, 1)));
+    }
+    if (b->h_calls.n < b->tot_calls || !b->h_calls.p)
+        HIP_TRY(b->h_calls.ensure(std::max<uint64_t>(b->tot_calls + b->tot_calls / 4, 1)));
     HIP_TRY(hipMemcpyAsync(b->h_intv_off.p, b->d_intv_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
     HIP_TRY(hipMemcpyAsync(b->h_call_off.p, b->d_call_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
-    if (b->tot_intv)
+    if (b->tot_intv && b->packed) {
+        HIP_TRY(smem_launch_pack_intv(b->d_flat_intv.p, b->tot_intv, b->d_pintv.p, b->st));
+        HIP_TRY(hipMemcpyAsync(b->h_pintv.p, b->d_pintv.p, sizeof(uint4) * b->tot_intv, hipMemcpyDeviceToHost, b->st));
+    } else if (b->tot_intv) {
         HIP_TRY(hipMemcpyAsync(b->h_intv.p, b->d_flat_intv.p, sizeof(Intv) * b->tot_intv, hipMemcpyDeviceToHost, b->st));
+    }
     if (b->tot_calls)
         HIP_TRY(hipMemcpyAsync(b->h_calls.p, b->d_flat_calls.p, sizeof(uint32_t) * b->tot_calls, hipMemcpyDeviceToHost, b->st));
     if (b->sa_ran) {
@@ -862,7 +888,7 @@ int smem_batch_sa_results(const smem_batch_t* b, const uint64_t** pos, const uin
 
 int smem_batch_read(const smem_batch_t* b, int i, const smem_intv_t** intv, int* n_intv, const uint32_t** call_n,
                     int* n_calls) {
-    if (!b || !b->fetched || i < 0 || i >= b->n_reads) return SMEM_E_ARG;
+    if (!b || !b->fetched || b->packed || i < 0 || i >= b->n_reads) return SMEM_E_ARG;
     const uint64_t o = b->h_intv_off.p[i], co = b->h_call_off.p[i];
     if (intv) *intv = reinterpret_cast<const smem_intv_t*>(b->h_intv.p + o);
     if (n_intv) *n_intv = (int)(b->h_intv_off.p[i + 1] - o);
@@ -871,9 +897,19 @@ int smem_batch_read(const smem_batch_t* b, int i, const smem_intv_t** intv, int*
     return SMEM_OK;
 }
 
+int smem_batch_results_packed(const smem_batch_t* b, const smem_pintv_t** pintv, const uint64_t** intv_off,
+                              const uint32_t** call_n, const uint64_t** call_off) {
+    if (!b || !b->fetched || !b->packed) return SMEM_E_ARG;
+    if (pintv) *pintv = reinterpret_cast<const smem_pintv_t*>(b->h_pintv.p);
+    if (intv_off) *intv_off = b->h_intv_off.p;
+    if (call_n) *call_n = b->h_calls.p;
+    if (call_off) *call_off = b->h_call_off.p;
+    return SMEM_OK;
+}
+
 int smem_batch_results(const smem_batch_t* b, const smem_intv_t** intv, const uint64_t** intv_off,
                        const uint32_t** call_n, const uint64_t** call_off) {
-    if (!b || !b->fetched) return SMEM_E_ARG;
+    if (!b || !b->fetched || b->packed) return SMEM_E_ARG;
     if (intv) *intv = reinterpret_cast<const smem_intv_t*>(b->h_intv.p);
     if (intv_off) *intv_off = b->h_intv_off.p;
     if (call_n) *call_n = b->h_calls.p;
@@ -1110,6 +1146,125 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
 int smem_batch_stats(const smem_batch_t* b, smem_batch_stats_t* st) {
     if (!b || !st) return SMEM_E_ARG;
     *st = b->stats;
+    return SMEM_OK;
+}
+
+// ---- streaming: bwa mem's chunk loop (software/fastmap.c:213-228) with its
+// kt_for_batch workers (software/kthread_batch.c:29-59) over one device.
+// Each worker owns a batch (pinned staging, HIP stream, device buffers) and
+// runs whole chunks: stage + H2D, seed + compact, D2H into pinned memory,
+// then the caller's callback.  The workers' chunks interleave on the device,
+// so one chunk's copies overlap another's kernels.
+int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, const uint64_t* offs,
+                         const smem_opt_t* opt, int chunk_reads, int n_workers, int flags, smem_chunk_fn fn, void* ctx,
+                         smem_stream_stats_t* stats) {
+    g_err[0] = 0;
+    if (!g || !opt || n_reads < 0 || (n_reads > 0 && (!codes || !offs)) || chunk_reads <= 0 || n_workers <= 0 ||
+        n_workers > 64 || (flags & ~(SMEM_STREAM_PAIRS | SMEM_STREAM_PACKED)))
+        return fail(SMEM_E_ARG, "smem_gpu_seed_stream: bad arguments");
+    const bool pairs = flags & SMEM_STREAM_PAIRS, packed = flags & SMEM_STREAM_PACKED;
+    if (pairs) {
+        if (n_reads & 1) return fail(SMEM_E_ARG, "smem_gpu_seed_stream: pairs need an even read count");
+        chunk_reads = std::max(2, chunk_reads & ~1);  // both mates of a pair in one chunk (software/bwamem.c:1600-1609)
+    }
+    const int64_t n_chunks = (n_reads + chunk_reads - 1) / chunk_reads;
+    // the largest chunk: reads, bases, read length
+    int max_len = 1;
+    uint64_t max_bases = 1;
+    for (int64_t c = 0; c < n_chunks; ++c) {
+        const int64_t a = c * chunk_reads, e = std::min<int64_t>(n_reads, a + chunk_reads);
+        if (offs[e] < offs[a]) return fail(SMEM_E_ARG, "smem_gpu_seed_stream: offsets not ascending");
+        max_bases = std::max<uint64_t>(max_bases, offs[e] - offs[a]);
+    }
+    for (int64_t r = 0; r < n_reads; ++r) {
+        if (offs[r + 1] < offs[r]) return fail(SMEM_E_ARG, "smem_gpu_seed_stream: offsets not ascending");
+        max_len = std::max<int>(max_len, (int)std::min<uint64_t>(offs[r + 1] - offs[r], 1u << 24));
+    }
+    if (packed && max_len > SMEM_PINTV_MAX_LEN)
+        return fail(SMEM_E_ARG, "smem_gpu_seed_stream: packed entries hold reads up to 8191 bp");
+    const int nw = (int)std::max<int64_t>(1, std::min<int64_t>(n_workers, n_chunks));
+    const int want_reads = (int)std::min<int64_t>(chunk_reads, std::max<int64_t>(n_reads, 1));
+    std::vector<smem_batch_t*> bs(nw, nullptr);
+    int rc = SMEM_OK;
+    {
+        // reuse pooled batches that are large enough (one stream at a time per pool entry)
+        std::lock_guard<std::mutex> lk(g->mu);
+        for (int w = 0; w < nw; ++w) {
+            for (size_t k = 0; k < g->stream_pool.size(); ++k) {
+                smem_batch_t* c = g->stream_pool[k];
+                if (c->max_reads >= want_reads && c->max_bases >= max_bases && c->max_len >= max_len) {
+                    bs[w] = c;
+                    g->stream_pool.erase(g->stream_pool.begin() + (long)k);
+                    break;
+                }
+            }
+        }
+    }
+    for (int w = 0; w < nw && rc == SMEM_OK; ++w)
+        if (!bs[w]) rc = smem_batch_create(g, want_reads, max_bases, max_len, &bs[w]);
+    std::atomic<int64_t> next{0};
+    std::atomic<int> err{SMEM_OK};
+    std::atomic<uint64_t> n_intv{0}, h2d{0}, d2h{0};
+    std::mutex emu;
+    std::string emsg;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto worker = [&](int w) {
+        smem_batch_t* b = bs[w];
+        b->packed = packed;
+        for (;;) {
+            const int64_t c = next.fetch_add(1);
+            if (c >= n_chunks || err.load() != SMEM_OK) break;
+            const int64_t a = c * chunk_reads, e = std::min<int64_t>(n_reads, a + chunk_reads);
+            const int n = (int)(e - a);
+            int r = smem_batch_set_reads_packed(b, n, codes, offs + a);
+            if (!r) r = smem_batch_run(b, opt);
+            if (!r) r = smem_batch_fetch(b);
+            if (!r) {
+                n_intv += b->tot_intv;
+                h2d += (offs[e] - offs[a]) + 8ull * (uint64_t)(n + 1);
+                d2h += (packed ? 16ull : sizeof(Intv)) * b->tot_intv + 4ull * b->tot_calls + 16ull * (uint64_t)(n + 1);
+                if (fn) r = fn(ctx, c, a, n, b);
+            }
+            if (r) {
+                int expect = SMEM_OK;
+                if (err.compare_exchange_strong(expect, r)) {
+                    std::lock_guard<std::mutex> lk(emu);
+                    emsg = g_err;
+                }
+                break;
+            }
+        }
+    };
+    if (rc == SMEM_OK) {
+        std::vector<std::thread> th;
+        for (int w = 1; w < nw; ++w) th.emplace_back(worker, w);
+        worker(0);
+        for (auto& t : th) t.join();
+        rc = err.load();
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        for (auto* b : bs)
+            if (b) {
+                b->packed = false;
+                if (rc == SMEM_OK && g->stream_pool.size() < 16) g->stream_pool.push_back(b);
+                else smem_batch_destroy(b);
+            }
+    }
+    if (rc != SMEM_OK) {
+        if (!emsg.empty()) snprintf(g_err, sizeof(g_err), "smem_gpu_seed_stream: %s", emsg.c_str());
+        return rc;
+    }
+    if (stats) {
+        stats->wall_s = secs;
+        stats->n_reads = (uint64_t)n_reads;
+        stats->n_chunks = (uint64_t)n_chunks;
+        stats->n_intv = n_intv.load();
+        stats->h2d_bytes = h2d.load();
+        stats->d2h_bytes = d2h.load();
+        stats->workers = nw;
+    }
     return SMEM_OK;
 }
 

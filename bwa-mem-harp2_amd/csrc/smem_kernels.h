@@ -98,6 +98,7 @@ hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32
 hipError_t smem_launch_occ192(const uint32_t* occ64, uint64_t n_blocks, uint32_t* out, hipStream_t st);
 hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int write, hipStream_t st);
 hipError_t smem_launch_fill_i32(int32_t* p, int32_t v, int n, hipStream_t st);
+hipError_t smem_launch_pack_intv(const smem::Intv* in, uint64_t n, uint4* out, hipStream_t st);
 hipError_t smem_launch_ovf_slot(const int32_t* items, int n_ovf, int32_t* ovf_slot, hipStream_t st);
 hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t st);
 hipError_t smem_launch_sa_densify(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense, uint64_t* dense,

@@ -1060,6 +1060,27 @@ extern "C" hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int wr
     return hipGetLastError();
 }
 
+namespace smem {
+// flat bwtintv_t (32 B) -> the 16-B wire entry smem_pintv_t (include/smem_gpu.h):
+// x0, x1, x2 low words, then x0/x1/x2 bits 32-33 and the query begin / end
+// (13 bits each: reads < 8192 bp, checked on the host)
+__global__ __launch_bounds__(256) void pack_intv_kernel(const Intv* __restrict__ in, uint64_t n, uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const Intv v = in[i];
+    const uint32_t beg = (uint32_t)(v.info >> 32), end = (uint32_t)v.info;
+    out[i] = make_uint4((uint32_t)v.x0, (uint32_t)v.x1, (uint32_t)v.x2,
+                        (uint32_t)(v.x0 >> 32) | (uint32_t)(v.x1 >> 32) << 2 | (uint32_t)(v.x2 >> 32) << 4 | beg << 6 |
+                            end << 19);
+}
+}  // namespace smem
+
+extern "C" hipError_t smem_launch_pack_intv(const smem::Intv* in, uint64_t n, uint4* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(smem::pack_intv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, out);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t smem_launch_fill_i32(int32_t* p, int32_t v, int n, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(smem::fill_i32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p, v, n);

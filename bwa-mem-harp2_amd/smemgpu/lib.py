@@ -31,6 +31,7 @@ EXPORTED = [
     "smem_batch_sa", "smem_batch_sa_results",
     "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results", "smem_bwt_build_gpu_large",
     "smem_ksw_opt_default", "smem_ksw_extend", "smem_aln_opt_default", "smem_chain2aln",
+    "smem_gpu_seed_stream", "smem_batch_results_packed",
 ]
 
 
@@ -83,6 +84,16 @@ class BatchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
                 ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int),
                 ("sa_ms", C.c_double), ("n_occ", C.c_uint64), ("chain_ms", C.c_double), ("n_chains", C.c_uint64)]
+
+
+class StreamStats(C.Structure):
+    """smem_stream_stats_t"""
+    _fields_ = [("wall_s", C.c_double), ("n_reads", C.c_uint64), ("n_chunks", C.c_uint64), ("n_intv", C.c_uint64),
+                ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64), ("workers", C.c_int)]
+
+
+# int (*smem_chunk_fn)(void *ctx, int64_t chunk, int64_t first_read, int n_reads, const smem_batch_t *b)
+CHUNK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p)
 
 
 class KswOptT(C.Structure):
@@ -148,6 +159,10 @@ def load() -> C.CDLL:
     lib.smem_gpu_shutdown.argtypes = [C.c_void_p]
     lib.smem_gpu_shutdown.restype = None
     lib.smem_gpu_collect.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, P(OptT), P(C.c_void_p)]
+    lib.smem_gpu_seed_stream.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, P(OptT), C.c_int, C.c_int,
+                                         C.c_int, C.c_void_p, C.c_void_p, P(StreamStats)]
+    lib.smem_batch_results_packed.argtypes = [C.c_void_p, P(C.c_void_p), P(P(C.c_uint64)), P(P(C.c_uint32)),
+                                              P(P(C.c_uint64))]
     lib.smem_batch_create.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_int, P(C.c_void_p)]
     lib.smem_batch_destroy.argtypes = [C.c_void_p]
     lib.smem_batch_destroy.restype = None
@@ -393,6 +408,38 @@ class Gpu:
     def batch(self, max_reads: int, max_bases: int, max_len: int) -> "Batch":
         return Batch(self, max_reads, max_bases, max_len)
 
+    def seed_stream(self, codes: np.ndarray, offs: np.ndarray, opt: "Options" = None, chunk_reads: int = 1 << 20,
+                    workers: int = 3, pairs: bool = False, collect: bool = False, packed: bool = False) -> tuple:
+        """Stream a read set through smem_gpu_seed_stream (chunks of
+        chunk_reads, `workers` host workers each with its own batch and HIP
+        stream; packed: 16-B wire entries).  Returns (stats dict, per-chunk
+        Results in chunk order when collect else None)."""
+        lib = load()
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        o = (opt or Options()).c()
+        st = StreamStats()
+        got = {}
+        err = []
+
+        def on_chunk(ctx, chunk, first, n, bh):
+            try:
+                got[int(chunk)] = _results_of(lib, bh, n, packed)
+                return 0
+            except Exception as e:  # surfaced after the stream returns
+                err.append(e)
+                return -5
+
+        cb = CHUNK_FN(on_chunk) if collect else None
+        rc = lib.smem_gpu_seed_stream(self._h, offs.size - 1, codes.ctypes.data, offs.ctypes.data, C.byref(o),
+                                      int(chunk_reads), int(workers), (1 if pairs else 0) | (2 if packed else 0),
+                                      C.cast(cb, C.c_void_p) if cb else None, None, C.byref(st))
+        if err:
+            raise err[0]
+        _check(rc, "smem_gpu_seed_stream")
+        stats = {k: getattr(st, k) for k, _ in StreamStats._fields_}
+        return stats, ([got[k] for k in sorted(got)] if collect else None)
+
     def ksw_extend(self, kb) -> tuple:
         """ksw_extend2 (software/ksw.c:379) of every task of a synth.KswBatch on
         this device: (results as synth.KSW_RESULT, kernel ms)."""
@@ -494,19 +541,9 @@ class Batch:
     def fetch(self) -> Results:
         lib = load()
         _check(lib.smem_batch_fetch(self._h), "smem_batch_fetch")
-        iv = C.POINTER(Intv)()
-        io = C.POINTER(C.c_uint64)()
-        cn = C.POINTER(C.c_uint32)()
-        co = C.POINTER(C.c_uint64)()
-        _check(lib.smem_batch_results(self._h, C.byref(iv), C.byref(io), C.byref(cn), C.byref(co)), "smem_batch_results")
         n = int(self._keep[1].size - 1)
-        intv_off = np.ctypeslib.as_array(io, shape=(n + 1,)).copy()
-        call_off = np.ctypeslib.as_array(co, shape=(n + 1,)).copy()
-        ni, nc = int(intv_off[-1]), int(call_off[-1])
-        intv = (np.ctypeslib.as_array(C.cast(iv, C.POINTER(C.c_uint64)), shape=(max(ni, 1) * 4,))[:ni * 4]
-                .reshape(ni, 4).copy())
-        call_n = np.ctypeslib.as_array(cn, shape=(max(nc, 1),))[:nc].copy()
-        res = Results(intv, intv_off, call_n, call_off)
+        res = _results_of(lib, self._h, n)
+        ni = int(res.intv_off[-1])
         pos = C.POINTER(C.c_uint64)()
         oo = C.POINTER(C.c_uint64)()
         no = C.c_uint64()
@@ -537,6 +574,44 @@ class Batch:
             self.close()
         except Exception:
             pass
+
+
+def unpack_pintv(p: np.ndarray) -> np.ndarray:
+    """(N, 4) uint32 smem_pintv_t entries -> (N, 4) uint64 bwtintv_t (smem_pintv_unpack)."""
+    p = p.astype(np.uint64)
+    w = p[:, 3]
+    out = np.empty((p.shape[0], 4), dtype=np.uint64)
+    out[:, 0] = (w & np.uint64(3)) << np.uint64(32) | p[:, 0]
+    out[:, 1] = ((w >> np.uint64(2)) & np.uint64(3)) << np.uint64(32) | p[:, 1]
+    out[:, 2] = ((w >> np.uint64(4)) & np.uint64(3)) << np.uint64(32) | p[:, 2]
+    out[:, 3] = ((w >> np.uint64(6)) & np.uint64(8191)) << np.uint64(32) | (w >> np.uint64(19))
+    return out
+
+
+def _results_of(lib, bh, n: int, packed: bool = False) -> Results:
+    """Copies of a fetched batch's interval lists (smem_batch_results, or the
+    packed view unpacked)."""
+    iv = C.POINTER(Intv)()
+    pv = C.c_void_p()
+    io = C.POINTER(C.c_uint64)()
+    cn = C.POINTER(C.c_uint32)()
+    co = C.POINTER(C.c_uint64)()
+    if packed:
+        _check(lib.smem_batch_results_packed(bh, C.byref(pv), C.byref(io), C.byref(cn), C.byref(co)),
+               "smem_batch_results_packed")
+    else:
+        _check(lib.smem_batch_results(bh, C.byref(iv), C.byref(io), C.byref(cn), C.byref(co)), "smem_batch_results")
+    intv_off = np.ctypeslib.as_array(io, shape=(n + 1,)).copy()
+    call_off = np.ctypeslib.as_array(co, shape=(n + 1,)).copy()
+    ni, nc = int(intv_off[-1]), int(call_off[-1])
+    if packed:
+        raw = np.ctypeslib.as_array(C.cast(pv, C.POINTER(C.c_uint32)), shape=(max(ni, 1) * 4,))[:ni * 4]
+        intv = unpack_pintv(raw.reshape(ni, 4))
+    else:
+        intv = (np.ctypeslib.as_array(C.cast(iv, C.POINTER(C.c_uint64)), shape=(max(ni, 1) * 4,))[:ni * 4]
+                .reshape(ni, 4).copy())
+    call_n = np.ctypeslib.as_array(cn, shape=(max(nc, 1),))[:nc].copy()
+    return Results(intv, intv_off, call_n, call_off)
 
 
 def seed(gpu: Gpu, codes: np.ndarray, offs: np.ndarray, opt: Options = Options()) -> Results:

@@ -98,6 +98,101 @@ def make_genome(n_bp: int, seed: int = 1, n_chrom: int = 4, repeat_frac: float =
     return Genome(g, names, starts)
 
 
+# Repeat profile shaped like human_g1k_v37's (RepeatMasker classes, roughly):
+# (name, genome fraction, family length range, n families, divergence range,
+#  truncation: copies keep a random 3' part of at least this fraction)
+HUMAN_REPEATS = (
+    ("alu", 0.10, (280, 320), 40, (0.02, 0.18), 1.0),        # SINE: ~1.2 M copies of ~300 bp
+    ("l1", 0.17, (5500, 6500), 30, (0.03, 0.25), 0.1),       # LINE-1: mostly 5'-truncated
+    ("l2_mir", 0.05, (150, 3000), 200, (0.15, 0.30), 0.2),  # old LINE-2 / MIR
+    ("ltr", 0.08, (300, 8000), 300, (0.05, 0.25), 0.3),     # ERV / LTR elements
+    ("dna", 0.03, (200, 2500), 200, (0.10, 0.30), 0.3),     # DNA transposons
+)
+
+
+def _scatter_copies(g: np.ndarray, fam: np.ndarray, n_copies: int, div_lo: float, div_hi: float, trunc: float,
+                    rng: np.random.Generator) -> int:
+    """Write n_copies diverged (and 5'-truncated) copies of fam at random
+    positions of g, half of them reverse-complemented; vectorised per
+    family.  Returns the bases written."""
+    F = fam.size
+    n = g.size
+    if n_copies <= 0 or F >= n:
+        return 0
+    keep = np.maximum((F * (trunc + (1 - trunc) * rng.random(n_copies))).astype(np.int64), 1)
+    div = div_lo + (div_hi - div_lo) * rng.random(n_copies)
+    copies = np.broadcast_to(fam, (n_copies, F)).copy()
+    hit = rng.random((n_copies, F)) < div[:, None]
+    copies[hit] = (copies[hit] + rng.integers(1, 4, size=int(hit.sum()), dtype=np.uint8)) & 3
+    rc = rng.random(n_copies) < 0.5
+    copies[rc] = (3 - copies[rc])[:, ::-1]
+    starts = (rng.random(n_copies) * (n - F)).astype(np.int64)
+    # copy c keeps its last keep[c] bases (columns F-keep .. F-1 before the flip)
+    col = np.arange(F)[None, :]
+    mask = col >= (F - keep)[:, None]
+    mask[rc] = mask[rc][:, ::-1]
+    rows, cols = np.nonzero(mask)
+    g[starts[rows] + cols] = copies[rows, cols]
+    return int(keep.sum())
+
+
+def _satellites(g: np.ndarray, frac: float, rng: np.random.Generator) -> None:
+    """Alpha-satellite-like arrays (171-bp monomers, 2-10 % diverged, tens of
+    kb long) and microsatellites (periods 1-6, 20-400 bp)."""
+    n = g.size
+    budget = int(n * frac * 0.8)
+    mono = rng.integers(0, 4, size=171, dtype=np.uint8)
+    while budget > 0 and n > 200_000:
+        ln = int(rng.integers(20_000, 200_000))
+        k = ln // 171 + 1
+        arr = np.tile(mono, k)[:ln]
+        hit = rng.random(ln) < float(rng.uniform(0.02, 0.10))
+        arr[hit] = (arr[hit] + rng.integers(1, 4, size=int(hit.sum()), dtype=np.uint8)) & 3
+        p = int(rng.integers(0, n - ln))
+        g[p:p + ln] = arr
+        budget -= ln
+    budget = int(n * frac * 0.2)
+    while budget > 0 and n > 20_000:
+        m = min(4096, max(1, budget // 200))
+        period = rng.integers(1, 7, size=m)
+        ln = rng.integers(20, 400, size=m)
+        for per, L in zip(period, ln):
+            unit = rng.integers(0, 4, size=int(per), dtype=np.uint8)
+            p = int(rng.integers(0, n - int(L)))
+            g[p:p + int(L)] = np.resize(unit, int(L))
+        budget -= int(ln.sum())
+
+
+def make_genome_human_like(n_bp: int, seed: int = 1, n_chrom: int = 24, satellite_frac: float = 0.03) -> Genome:
+    """Random genome with a human-like interspersed repeat profile (~46 % of
+    the bases are repeat copies, HUMAN_REPEATS: Alu-like high-copy ~300-bp
+    families at 2-18 % divergence, 5'-truncated ~6-kb L1-like families, old
+    diverged LINE-2/MIR, LTR and DNA-transposon families) plus ~3 % satellite
+    and simple-sequence arrays.  human_g1k_v37 is ~50 % repeats; the default
+    make_genome has 2 %."""
+    rng = np.random.default_rng([seed, 0x48554d])
+    g = rng.integers(0, 4, size=n_bp, dtype=np.uint8)
+    for _name, frac, (lo, hi), n_fam, (dlo, dhi), trunc in HUMAN_REPEATS:
+        budget = int(n_bp * frac)
+        fams = [rng.integers(0, 4, size=int(rng.integers(lo, hi + 1)), dtype=np.uint8) for _ in range(n_fam)]
+        # family sizes in copy number follow a steep power law (a few very
+        # young, high-copy families), the bases split accordingly
+        w = 1.0 / np.arange(1, n_fam + 1) ** 1.2
+        w /= w.sum()
+        for f, share in zip(fams, w):
+            mean_keep = f.size * (trunc + (1 - trunc) / 2)
+            n_cp = int(budget * share / max(mean_keep, 1))
+            while n_cp > 0:   # bounded temporaries: at most ~64 MB of copies at a time
+                step = max(1, min(n_cp, (64 << 20) // f.size))
+                _scatter_copies(g, f, step, dlo, dhi, trunc, rng)
+                n_cp -= step
+    _satellites(g, satellite_frac, rng)
+    n_chrom = max(1, min(n_chrom, n_bp // 1000 if n_bp >= 1000 else 1))
+    cuts = np.sort(rng.choice(np.arange(1, n_bp), size=n_chrom - 1, replace=False)) if n_chrom > 1 else np.array([], dtype=np.int64)
+    starts = np.concatenate([[0], cuts, [n_bp]]).astype(np.int64)
+    return Genome(g, [f"chr{i + 1}" for i in range(n_chrom)], starts)
+
+
 def write_fasta(path: str, genome: Genome, width: int = 60) -> None:
     with open(path, "wb") as fh:
         for i, name in enumerate(genome.chrom_names):
@@ -178,6 +273,84 @@ def make_reads(genome_codes: np.ndarray, n_reads: int, read_len, seed: int = 1, 
     if n_rate > 0 and total:
         codes[rng.random(total) < n_rate] = 4
     return Reads(lens, codes, offs)
+
+
+def block_seed(seed: int, b: int) -> int:
+    """The seed of block b of a blocked read stream."""
+    return int(np.random.SeedSequence([seed, b]).generate_state(1)[0])
+
+
+def make_read_blocks(genome_codes: np.ndarray, blocks, block: int, read_len: int, seed: int = 1, pairs: bool = False,
+                     **kw) -> Reads:
+    """Blocks of a read stream defined block by block: block b holds `block`
+    reads (pairs: block // 2 interleaved pairs) drawn with seed block_seed(seed, b),
+    so any subset of blocks -- a rank's shard (contiguous
+    chunks dealt round-robin to the GPUs) -- is generated without the rest,
+    and shards reassembled in block order are the single-rank stream."""
+    def one(b):
+        s = block_seed(seed, int(b))
+        if pairs:
+            return make_pairs(genome_codes, block // 2, read_len, seed=s, **kw)
+        return make_reads(genome_codes, block, read_len, seed=s, **kw)
+
+    blocks = list(blocks)
+    if len(blocks) > 2:   # blocks are independent: numpy releases the GIL in the bulk work
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=min(8, len(blocks))) as ex:
+            parts = list(ex.map(one, blocks))
+    else:
+        parts = [one(b) for b in blocks]
+    return concat_reads(parts) if parts else make_reads(genome_codes, 0, read_len, seed=seed)
+
+
+def make_reads_big(genome_codes: np.ndarray, n_reads: int, read_len: int, seed: int = 1, block: int = 1 << 20,
+                   **kw) -> Reads:
+    """make_reads for read sets of tens of millions, generated in blocks of
+    `block` reads (block b from block_seed(seed, b)) so one block's index
+    matrix bounds the temporary memory; the last block is cut to n_reads."""
+    nb = (n_reads + block - 1) // block
+    r = make_read_blocks(genome_codes, range(nb), block, read_len, seed=seed, **kw)
+    return r.subset(np.arange(n_reads)) if r.n > n_reads else r
+
+
+def make_pairs(genome_codes: np.ndarray, n_pairs: int, read_len: int, seed: int = 1, insert_mean: float = 500.0,
+               insert_sd: float = 50.0, sub_rate: float = 0.02, n_rate: float = 0.001, block: int = 1 << 19,
+               with_pos: bool = False):
+    """Paired-end reads, interleaved as bwa mem reads them (read 2k = mate 1,
+    2k + 1 = mate 2 of pair k; software/bwamem.c:1600-1609): a fragment of
+    length ~N(insert_mean, insert_sd) (at least read_len) from a uniform
+    position; mate 1 is its first read_len bases, mate 2 the reverse
+    complement of its last read_len bases (FR orientation); half of the
+    fragments come from the reverse strand (mates swapped in effect).
+    Substitutions at sub_rate and ambiguous bases at n_rate per base."""
+    L = int(read_len)
+    G = genome_codes.size
+    lens = np.full(2 * n_pairs, L, dtype=np.int32)
+    codes = np.empty(2 * n_pairs * L, dtype=np.uint8)
+    frag = np.zeros((n_pairs, 3), dtype=np.int64)   # (start, insert, reverse strand)
+    for b, a in enumerate(range(0, n_pairs, block)):
+        n = min(block, n_pairs - a)
+        rng = np.random.default_rng([seed, b])
+        ins = np.clip(np.rint(rng.normal(insert_mean, insert_sd, size=n)), L, max(L, G - 1)).astype(np.int64)
+        pos = (rng.random(n) * (G - ins + 1)).astype(np.int64)
+        ar = np.arange(L)[None, :]
+        m1 = genome_codes[pos[:, None] + ar]
+        m2 = genome_codes[(pos + ins - L)[:, None] + ar]
+        m2 = (3 - m2)[:, ::-1]
+        rc = rng.random(n) < 0.5   # fragment from the reverse strand: mate 1 is the other end
+        m1[rc], m2[rc] = m2[rc].copy(), m1[rc].copy()
+        blk = np.empty((n, 2, L), dtype=np.uint8)
+        blk[:, 0], blk[:, 1] = m1, m2
+        flat = blk.reshape(-1)
+        if sub_rate > 0:
+            hit = rng.random(flat.size) < sub_rate
+            flat[hit] = (flat[hit] + rng.integers(1, 4, size=int(hit.sum()), dtype=np.uint8)) & 3
+        if n_rate > 0:
+            flat[rng.random(flat.size) < n_rate] = 4
+        codes[2 * a * L:2 * (a + n) * L] = flat
+        frag[a:a + n, 0], frag[a:a + n, 1], frag[a:a + n, 2] = pos, ins, rc
+    r = Reads(lens, codes, np.concatenate([[0], np.cumsum(lens, dtype=np.int64)]))
+    return (r, frag) if with_pos else r
 
 
 def concat_reads(parts) -> Reads:

@@ -133,6 +133,39 @@ void smem_gpu_shutdown(smem_gpu_t *gpu);
 int  smem_gpu_collect(smem_gpu_t *gpu, int n_reads, const uint8_t *const *seq, const int *len,
                       const smem_opt_t *opt, smem_batch_t **batch_out);
 
+/* ------------------------------------------------------------ streaming */
+/* bwa mem's chunk loop (software/fastmap.c:213-228, mem_process_seqs ->
+ * kt_for_batch, software/bwamem.c:1614-1640, software/kthread_batch.c:29-59)
+ * over one device, for read sets larger than one batch.  Reads [0, n_reads)
+ * (nt4 codes, offs[n_reads + 1] into codes) are cut into chunks of at most
+ * chunk_reads; n_workers host threads each own a batch (pinned staging
+ * buffers, a HIP stream, device buffers) and run whole chunks: stage + H2D,
+ * seeding + compaction, D2H into pinned host memory, then fn(ctx, chunk,
+ * first_read, n, batch) on that worker's thread, where smem_batch_read /
+ * smem_batch_results give the chunk's results (valid until fn returns).
+ * Chunks are claimed in order; callbacks of different workers may overlap
+ * and complete out of order (the chunk index orders them).  flags:
+ * SMEM_STREAM_PAIRS -- n_reads must be even and chunk boundaries are kept
+ * even, so both mates of a pair (reads 2k, 2k+1, interleaved as
+ * software/bwamem.c:1600-1609 reads them) land in one chunk;
+ * SMEM_STREAM_PACKED -- each interval crosses PCIe as a 16-B smem_pintv_t
+ * (reads < 8192 bp), read with smem_batch_results_packed + smem_pintv_unpack
+ * in the callback.  fn may be NULL; a non-zero return from fn stops the
+ * stream and is returned. */
+typedef int (*smem_chunk_fn)(void *ctx, int64_t chunk, int64_t first_read, int n_reads, const smem_batch_t *b);
+#define SMEM_STREAM_PAIRS   1   /* interleaved mates: chunks keep pairs whole */
+#define SMEM_STREAM_PACKED  2   /* results as 16-B smem_pintv_t (smem_batch_results_packed): half the D2H */
+typedef struct {
+	double wall_s;           /* first chunk claimed -> last chunk delivered */
+	uint64_t n_reads, n_chunks, n_intv;
+	uint64_t h2d_bytes;      /* reads + offsets copied host -> device */
+	uint64_t d2h_bytes;      /* intervals + list sizes + offsets copied device -> host */
+	int workers;
+} smem_stream_stats_t;
+int  smem_gpu_seed_stream(smem_gpu_t *gpu, int64_t n_reads, const uint8_t *codes, const uint64_t *offs,
+                          const smem_opt_t *opt, int chunk_reads, int n_workers, int flags, smem_chunk_fn fn,
+                          void *ctx, smem_stream_stats_t *stats);
+
 /* ------------------------------------------------------- batch (explicit) */
 int  smem_batch_create(smem_gpu_t *gpu, int max_reads, uint64_t max_bases, int max_len, smem_batch_t **b);
 void smem_batch_destroy(smem_batch_t *b);
@@ -151,6 +184,22 @@ int  smem_batch_read(const smem_batch_t *b, int i, const smem_intv_t **intv, int
 /* whole-batch views of fetched results: intv_off/call_off have n_reads+1 entries */
 int  smem_batch_results(const smem_batch_t *b, const smem_intv_t **intv, const uint64_t **intv_off,
                         const uint32_t **call_n, const uint64_t **call_off);
+
+/* 16-B wire form of a bwtintv_t (SMEM_STREAM_PACKED): x0, x1, x2 low words;
+ * w = x0 bits 32-33 | x1 bits 32-33 << 2 | x2 bits 32-33 << 4 | query begin << 6
+ * | query end << 19 (13 bits each) */
+typedef struct { uint32_t x0, x1, x2, w; } smem_pintv_t;
+#define SMEM_PINTV_MAX_LEN 8191
+static inline void smem_pintv_unpack(const smem_pintv_t *p, smem_intv_t *o)
+{
+	o->x[0] = (uint64_t)(p->w & 3) << 32 | p->x0;
+	o->x[1] = (uint64_t)(p->w >> 2 & 3) << 32 | p->x1;
+	o->x[2] = (uint64_t)(p->w >> 4 & 3) << 32 | p->x2;
+	o->info = (uint64_t)(p->w >> 6 & 8191) << 32 | (p->w >> 19);
+}
+/* the packed view of a batch fetched in SMEM_STREAM_PACKED mode */
+int  smem_batch_results_packed(const smem_batch_t *b, const smem_pintv_t **pintv, const uint64_t **intv_off,
+                               const uint32_t **call_n, const uint64_t **call_off);
 
 /* ------------------------------------------------------- SA lookup */
 /* Keep the sampled SA of the uploaded index resident in HBM (the index's

@@ -178,6 +178,8 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 	orc_intv_t ik, ok[4];
 	ivec_t *prev = &w->prev, *curr = &w->curr, *t;
 	int i, j, c, ret;
+	uint64_t ik_prev2 = 0;
+	int had_u1 = 0, has_u1 = 0;
 
 	mem->n = 0;
 	w->st.n_smem1++;
@@ -197,6 +199,11 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 		c = 3 - q[i];
 		orc_extend(b, &ik, ok, 0);
 		count_extend(b, &ik, 0, 1, &w->st);
+		w->st.n_ext_fwd++;
+		w->st.n_ext_len[i + 1 - x < 32 ? i + 1 - x : 32]++;
+		if (i - x <= 12) w->st.n_ext_fwd_k12++;
+		if (ik.x[2] == 1) { w->st.n_ext_u1_fwd++; if (i == x + 1 || ik_prev2 != 1) w->st.n_run_u1++; }
+		ik_prev2 = ik.x[2];
 		if (ok[c].x[2] != ik.x[2]) {
 			iv_push(&w->fwd, &ik);
 			if (ok[c].x[2] < (uint64_t)min_intv) break;
@@ -214,10 +221,17 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 	for (i = x - 1; i >= -1; --i) {
 		c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
 		curr->n = 0;
+		had_u1 = has_u1; has_u1 = 0;
 		for (j = 0; j < (int)prev->n; ++j) {
 			orc_intv_t *p = &prev->a[j];
 			orc_extend(b, p, ok, 1);
 			count_extend(b, p, 1, c >= 0, &w->st);
+			if (c >= 0) { int sl = (int)(uint32_t)p->info - i; w->st.n_ext_len[sl < 32 ? sl : 32]++; }
+			if (c >= 0 && p->x[2] == 1) {
+				w->st.n_ext_u1_bwd++;
+				if (!had_u1) w->st.n_run_u1++;
+				has_u1 = 1;
+			}
 			if (c < 0 || ok[c].x[2] < (uint64_t)min_intv) {
 				/* p cannot be extended: it is a MEM unless a longer one was
 				 * already kept at this i, or it is contained in the last one */
@@ -366,6 +380,9 @@ static void add_stats(orc_stats_t *d, const orc_stats_t *s)
 	d->n_calls += s->n_calls; d->n_intv += s->n_intv; d->n_smem1 += s->n_smem1;
 	d->n_ext += s->n_ext; d->n_ext_ref += s->n_ext_ref; d->n_bkt += s->n_bkt;
 	d->n_bkt_ref += s->n_bkt_ref; d->n_bases += s->n_bases; d->n_bkt64 += s->n_bkt64;
+	d->n_ext_fwd += s->n_ext_fwd; d->n_ext_u1_fwd += s->n_ext_u1_fwd; d->n_ext_u1_bwd += s->n_ext_u1_bwd;
+	d->n_run_u1 += s->n_run_u1; d->n_ext_fwd_k12 += s->n_ext_fwd_k12;
+	{ int k; for (k = 0; k < 33; ++k) d->n_ext_len[k] += s->n_ext_len[k]; }
 }
 
 int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,

@@ -52,6 +52,12 @@ typedef struct {
 	uint64_t n_bkt_ref;     /* same over n_ext_ref */
 	uint64_t n_bases;       /* query bases of reads that entered the loop */
 	uint64_t n_bkt64;       /* distinct 32-B Occ64 buckets (64 symbols) over n_ext: the GPU layout */
+	uint64_t n_ext_fwd;     /* n_ext in forward loops (software/bwt.c:791-805) */
+	uint64_t n_ext_u1_fwd;  /* forward extends of a size-1 interval (x2 == 1) */
+	uint64_t n_ext_u1_bwd;  /* backward extends (c >= 0) of a size-1 interval */
+	uint64_t n_run_u1;      /* maximal runs of size-1 extends of one interval (fwd or bwd) */
+	uint64_t n_ext_fwd_k12; /* forward extends at depth i - x < 12 with no N before them */
+	uint64_t n_ext_len[33]; /* used extends by the length of the string they produce (32 = 32 or more) */
 } orc_stats_t;
 
 orc_bwt_t *orc_bwt_load(const char *fn);

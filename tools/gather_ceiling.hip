@@ -14,7 +14,9 @@
 // mode 3: the cooperative layout through registers (global_load_dwordx4 + ds_write_b128);
 // mode 4: per-lane buckets (2 per lane) by LDS-DMA, 4 chunk-planes per bucket;
 // mode 5: mode 4 plus argv[8] lane-private cache-hit loads per round;
-// mode 6: the Occ64 fetch, 2 random 32-B buckets per lane (2 x 16-B chunks each).
+// mode 6: the Occ64 fetch, 2 random 32-B buckets per lane (2 x 16-B chunks each);
+// mode 7: k-mer interval table probes, 2 random 16-B entries per lane (64-bit
+//         indices: tables past 64 GB).
 // Every round waits for its data (vmcnt(0)) before the next, like the
 // kernel; addresses are independent so only bandwidth/queueing limit it.
 #include <hip/hip_runtime.h>
@@ -37,7 +39,7 @@ __device__ __forceinline__ uint32_t mix(uint32_t x) {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void gather(const uint4* __restrict__ tab, uint32_t n_buckets, int iters,
+__global__ __launch_bounds__(256) void gather(const uint4* __restrict__ tab, uint64_t n_buckets, int iters,
                                               uint32_t* __restrict__ sink, int active, int extra) {
     __shared__ uint4 img[4][256][4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -86,6 +88,20 @@ __global__ __launch_bounds__(256) void gather(const uint4* __restrict__ tab, uin
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint4* pl = &img[w][0][0];
             const uint4 v = pl[lane], u = pl[3 * 64 + lane];
+            acc ^= v.x ^ u.w;
+        } else if (MODE == 7) {
+            // 2 random 16-B table entries per lane, 64-bit indices
+            if (lane < active)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const uint32_t h = mix(seed + it * 2 + b);
+                const uint64_t e = (((uint64_t)mix(h ^ 0x5bd1e995u) << 32) | h) % n_buckets;
+                __builtin_amdgcn_global_load_lds(tab + e, (__attribute__((address_space(3))) void*)&img[w][b * 16][0],
+                                                 16, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint4* pl = &img[w][0][0];
+            const uint4 v = pl[lane], u = pl[64 + lane];
             acc ^= v.x ^ u.w;
         } else if (MODE == 5) {
             // mode 4 plus `extra` per-lane 16-B LDS-DMA loads from a lane-private
@@ -155,10 +171,11 @@ int main(int argc, char** argv) {
         CHECK(hipMalloc(&tab, bytes));
     CHECK(hipMalloc(&sink, 4));
     CHECK(hipMemset(tab, 1, bytes));
-    const int bsz = (mode == 2 || mode == 6) ? 32 : 64;
+    const int bsz = mode == 7 ? 16 : (mode == 2 || mode == 6) ? 32 : 64;
     // argv[5]: restrict the addresses to the first N buckets (e.g. 256 = L1-resident)
-    uint32_t n_buckets = (uint32_t)(bytes / bsz);
-    if (argc > 5 && atol(argv[5]) > 0 && (uint64_t)atol(argv[5]) < n_buckets) n_buckets = (uint32_t)atol(argv[5]);
+    uint64_t n_buckets = bytes / bsz;
+    if (mode != 7 && n_buckets > 0xffffffffull) n_buckets = 0xffffffffull;
+    if (argc > 5 && atol(argv[5]) > 0 && (uint64_t)atol(argv[5]) < n_buckets) n_buckets = (uint64_t)atol(argv[5]);
     const int grid = prop.multiProcessorCount * wpc / 4;
     int active = argc > 6 ? atoi(argv[6]) : 64;  // mode 4: lanes that fetch
     if (active < 1 || active > 64) active = 64;
@@ -175,11 +192,12 @@ int main(int argc, char** argv) {
         if (mode == 4) hipLaunchKernelGGL(gather<4>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
         if (mode == 5) hipLaunchKernelGGL(gather<5>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
         if (mode == 6) hipLaunchKernelGGL(gather<6>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 7) hipLaunchKernelGGL(gather<7>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
-        const double nbk = (double)grid * 4 * iters * ((mode == 4 || mode == 6) ? 2 * active : 128);  // buckets fetched
+        const double nbk = (double)grid * 4 * iters * ((mode == 4 || mode == 6 || mode == 7) ? 2 * active : 128);  // buckets fetched
         printf("{\"table_MB\": %zu, \"waves_per_cu\": %d, \"mode\": %d, \"bucket_B\": %d, \"ms\": %.3f, "
                "\"Gbuckets_per_s\": %.2f, \"TB_per_s\": %.3f, \"active\": %d, \"us_per_round\": %.3f}\n",
                mb, wpc, mode, bsz, ms, nbk / ms * 1e-6, nbk * bsz / ms * 1e-9, active, ms * 1e3 / iters);

@@ -1,19 +1,21 @@
-"""Record the seeding kernel's per-launch memory-side traffic for bench.py.
+"""Record the seeding kernel's per-launch memory-side counters for bench.py.
 
-Runs two rocprofv3 counter passes (FETCH_SIZE, then WRITE_SIZE: they do not
-fit one pass, MI355X_MICROARCH.md §counters) over tools/prof_run.py on the
-bench workload and writes profiles/traffic.json, which bench.py reports as
-roofline.traffic when its workload matches.
+Runs rocprofv3 counter passes (one run per pass, nothing else combined with
+--pmc: MI355X_MICROARCH.md §counters) over tools/prof_run.py on the bench
+workload and writes profiles/traffic.json, which bench.py reports in
+roofline.traffic / request_roofline when its workload AND its library build
+(smem_gpu_build_id) match:
 
-    python tools/traffic.py [--genome-mbp 1000 --reads 1000000] [--out profiles/traffic.json]
+  pass 1: TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum  -- L2 fabric read requests
+  pass 2: WRITE_SIZE
 
-FETCH_SIZE is TCC_EA0_RDREQ x 64 B (KiB units): the L2's fabric-side read
-requests, Infinity-Cache hits included.  The guide calibrates it at 1/2 of
-the bytes for 16-B-per-lane coalesced streaming reads and leaves other access
-shapes uncalibrated; the seeding kernel's are random 16-B lane chunks, so the
-value is reported as measured.
+Calibration (profiles/r02/probe/fetch_size_calibration.txt): on random 16-B
+and 32-B gathers of known count, TCC_EA0_RDREQ counts exactly one request per
+gather and FETCH_SIZE = 64 B x TCC_EA0_RDREQ, i.e. each random request moves
+one 64-B line; so traffic = 64 B x TCC_EA0_RDREQ.
+
+    python tools/traffic.py [bench.py workload args] [--out profiles/traffic.json]
 """
-import argparse
 import csv
 import glob
 import json
@@ -23,43 +25,47 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
+sys.path.insert(0, ROOT)
 
 
-def run_pass(counter: str, out_dir: str, a) -> float:
-    d = os.path.join(out_dir, counter)
-    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "seed_kernel", "--output-format", "csv",
-           "-d", d, "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_run.py"),
-           "--genome-mbp", str(a.genome_mbp), "--reads", str(a.reads), "--read-len", str(a.read_len),
-           "--seed", str(a.seed), "--launches", "1"]
-    subprocess.run(cmd, check=True, timeout=600)
-    tot, n = 0.0, set()
+def run_pass(counters: list, out_dir: str, rest: list) -> dict:
+    d = os.path.join(out_dir, "_".join(c.split("_")[0] + str(i) for i, c in enumerate(counters)))
+    cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", *counters, "--kernel-include-regex", "seed_kernel",
+           "--output-format", "csv", "-d", d, "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_run.py"),
+           "--launches", "1", *rest]
+    subprocess.run(cmd, check=True)
+    tot, disp = {}, {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == counter:
-                tot += float(r["Counter_Value"])
-                n.add(r.get("Dispatch_Id", ""))
-    # the main pass only (an overflow re-run would be a second dispatch)
-    return tot * 1024.0, len(n)
+            k = r["Counter_Name"]
+            tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
+            disp.setdefault(k, set()).add(r.get("Dispatch_Id", ""))
+    return {k: (v, len(disp[k])) for k, v in tot.items()}
 
 
 def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--genome-mbp", type=float, default=3101.804739)
-    p.add_argument("--reads", type=int, default=1_000_000)
-    p.add_argument("--read-len", type=int, default=150)
-    p.add_argument("--seed", type=int, default=1)
-    p.add_argument("--tmp", default=os.path.join(ROOT, "gpurun_out", "traffic"))
+    import argparse
+    p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    a = p.parse_args()
+    p.add_argument("--tmp", default=os.path.join(ROOT, "gpurun_out", "traffic"))
+    own, rest = p.parse_known_args()
+    import bench
+    import smemgpu
+    a = bench.parse(rest)
     os.environ.setdefault("TMPDIR", "/tmp")
-    fetch, nf = run_pass("FETCH_SIZE", a.tmp, a)
-    write, nw = run_pass("WRITE_SIZE", a.tmp, a)
-    out = {"bytes_per_launch": fetch, "write_bytes_per_launch": write, "dispatches": [nf, nw],
-           "counter": "FETCH_SIZE x 1024 (TCC_EA0_RDREQ x 64 B), as measured",
-           "workload": {"genome_mbp": a.genome_mbp, "reads": a.reads, "read_len": a.read_len, "seed": a.seed},
+    r1 = run_pass(["TCC_EA0_RDREQ_sum", "TCC_HIT_sum", "TCC_MISS_sum"], own.tmp, rest)
+    r2 = run_pass(["WRITE_SIZE"], own.tmp, rest)
+    out = {"rdreq_per_launch": r1["TCC_EA0_RDREQ_sum"][0], "tcc_hit_per_launch": r1["TCC_HIT_sum"][0],
+           "tcc_miss_per_launch": r1["TCC_MISS_sum"][0], "write_bytes_per_launch": r2["WRITE_SIZE"][0] * 1024.0,
+           "dispatches": [r1["TCC_EA0_RDREQ_sum"][1], r2["WRITE_SIZE"][1]],
+           "counter": "TCC_EA0_RDREQ_sum (L2 -> fabric read requests), TCC_HIT/MISS_sum, WRITE_SIZE x 1024",
+           "workload": {"genome_mbp": a.genome_mbp, "reads": a.reads, "read_len": a.read_len, "seed": a.seed,
+                        "sub": a.sub, "genome_profile": a.genome_profile},
+           "build_id": smemgpu.source_hash(),  # == the loaded build (prof_run refuses nothing; bench checks)
            "measured": time.strftime("%Y-%m-%d %H:%M:%S")}
-    os.makedirs(os.path.dirname(a.out), exist_ok=True)
-    with open(a.out, "w") as fh:
+    os.makedirs(os.path.dirname(own.out) or ".", exist_ok=True)
+    with open(own.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
 
