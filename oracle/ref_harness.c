@@ -35,6 +35,18 @@
  *       (software/bwamem.c:1452-1460); every read's regions written as SMRG:
  *       "SMRG0001", u64 n_reads, per read u32 n then n x {i64 rb, re;
  *       i32 qb, qe, score, truesc, sub, csub, sub_n, w, seedcov, secondary}.
+ *   mem   <prefix> <reads.fq> <n_threads> <batch_size> <pe> [<pg>]
+ *       The body of the reference's main_mem (software/fastmap.c:193-230) on the
+ *       unmodified pipeline: bwa_print_sam_hdr, then bseq_read chunks through
+ *       mem_process_seqs (software/bwamem.c:1614: kt_for_batch -> worker1_batched
+ *       -> mem_align1_core_batched, then mem_sam_pe / mem_reg2sam_se), SAM on
+ *       stdout.  The index is loaded as bwa_idx_load does (software/bwa.c:312-333)
+ *       minus bwa_idx_load_bwt's FPGA upload (software/bwa.c:283-307), and the
+ *       per-worker buffers main_mem allocates for the HARP path
+ *       (software/fastmap.c:208-210; sw_handshake as the manager allocates it,
+ *       :324) are allocated the same way.  With batch_size <= 2 every batch takes
+ *       bwt_smem1_batched's CPU path (software/bwt.c:603, 686-717): this is
+ *       `bwa mem -t N -b 1` of the reference, the golden SAM for the GPU build.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -43,9 +55,15 @@
 #include <pthread.h>
 #include <sys/time.h>
 
+#include <zlib.h>
 #include "bwt.h"
 #include "bwamem.h"
+#include "bwa.h"
+#include "bntseq.h"
+#include "kseq.h"
+#include "utils.h"
 #include "smem_formats.h"
+KSEQ_DECLARE(gzFile)
 
 /* defined in software/bwamem.c:244 (not exported by software/bwamem.h) */
 extern const bwtintv_v *smem_next2(smem_i *itr, int split_len, int split_width, int start_width);
@@ -418,6 +436,74 @@ static int cmd_ksw(int argc, char **argv)
 	return 0;
 }
 
+/* the HARP-path globals of software/fastmap.c:27-29 and software/main.c:28 (their
+ * definitions are linked from the reference objects; allocated here as
+ * main_mem and the manager thread do) */
+extern unsigned long int **worker_mem;
+extern volatile unsigned char *sw_handshake;
+extern char *bwa_pg;
+
+static int cmd_mem(int argc, char **argv)
+{
+	mem_opt_t *opt;
+	bwt_t *bwt;
+	bntseq_t *bns;
+	uint8_t *pac;
+	char *tmp;
+	gzFile fp;
+	kseq_t *ks;
+	bseq1_t *seqs;
+	int i, n;
+	int64_t n_processed = 0;
+	if (argc < 6) { fprintf(stderr, "usage: mem <prefix> <reads.fq> <threads> <batch> <pe> [pg]\n"); return 1; }
+	opt = mem_opt_init();
+	opt->n_threads = atoi(argv[3]);
+	opt->batch_size = atoi(argv[4]) > 1? atoi(argv[4]) : 1;
+	if (atoi(argv[5])) opt->flag |= MEM_F_PE;
+	bwa_pg = argc > 6? argv[6] : "@PG\tID:bwa\tPN:bwa\tVN:0.7.8-r455";
+	tmp = calloc(strlen(argv[1]) + 5, 1);
+	strcat(strcpy(tmp, argv[1]), ".bwt");
+	bwt = bwt_restore_bwt(tmp);
+	strcat(strcpy(tmp, argv[1]), ".sa");
+	bwt_restore_sa(tmp, bwt);
+	free(tmp);
+	bns = bns_restore(argv[1]);
+	pac = calloc(bns->l_pac / 4 + 1, 1);
+	err_fread_noeof(pac, 1, bns->l_pac / 4 + 1, bns->fp_pac);
+	err_fclose(bns->fp_pac);
+	bns->fp_pac = 0;
+	fp = gzopen(argv[2], "r");
+	if (!fp) return 1;
+	ks = kseq_init(fp);
+	bwa_print_sam_hdr(bns, 0);
+	worker_mem = (unsigned long int **)malloc(sizeof(unsigned long int *) * opt->n_threads);
+	for (i = 0; i < opt->n_threads; ++i)
+		worker_mem[i] = (unsigned long int *)malloc(sizeof(unsigned long int) * 1024 * 1024 + 1);
+	sw_handshake = (unsigned char *)calloc(opt->n_threads + 1, 1);
+	while ((seqs = bseq_read(opt->chunk_size * opt->n_threads, &n, ks, 0)) != 0) {
+		if ((opt->flag & MEM_F_PE) && (n & 1)) n = n >> 1 << 1;
+		for (i = 0; i < n; ++i) { free(seqs[i].comment); seqs[i].comment = 0; }
+		mem_process_seqs(opt, bwt, bns, pac, n_processed, n, seqs, 0);
+		n_processed += n;
+		for (i = 0; i < n; ++i) {
+			err_fputs(seqs[i].sam, stdout);
+			free(seqs[i].name); free(seqs[i].comment); free(seqs[i].seq); free(seqs[i].qual); free(seqs[i].sam);
+		}
+		free(seqs);
+	}
+	for (i = 0; i < opt->n_threads; ++i) free(worker_mem[i]);
+	free(worker_mem);
+	free((void*)sw_handshake);
+	kseq_destroy(ks);
+	gzclose(fp);
+	free(pac);
+	bns_destroy(bns);
+	bwt_destroy(bwt);
+	free(opt);
+	fflush(stdout);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	if (argc < 2) {
@@ -436,6 +522,7 @@ int main(int argc, char **argv)
 	if (strcmp(argv[1], "chain") == 0) return cmd_chain(argc - 1, argv + 1);
 	if (strcmp(argv[1], "ksw") == 0) return cmd_ksw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "aln") == 0) return cmd_aln(argc - 1, argv + 1);
+	if (strcmp(argv[1], "mem") == 0) return cmd_mem(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }
