@@ -429,6 +429,59 @@ def chain_report(batch, opt, l_pac: int, reps: int = 3) -> dict:
             "what": "mem_chain (kbtree of chains, test_and_merge) + mem_chain_flt, w 100, max_chain_gap 10000"}
 
 
+def pack_pac(codes) -> np.ndarray:
+    """2-bit forward strand as bns_fasta2bntseq packs it (software/bntseq.c:303-309)."""
+    c = np.asarray(codes, dtype=np.uint8)
+    n = c.size
+    out = np.zeros((n + 3) // 4, dtype=np.uint8)
+    for k in range(4):
+        part = c[k::4]
+        out[:part.size] |= (np.minimum(part, 3) << (6 - 2 * k)).astype(np.uint8)
+    return out
+
+
+def aln_report(gpu, batch, opt, l_pac: int, reps: int = 3) -> dict:
+    """Chains -> alignment regions (mem_chain2aln_short /
+    mem_chain2aln of every filtered chain, software/bwamem.c:1452-1460) on the
+    GPU over the chains, seeds, reads and .pac already in HBM
+    (smem_batch_chain2aln); reported beside the SMEM metric."""
+    from oracle import oracle
+    batch.run(opt)
+    batch.sa(opt.min_seed_len, 10000)
+    batch.chain(l_pac)
+    best = None
+    for _ in range(reps):
+        batch.chain2aln(oracle.aln_opt(min_seed_len=opt.min_seed_len))
+        st = batch.stats()
+        if best is None or st["aln_ms"] < best["aln_ms"]:
+            best = st
+    n = batch.n_reads
+    return {"ms_per_batch": round(best["aln_ms"], 3), "regions": int(best["n_regs"]), "chains": int(best["n_chains"]),
+            "reads_per_s": round(n / (best["aln_ms"] * 1e-3), 1),
+            "what": "mem_chain2aln_short / mem_chain2aln (ksw_align2, ksw_extend2 both ways, MAX_BAND_TRY) of every "
+                    "chain kept by mem_chain_flt, one wave per read, chains / seeds / reads / .pac resident in HBM"}
+
+
+def aln_cpu(args, idx_path: str, reads, genome_codes, opt, n: int = 20000) -> dict:
+    """The reference's own chain2aln loop (oracle/_ref ref_harness aln: mem_chain
+    + mem_chain_flt untimed, then mem_chain2aln_short / mem_chain2aln timed),
+    one thread, on the first n reads: the alignment stage's CPU baseline."""
+    from oracle import oracle
+    from smemgpu import synth
+    if not oracle.ref_available():
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        pac = os.path.join(d, "g.pac")
+        pack_pac(genome_codes).tofile(pac)
+        p = os.path.join(d, "s.smrd")
+        m = min(n, reads.n)
+        synth.write_smrd(p, reads.subset(np.arange(m)))
+        r = oracle.ref_aln_time(idx_path, idx_path[:-4] + ".sa", pac, p, opt.min_seed_len)
+    return {"value": round(r["reads"] / r["chain2aln_seconds"], 1), "unit": "reads/s", "cores": 1,
+            "kind": "reference", "regions": int(r["regions"]),
+            "sample": f"first {m} reads, chain2aln loop {r['chain2aln_seconds']:.2f} s (chaining untimed)"}
+
+
 def sw_report(gpu, genome_codes, n_unique: int = 20000, tile: int = 10, reps: int = 3):
     """SW extension: ksw_extend2 on the GPU over
     problems shaped like mem_chain2aln's left/right extensions, drawn from the
@@ -596,10 +649,12 @@ def main():
     srep["reads_per_s_all_ranks"] = round(s_rate, 1)
     del sreads
 
-    sa_rep = chain_rep = sw_rep = sw_tasks = None
+    sa_rep = chain_rep = sw_rep = sw_tasks = aln_rep = None
     if rank == 0 and args.side_stages:
         sa_rep = sa_lookup(batch, opt)
         chain_rep = chain_report(batch, opt, idx.seq_len // 2)
+        gpu.load_pac(pack_pac(genome_codes), idx.seq_len // 2)
+        aln_rep = aln_report(gpu, batch, opt, idx.seq_len // 2)
         sw_rep, sw_tasks = sw_report(gpu, np.asarray(genome_codes))
 
     if rank == 0:
@@ -609,6 +664,8 @@ def main():
                                                                           sw_tasks)
         if sw_rep is not None:
             sw_rep["cpu_baseline"] = sw_cpu_rep
+        if aln_rep is not None and args.cpu_seconds > 0:
+            aln_rep["cpu_baseline"] = aln_cpu(args, idx_path, reads, genome_codes, opt)
         k_ms = float(np.mean(kernel_ms))
         a_ms = float(np.mean(alone_ms))
         cfg = CONFIGS[args.config]
@@ -650,6 +707,7 @@ def main():
             "streaming": srep,
             "sa_lookup": sa_rep,
             "chaining": chain_rep,
+            "alignment": aln_rep,
             "sw_extension": sw_rep,
             "overflow_reads": st["n_overflow"],
             "build_id": smemgpu.build_id(),

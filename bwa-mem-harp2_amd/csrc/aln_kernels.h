@@ -45,9 +45,29 @@ struct AlnParams {
     AlnReg* out;
 };
 
+// one ksw_align2 call (software/ksw.c:342) as mem_chain2aln_short makes it
+struct KswATask {
+    uint64_t q_off, t_off;
+    int32_t qlen, tlen, xtra, pad;
+};
+struct KswAResult {
+    int32_t score, te, qe, score2, te2, tb, qb;
+};
+struct KswAParams {
+    const KswATask* task;
+    int n;
+    const uint8_t* q;
+    const uint8_t* t;
+    int8_t mat[28];
+    int o_del, e_del, o_ins, e_ins;
+    int shift, top;
+    KswAResult* out;
+};
+
 }  // namespace smem
 
 extern "C" {
+hipError_t smem_launch_ksw_align2(const smem::KswAParams* K, int n_cu, hipStream_t st);
 // long_reads != 0: the batch holds reads of 257..1024 bp (second instantiation)
 hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st);
 hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st);

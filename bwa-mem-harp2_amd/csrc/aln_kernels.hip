@@ -312,8 +312,31 @@ __global__ __launch_bounds__(256) void aln_write_kernel(AlnParams P) {
     for (uint64_t i = 0; i < n; ++i) dst[i] = src[i];
 }
 
+// ksw_align2 of a batch of independent problems, one wave each (qlen <= 256)
+__global__ __launch_bounds__(256) void ksw_align2_kernel(KswAParams K) {
+    const int lane = threadIdx.x & 63;
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int n_waves = (int)((gridDim.x * blockDim.x) >> 6);
+    for (int it = wave; it < K.n; it += n_waves) {
+        const KswATask T = K.task[it];
+        const uint8_t* q = K.q + T.q_off;
+        const uint8_t* tg = K.t + T.t_off;
+        const kswd::SwAlign a = kswd::sw_align_wave(
+            T.qlen, [&](int j) { return (int)q[j]; }, T.tlen, [&](int i) { return (int)tg[i]; }, K.mat, K.o_del,
+            K.e_del, K.o_ins, K.e_ins, T.xtra, K.shift, K.top);
+        if (lane == 0) K.out[it] = KswAResult{a.score, a.te, a.qe, a.score2, a.te2, a.tb, a.qb};
+    }
+}
+
 }  // namespace
 }  // namespace smem
+
+extern "C" hipError_t smem_launch_ksw_align2(const smem::KswAParams* K, int n_cu, hipStream_t st) {
+    if (K->n <= 0) return hipSuccess;
+    const int waves = K->n < n_cu * 32 ? K->n : n_cu * 32;
+    hipLaunchKernelGGL(smem::ksw_align2_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, *K);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;

@@ -199,7 +199,7 @@ __device__ __forceinline__ KswResult extend_wave(const ExtIn& T, QF qsym, TF tsy
 constexpr int SW_XBYTE = 0x10000, SW_XSTOP = 0x20000, SW_XSUBO = 0x40000, SW_XSTART = 0x80000;
 
 struct SwOut {
-    int score, te, qe, score2;
+    int score, te, qe, score2, te2;
 };
 
 // One ksw_u8 (p = 16) or ksw_i16 (p = 8) pass.  The reference cuts the query
@@ -312,6 +312,7 @@ __device__ __forceinline__ SwOut sw_pass_wave(int p, int qlen, QF qsym, int tlen
     r.te = te;
     r.qe = -1;
     r.score2 = -1;
+    r.te2 = -1;
     if (!u8 || r.score != 255) {
         int m = NEG;
 #pragma unroll
@@ -330,13 +331,22 @@ __device__ __forceinline__ SwOut sw_pass_wave(int p, int qlen, QF qsym, int tlen
             for (int c = 0; c < 4; ++c)
                 if (64 * c + lane < n_b && (br[c] < low || br[c] > high)) cand = imax(cand, bv[c]);
             r.score2 = imax(-1, wave_max(cand));
+            // te2: the row of the first list entry holding score2 (the strict > scan)
+            if (r.score2 >= 0) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint64_t hit = __ballot(64 * c + lane < n_b && (br[c] < low || br[c] > high) &&
+                                                  bv[c] == r.score2);
+                    if (hit && r.te2 < 0) r.te2 = rl(br[c], __builtin_ctzll(hit));
+                }
+            }
         }
     }
     return r;
 }
 
 struct SwAlign {
-    int score, te, qe, score2, tb, qb;
+    int score, te, qe, score2, te2, tb, qb;  // kswr_t (software/ksw.h:13-15)
 };
 
 // ksw_align2 (software/ksw.c:342-364): the forward pass, then, for KSW_XSTART,
@@ -349,7 +359,7 @@ __device__ __forceinline__ SwAlign sw_align_wave(int qlen, QF qsym, int tlen, TF
     const int p = (xtra & SW_XBYTE) ? 16 : 8;
     const int minsc = (xtra & SW_XSUBO) ? xtra & 0xffff : 0x10000;
     const SwOut r = sw_pass_wave(p, qlen, qsym, tlen, tsym, mat, o_del, e_del, o_ins, e_ins, minsc, 0x10000, shift, top);
-    SwAlign a{r.score, r.te, r.qe, r.score2, -1, -1};
+    SwAlign a{r.score, r.te, r.qe, r.score2, r.te2, -1, -1};
     if ((xtra & SW_XSTART) == 0 || ((xtra & SW_XSUBO) && r.score < (xtra & 0xffff)) || r.qe < 0) return a;
     const int qe = r.qe, te = r.te;
     const SwOut rr = sw_pass_wave(

@@ -113,6 +113,8 @@ struct smem_gpu {
     uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
     uint32_t* d_occ192 = nullptr;   // Occ192 layout (variant 10)
     uint64_t* d_sa = nullptr;       // sampled SA (smem_gpu_load_sa), n_sa + 1 words
+    uint8_t* d_pac = nullptr;       // 2-bit forward strand (smem_gpu_load_pac)
+    int64_t l_pac = 0;
     uint64_t n_sa = 0;
     uint32_t sa_shift = 0;
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
@@ -185,8 +187,16 @@ struct smem_batch {
     HostBuf<uint64_t> h_chain_off;
     HostBuf<smem::OutChain> h_out_chain;
     HostBuf<smem::SeedRec> h_out_seed;
-    bool chain_ran = false, chain_fetched = false;
+    bool chain_ran = false, chain_fetched = false, chain_filtered = false;
     uint64_t tot_chains = 0, tot_seeds = 0;
+    // alignment regions (smem_batch_chain2aln)
+    DevBuf<uint64_t> d_aln_srt, d_aln_nregs, d_aln_regoff;
+    DevBuf<smem::AlnReg> d_aln_raw, d_aln_out;
+    DevBuf<uint32_t> d_aln_ctr;
+    HostBuf<uint64_t> h_aln_regoff;
+    HostBuf<smem::AlnReg> h_aln_regs;
+    bool aln_ran = false, aln_fetched = false;
+    uint64_t tot_regs = 0;
     smem_batch_stats_t stats{};
 };
 
@@ -322,6 +332,8 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_chn.release(); b->d_node.release(); b->d_flt.release(); b->d_n_out.release(); b->d_ns_out.release();
     b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release(); b->d_heavy.release();
     b->h_chain_off.release(); b->h_out_chain.release(); b->h_out_seed.release();
+    b->d_aln_srt.release(); b->d_aln_nregs.release(); b->d_aln_regoff.release(); b->d_aln_raw.release();
+    b->d_aln_out.release(); b->d_aln_ctr.release(); b->h_aln_regoff.release(); b->h_aln_regs.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
     b->d_pintv.release(); b->h_pintv.release();
     b->h_intv_off.release(); b->h_call_off.release();
@@ -342,6 +354,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     if (g->d_occ64) (void)hipFree(g->d_occ64);
     if (g->d_occ192) (void)hipFree(g->d_occ192);
     if (g->d_sa) (void)hipFree(g->d_sa);
+    if (g->d_pac) (void)hipFree(g->d_pac);
     delete g;
 }
 
@@ -483,6 +496,8 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->tot_occ = 0;
     b->chain_ran = b->chain_fetched = false;
     b->tot_chains = b->tot_seeds = 0;
+    b->aln_ran = b->aln_fetched = false;
+    b->tot_regs = 0;
     b->stats = smem_batch_stats_t{};
     b->stats.block = 256;
     smem::SeedParams P;
@@ -653,10 +668,21 @@ int smem_batch_fetch(smem_batch_t* b) {
             HIP_TRY(hipMemcpyAsync(b->h_out_seed.p, b->d_out_seed.p, sizeof(smem::SeedRec) * b->tot_seeds,
                                    hipMemcpyDeviceToHost, b->st));
     }
+    if (b->aln_ran) {
+        if (b->h_aln_regoff.n < (uint64_t)n + 1 || !b->h_aln_regoff.p) HIP_TRY(b->h_aln_regoff.ensure(n + 1));
+        if (b->h_aln_regs.n < b->tot_regs || !b->h_aln_regs.p)
+            HIP_TRY(b->h_aln_regs.ensure(std::max<uint64_t>(b->tot_regs + b->tot_regs / 4, 1)));
+        HIP_TRY(hipMemcpyAsync(b->h_aln_regoff.p, b->d_aln_regoff.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost,
+                               b->st));
+        if (b->tot_regs)
+            HIP_TRY(hipMemcpyAsync(b->h_aln_regs.p, b->d_aln_out.p, sizeof(smem::AlnReg) * b->tot_regs,
+                                   hipMemcpyDeviceToHost, b->st));
+    }
     HIP_TRY(hipStreamSynchronize(b->st));
     b->fetched = true;
     b->sa_fetched = b->sa_ran;
     b->chain_fetched = b->chain_ran;
+    b->aln_fetched = b->aln_ran;
     return SMEM_OK;
 }
 
@@ -762,6 +788,7 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     b->sa_fetched = false;
     b->sa_min_seed_len = min_seed_len;
     b->chain_ran = b->chain_fetched = false;
+    b->aln_ran = b->aln_fetched = false;
     return SMEM_OK;
 }
 
@@ -864,6 +891,8 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     b->stats.n_chains = b->tot_chains;
     b->chain_ran = true;
     b->chain_fetched = false;
+    b->chain_filtered = opt->filter != 0;
+    b->aln_ran = b->aln_fetched = false;
     return SMEM_OK;
 }
 
@@ -1004,6 +1033,78 @@ int smem_ksw_extend(smem_gpu_t* g, int n, const smem_ksw_task_t* tasks, const ui
     return SMEM_OK;
 }
 
+static_assert(sizeof(smem_ksw_atask_t) == sizeof(smem::KswATask), "align task layout");
+static_assert(sizeof(smem_ksw_aresult_t) == sizeof(smem::KswAResult), "align result layout");
+
+int smem_ksw_align2(smem_gpu_t* g, int n, const smem_ksw_atask_t* tasks, const uint8_t* q, uint64_t q_bytes,
+                    const uint8_t* t, uint64_t t_bytes, const smem_ksw_opt_t* opt, smem_ksw_aresult_t* out,
+                    double* kernel_ms) {
+    g_err[0] = 0;
+    if (!g || n < 0 || !opt || (n > 0 && (!tasks || !out))) return fail(SMEM_E_ARG, "smem_ksw_align2: bad arguments");
+    if (opt->e_del < 1 || opt->e_ins < 1 || opt->o_del < 0 || opt->o_ins < 0)
+        return fail(SMEM_E_ARG, "smem_ksw_align2: gap penalties need e >= 1, o >= 0");
+    for (int i = 0; i < n; ++i) {
+        const smem_ksw_atask_t& k = tasks[i];
+        if (k.qlen < 1 || k.qlen > 256 || k.tlen < 0 || k.tlen > 256 || k.q_off + (uint64_t)k.qlen > q_bytes ||
+            k.t_off + (uint64_t)k.tlen > t_bytes)
+            return fail(SMEM_E_ARG, "smem_ksw_align2: task outside 1 <= qlen <= 256, tlen <= 256 or its pools");
+        // a byte-scored problem must not overflow 255 from below the bias (ksw_align2's callers size
+        // XBYTE for that; a saturated u8 score is returned as 255, as ksw_u8 does)
+    }
+    for (uint64_t k = 0; k < q_bytes; ++k)
+        if (q[k] > 4) return fail(SMEM_E_ARG, "smem_ksw_align2: query code > 4");
+    if (kernel_ms) *kernel_ms = 0.0;
+    if (n == 0) return SMEM_OK;
+    HIP_TRY(hipSetDevice(g->device));
+    DevBuf<smem::KswATask> dt;
+    DevBuf<smem::KswAResult> dr;
+    DevBuf<uint8_t> dq, dtg;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    struct Guard {
+        DevBuf<smem::KswATask>& a; DevBuf<smem::KswAResult>& b; DevBuf<uint8_t>& c; DevBuf<uint8_t>& d;
+        hipStream_t& s; hipEvent_t* e;
+        ~Guard() {
+            a.release(); b.release(); c.release(); d.release();
+            if (e[0]) (void)hipEventDestroy(e[0]);
+            if (e[1]) (void)hipEventDestroy(e[1]);
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } guard{dt, dr, dq, dtg, st, ev};
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&ev[0]));
+    HIP_TRY(hipEventCreate(&ev[1]));
+    HIP_TRY(dt.ensure(n));
+    HIP_TRY(dr.ensure(n));
+    HIP_TRY(dq.ensure(q_bytes + 64));
+    HIP_TRY(dtg.ensure(t_bytes + 64));
+    HIP_TRY(hipMemcpyAsync(dt.p, tasks, sizeof(smem::KswATask) * n, hipMemcpyHostToDevice, st));
+    if (q_bytes) HIP_TRY(hipMemcpyAsync(dq.p, q, q_bytes, hipMemcpyHostToDevice, st));
+    if (t_bytes) HIP_TRY(hipMemcpyAsync(dtg.p, t, t_bytes, hipMemcpyHostToDevice, st));
+    smem::KswAParams K;
+    std::memset(&K, 0, sizeof(K));
+    K.task = dt.p, K.n = n, K.q = dq.p, K.t = dtg.p, K.out = dr.p;
+    std::memcpy(K.mat, opt->mat, 25);
+    K.o_del = opt->o_del, K.e_del = opt->e_del, K.o_ins = opt->o_ins, K.e_ins = opt->e_ins;
+    {  // ksw_qinit's bias and largest score (software/ksw.c:78-85)
+        uint8_t sh = 127, md = 0;
+        for (int k = 0; k < 25; ++k) {
+            if (opt->mat[k] < (int8_t)sh) sh = (uint8_t)opt->mat[k];
+            if (opt->mat[k] > (int8_t)md) md = (uint8_t)opt->mat[k];
+        }
+        K.top = md, K.shift = (uint8_t)(256 - sh);
+    }
+    HIP_TRY(hipEventRecord(ev[0], st));
+    HIP_TRY(smem_launch_ksw_align2(&K, g->n_cu, st));
+    HIP_TRY(hipEventRecord(ev[1], st));
+    HIP_TRY(hipMemcpyAsync(out, dr.p, sizeof(smem::KswAResult) * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    if (kernel_ms) *kernel_ms = ms;
+    return SMEM_OK;
+}
+
 void smem_aln_opt_default(smem_aln_opt_t* o) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
@@ -1016,15 +1117,114 @@ static_assert(sizeof(smem_alnreg_t) == sizeof(smem::AlnReg), "region layout");
 static_assert(sizeof(smem_chain_t) == sizeof(smem::OutChain), "chain layout");
 static_assert(sizeof(smem_seed_t) == sizeof(smem::SeedRec), "seed layout");
 
+// mem_opt_t scoring / extension fields into the kernel parameters
+static void aln_opt_params(const smem_aln_opt_t* opt, smem::AlnParams& P) {
+    std::memcpy(P.mat, opt->sc.mat, 25);
+    P.o_del = opt->sc.o_del, P.e_del = opt->sc.e_del, P.o_ins = opt->sc.o_ins, P.e_ins = opt->sc.e_ins;
+    P.a = opt->a, P.w = opt->w, P.zdrop = opt->zdrop, P.pen_clip5 = opt->pen_clip5, P.pen_clip3 = opt->pen_clip3;
+    P.min_seed_len = opt->min_seed_len;
+    // ksw_qinit's bias and largest score (software/ksw.c:78-85)
+    uint8_t sh = 127, md = 0;
+    for (int k = 0; k < 25; ++k) {
+        if (opt->sc.mat[k] < (int8_t)sh) sh = (uint8_t)opt->sc.mat[k];
+        if (opt->sc.mat[k] > (int8_t)md) md = (uint8_t)opt->sc.mat[k];
+    }
+    P.top = md, P.sw_shift = (uint8_t)(256 - sh);
+}
+
+static int aln_opt_ok(const smem_aln_opt_t* opt) {
+    return opt && opt->sc.e_del >= 1 && opt->sc.e_ins >= 1 && opt->sc.o_del >= 0 && opt->sc.o_ins >= 0 && opt->a >= 1 &&
+           opt->w >= 0;
+}
+
+int smem_gpu_load_pac(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
+    g_err[0] = 0;
+    if (!g || !pac || l_pac <= 0 || 2 * (uint64_t)l_pac != g->L2[4])
+        return fail(SMEM_E_ARG, "smem_gpu_load_pac: pac does not belong to this index (2 l_pac != seq_len)");
+    HIP_TRY(hipSetDevice(g->device));
+    if (g->d_pac) {
+        (void)hipFree(g->d_pac);
+        g->d_pac = nullptr;
+    }
+    const uint64_t bytes = (uint64_t)(l_pac + 3) / 4;
+    hipError_t e = hipMalloc(&g->d_pac, bytes + 64);
+    if (e != hipSuccess) return fail(SMEM_E_NOMEM, "smem_gpu_load_pac: hipMalloc", e);
+    e = hipMemcpy(g->d_pac, pac, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(g->d_pac + bytes, 0, 64);
+    if (e != hipSuccess) return fail(SMEM_E_DEVICE, "smem_gpu_load_pac: upload", e);
+    g->l_pac = l_pac;
+    return SMEM_OK;
+}
+
+int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
+    g_err[0] = 0;
+    if (!b || !b->chain_ran || !b->chain_filtered)
+        return fail(SMEM_E_ARG, "smem_batch_chain2aln: run smem_batch_chain with filter = 1 first");
+    if (!aln_opt_ok(opt)) return fail(SMEM_E_ARG, "smem_batch_chain2aln: scoring needs e >= 1, o >= 0, a >= 1, w >= 0");
+    smem_gpu_t* g = b->g;
+    if (!g->d_pac) return fail(SMEM_E_ARG, "smem_batch_chain2aln: no .pac loaded (smem_gpu_load_pac)");
+    if (b->max_len > 1024) return fail(SMEM_E_ARG, "smem_batch_chain2aln: reads longer than 1024 bp");
+    HIP_TRY(hipSetDevice(g->device));
+    const int n = b->n_reads;
+    const uint64_t ns = std::max<uint64_t>(b->tot_seeds, 1);
+    HIP_TRY(b->d_aln_srt.ensure(ns + 1));
+    HIP_TRY(b->d_aln_raw.ensure(ns + 1));
+    HIP_TRY(b->d_aln_nregs.ensure(std::max(n, 1)));
+    HIP_TRY(b->d_aln_regoff.ensure(n + 1));
+    HIP_TRY(b->d_aln_ctr.ensure(2));
+    size_t tmp = 0;
+    HIP_TRY(smem_launch_offsets(nullptr, nullptr, std::max(n, 1), nullptr, &tmp, b->st));
+    HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
+    smem::AlnParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.codes = b->d_codes.p, P.offs = b->d_offs.p, P.chains = b->d_out_chain.p, P.chain_off = b->d_chain_off.p;
+    P.seeds = b->d_out_seed.p;
+    P.seed_off = b->d_seed_off.p;  // a read's chains' seeds are contiguous: its region capacity
+    P.pac = g->d_pac, P.l_pac = g->l_pac, P.n_reads = n;
+    aln_opt_params(opt, P);
+    P.srt = b->d_aln_srt.p, P.raw = b->d_aln_raw.p, P.n_regs = b->d_aln_nregs.p, P.ctr = b->d_aln_ctr.p;
+    HIP_TRY(hipMemsetAsync(b->d_aln_ctr.p, 0, 2 * sizeof(uint32_t), b->st));
+    HIP_TRY(hipEventRecord(b->ev[0], b->st));
+    HIP_TRY(smem_launch_aln(&P, g->n_cu, b->max_len > 256 ? 1 : 0, b->st));
+    tmp = b->d_sa_tmp.n;
+    HIP_TRY(smem_launch_offsets(b->d_aln_nregs.p, b->d_aln_regoff.p, n, b->d_sa_tmp.p, &tmp, b->st));
+    HIP_TRY(hipMemcpyAsync(b->h_tot.p + 5, b->d_aln_regoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    b->tot_regs = n > 0 ? b->h_tot.p[5] : 0;
+    if (b->tot_regs > b->tot_seeds) return fail(SMEM_E_INTERNAL, "smem_batch_chain2aln: more regions than seeds");
+    HIP_TRY(b->d_aln_out.ensure(std::max<uint64_t>(b->tot_regs, 1)));
+    P.reg_off = b->d_aln_regoff.p, P.out = b->d_aln_out.p;
+    HIP_TRY(smem_launch_aln_write(&P, b->st));
+    HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    HIP_TRY(hipStreamSynchronize(b->st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
+    b->stats.aln_ms = ms;
+    b->stats.n_regs = b->tot_regs;
+    b->aln_ran = true;
+    b->aln_fetched = false;
+    return SMEM_OK;
+}
+
+int smem_batch_aln_results(const smem_batch_t* b, const smem_alnreg_t** regs, const uint64_t** reg_off,
+                           uint64_t* n_regs) {
+    if (!b || !b->aln_fetched) return SMEM_E_ARG;
+    if (regs) *regs = reinterpret_cast<const smem_alnreg_t*>(b->h_aln_regs.p);
+    if (reg_off) *reg_off = b->h_aln_regoff.p;
+    if (n_regs) *n_regs = b->tot_regs;
+    return SMEM_OK;
+}
+
 int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint64_t* offs, const smem_chain_t* chains,
                    const uint64_t* chain_off, const smem_seed_t* seeds, uint64_t n_seeds, const uint8_t* pac,
                    int64_t l_pac, const smem_aln_opt_t* opt, smem_alnreg_t* regs, uint64_t* reg_off,
                    double* kernel_ms) {
     g_err[0] = 0;
-    if (!g || n_reads < 0 || !opt || !reg_off || (n_reads > 0 && (!codes || !offs || !chain_off)) || l_pac <= 0 || !pac)
+    if (!g || n_reads < 0 || !opt || !reg_off || (n_reads > 0 && (!codes || !offs || !chain_off)) || l_pac <= 0)
         return fail(SMEM_E_ARG, "smem_chain2aln: bad arguments");
-    if (opt->sc.e_del < 1 || opt->sc.e_ins < 1 || opt->sc.o_del < 0 || opt->sc.o_ins < 0 || opt->a < 1 || opt->w < 0)
-        return fail(SMEM_E_ARG, "smem_chain2aln: scoring needs e >= 1, o >= 0, a >= 1, w >= 0");
+    if (!pac && !(g->d_pac && g->l_pac == l_pac))
+        return fail(SMEM_E_ARG, "smem_chain2aln: no pac given and none resident for this l_pac (smem_gpu_load_pac)");
+    if (!aln_opt_ok(opt)) return fail(SMEM_E_ARG, "smem_chain2aln: scoring needs e >= 1, o >= 0, a >= 1, w >= 0");
     if (kernel_ms) *kernel_ms = 0.0;
     reg_off[0] = 0;
     if (n_reads == 0) return SMEM_OK;
@@ -1054,6 +1254,18 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     }
     const uint64_t n_bases = offs[n_reads], n_cap = cap[n_reads];
     if (n_cap > 0 && !regs) return fail(SMEM_E_ARG, "smem_chain2aln: no region buffer");
+    // query codes index the 25-entry scoring matrix: 0..4 only
+    for (uint64_t k = offs[0]; k < n_bases; ++k)
+        if (codes[k] > 4) return fail(SMEM_E_ARG, "smem_chain2aln: query code > 4");
+    {   // each chain's seed range is its sort scratch: ranges must not overlap
+        std::vector<std::pair<uint64_t, uint64_t>> rng;
+        rng.reserve(n_chains);
+        for (uint64_t k = 0; k < n_chains; ++k)
+            if (chains[k].n > 0) rng.emplace_back(chains[k].seed_off, chains[k].seed_off + (uint64_t)chains[k].n);
+        std::sort(rng.begin(), rng.end());
+        for (size_t k = 1; k < rng.size(); ++k)
+            if (rng[k].first < rng[k - 1].second) return fail(SMEM_E_ARG, "smem_chain2aln: chains share seeds");
+    }
     HIP_TRY(hipSetDevice(g->device));
     DevBuf<uint8_t> dcodes, dpac;
     DevBuf<uint64_t> doffs, dchoff, dseedoff, dsrt, dnregs, dregoff;
@@ -1082,7 +1294,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     HIP_TRY(hipEventCreate(&ev[1]));
     const uint64_t pac_bytes = (uint64_t)(l_pac + 3) / 4;
     HIP_TRY(dcodes.ensure(n_bases + 64));
-    HIP_TRY(dpac.ensure(pac_bytes + 64));
+    if (pac) HIP_TRY(dpac.ensure(pac_bytes + 64));
     HIP_TRY(doffs.ensure(n_reads + 1));
     HIP_TRY(dchoff.ensure(n_reads + 1));
     HIP_TRY(dseedoff.ensure(n_reads + 1));
@@ -1095,7 +1307,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     HIP_TRY(dout.ensure(n_cap + 1));
     HIP_TRY(dctr.ensure(2));
     if (n_bases) HIP_TRY(hipMemcpyAsync(dcodes.p, codes, n_bases, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(dpac.p, pac, pac_bytes, hipMemcpyHostToDevice, st));
+    if (pac) HIP_TRY(hipMemcpyAsync(dpac.p, pac, pac_bytes, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(doffs.p, offs, 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(dchoff.p, chain_off, 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(dseedoff.p, cap.data(), 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
@@ -1105,19 +1317,8 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     smem::AlnParams P;
     std::memset(&P, 0, sizeof(P));
     P.codes = dcodes.p, P.offs = doffs.p, P.chains = dch.p, P.chain_off = dchoff.p, P.seeds = dseeds.p;
-    P.seed_off = dseedoff.p, P.pac = dpac.p, P.l_pac = l_pac, P.n_reads = n_reads;
-    std::memcpy(P.mat, opt->sc.mat, 25);
-    P.o_del = opt->sc.o_del, P.e_del = opt->sc.e_del, P.o_ins = opt->sc.o_ins, P.e_ins = opt->sc.e_ins;
-    P.a = opt->a, P.w = opt->w, P.zdrop = opt->zdrop, P.pen_clip5 = opt->pen_clip5, P.pen_clip3 = opt->pen_clip3;
-    P.min_seed_len = opt->min_seed_len;
-    {  // ksw_qinit's bias and largest score (software/ksw.c:78-85)
-        uint8_t sh = 127, md = 0;
-        for (int k = 0; k < 25; ++k) {
-            if (opt->sc.mat[k] < (int8_t)sh) sh = (uint8_t)opt->sc.mat[k];
-            if (opt->sc.mat[k] > (int8_t)md) md = (uint8_t)opt->sc.mat[k];
-        }
-        P.top = md, P.sw_shift = (uint8_t)(256 - sh);
-    }
+    P.seed_off = dseedoff.p, P.pac = pac ? dpac.p : g->d_pac, P.l_pac = l_pac, P.n_reads = n_reads;
+    aln_opt_params(opt, P);
     P.srt = dsrt.p, P.raw = draw.p, P.n_regs = dnregs.p, P.ctr = dctr.p;
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));

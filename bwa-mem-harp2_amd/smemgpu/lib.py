@@ -32,6 +32,7 @@ EXPORTED = [
     "smem_chain_opt_default", "smem_batch_chain", "smem_batch_chain_results", "smem_bwt_build_gpu_large",
     "smem_ksw_opt_default", "smem_ksw_extend", "smem_aln_opt_default", "smem_chain2aln",
     "smem_gpu_seed_stream", "smem_batch_results_packed",
+    "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
 ]
 
 
@@ -83,7 +84,8 @@ class OptT(C.Structure):
 class BatchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
                 ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int),
-                ("sa_ms", C.c_double), ("n_occ", C.c_uint64), ("chain_ms", C.c_double), ("n_chains", C.c_uint64)]
+                ("sa_ms", C.c_double), ("n_occ", C.c_uint64), ("chain_ms", C.c_double), ("n_chains", C.c_uint64),
+                ("aln_ms", C.c_double), ("n_regs", C.c_uint64)]
 
 
 class StreamStats(C.Structure):
@@ -161,6 +163,11 @@ def load() -> C.CDLL:
     lib.smem_gpu_collect.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, P(OptT), P(C.c_void_p)]
     lib.smem_gpu_seed_stream.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, P(OptT), C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, C.c_void_p, P(StreamStats)]
+    lib.smem_ksw_align2.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                    P(KswOptT), C.c_void_p, P(C.c_double)]
+    lib.smem_gpu_load_pac.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    lib.smem_batch_chain2aln.argtypes = [C.c_void_p, C.c_void_p]
+    lib.smem_batch_aln_results.argtypes = [C.c_void_p, P(C.c_void_p), P(P(C.c_uint64)), P(C.c_uint64)]
     lib.smem_batch_results_packed.argtypes = [C.c_void_p, P(C.c_void_p), P(P(C.c_uint64)), P(P(C.c_uint32)),
                                               P(P(C.c_uint64))]
     lib.smem_batch_create.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_int, P(C.c_void_p)]
@@ -339,6 +346,8 @@ class Results:
     chains: np.ndarray | None = None   # CHAIN_DT, when Batch.chain() ran
     chain_off: np.ndarray | None = None  # (n_reads + 1,) uint64
     seeds: np.ndarray | None = None    # SEED_DT, each chain's seeds contiguous
+    regs: np.ndarray | None = None     # raw 64-byte smem_alnreg_t records, when Batch.chain2aln() ran
+    reg_off: np.ndarray | None = None  # (n_reads + 1,) uint64
 
     def read_chains(self, i: int) -> list:
         """read i's chains as [(pos, seeds)], in mem_chain(+flt) order."""
@@ -458,25 +467,56 @@ class Gpu:
                                    t.size, C.byref(o), out.ctypes.data, C.byref(ms)), "smem_ksw_extend")
         return out[:tasks.size], ms.value
 
+    def ksw_align2(self, kb) -> tuple:
+        """ksw_align2 (software/ksw.c:342) of every KSWA_TASK of a synth.KswBatch
+        on this device: (results as synth.KSWA_RESULT, kernel ms)."""
+        from . import synth
+        lib = load()
+        tasks = np.ascontiguousarray(kb.tasks, dtype=synth.KSWA_TASK)
+        q = np.ascontiguousarray(kb.q, dtype=np.uint8)
+        t = np.ascontiguousarray(kb.t, dtype=np.uint8)
+        o = KswOptT()
+        for i, v in enumerate(np.asarray(kb.mat, dtype=np.int8)):
+            o.mat[i] = int(v)
+        o.o_del, o.e_del, o.o_ins, o.e_ins = kb.o_del, kb.e_del, kb.o_ins, kb.e_ins
+        out = np.zeros(max(tasks.size, 1), dtype=synth.KSWA_RESULT)
+        ms = C.c_double()
+        _check(lib.smem_ksw_align2(self._h, tasks.size, tasks.ctypes.data, q.ctypes.data, q.size, t.ctypes.data,
+                                   t.size, C.byref(o), out.ctypes.data, C.byref(ms)), "smem_ksw_align2")
+        return out[:tasks.size], ms.value
+
+    def load_pac(self, pac, l_pac: int) -> None:
+        """Keep the 2-bit .pac resident in HBM (smem_gpu_load_pac)."""
+        pac = np.ascontiguousarray(pac, dtype=np.uint8)
+        if pac.size < (l_pac + 3) // 4:
+            raise SmemError("load_pac: pac holds fewer than (l_pac + 3) / 4 bytes")
+        _check(load().smem_gpu_load_pac(self._h, pac.ctypes.data, int(l_pac)), "smem_gpu_load_pac")
+
     def chain2aln(self, pac, l_pac: int, codes, offs, chains, chain_off, seeds, opt) -> tuple:
         """mem_chain2aln_short / mem_chain2aln of every chain of every read
         (software/bwamem.c:1452-1460) on this device.  opt is a ctypes struct
         laid out as smem_aln_opt_t.  Returns (regions as 64-byte smem_alnreg_t
         records, reg_off[n_reads + 1], kernel ms)."""
         lib = load()
-        pac = np.ascontiguousarray(pac, dtype=np.uint8)
+        if pac is not None:
+            pac = np.ascontiguousarray(pac, dtype=np.uint8)
+            if pac.size < (int(l_pac) + 3) // 4:
+                raise SmemError("chain2aln: pac holds fewer than (l_pac + 3) / 4 bytes")
         codes = np.ascontiguousarray(codes, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         chain_off = np.ascontiguousarray(chain_off, dtype=np.uint64)
         chains = np.ascontiguousarray(chains, dtype=CHAIN_DT)
         seeds = np.ascontiguousarray(seeds, dtype=SEED_DT)
+        if chain_off.size != offs.size or (chain_off.size and int(chain_off[-1]) > chains.size):
+            raise SmemError("chain2aln: chain_off must have n_reads + 1 entries within chains")
         n = offs.size - 1
         cap = int(chains["n"].sum()) if chains.size else 0
         regs = np.zeros(max(cap, 1) * 64, dtype=np.uint8)
         reg_off = np.zeros(n + 1, dtype=np.uint64)
         ms = C.c_double()
         _check(lib.smem_chain2aln(self._h, n, codes.ctypes.data, offs.ctypes.data, chains.ctypes.data,
-                                  chain_off.ctypes.data, seeds.ctypes.data, seeds.size, pac.ctypes.data, l_pac,
+                                  chain_off.ctypes.data, seeds.ctypes.data, seeds.size,
+                                  pac.ctypes.data if pac is not None else None, l_pac,
                                   C.byref(opt), regs.ctypes.data, reg_off.ctypes.data, C.byref(ms)), "smem_chain2aln")
         return regs[:int(reg_off[-1]) * 64], reg_off, ms.value
 
@@ -531,6 +571,12 @@ class Batch:
         o = ChainOptT(w, max_chain_gap, mask_level, drop_ratio, int(bool(filter)))
         _check(load().smem_batch_chain(self._h, int(l_pac), C.byref(o)), "smem_batch_chain")
 
+    def chain2aln(self, opt) -> None:
+        """mem_chain2aln_short / mem_chain2aln of every chain of the last
+        chain(filter=True), over the chains in HBM and the resident .pac
+        (smem_batch_chain2aln); opt is laid out as smem_aln_opt_t."""
+        _check(load().smem_batch_chain2aln(self._h, C.byref(opt)), "smem_batch_chain2aln")
+
     def debug_words(self, n_words: int) -> np.ndarray:
         out = np.zeros(n_words, dtype=np.uint64)
         rc = load().smem_batch_debug(self._h, out.ctypes.data, n_words)
@@ -562,6 +608,13 @@ class Batch:
                                        dtype=CHAIN_DT)[:nc].copy()
             res.seeds = np.frombuffer((C.c_char * (max(ns, 1) * SEED_DT.itemsize)).from_address(sd.value),
                                       dtype=SEED_DT)[:ns].copy()
+        rg = C.c_void_p()
+        ro = C.POINTER(C.c_uint64)()
+        nr = C.c_uint64()
+        if lib.smem_batch_aln_results(self._h, C.byref(rg), C.byref(ro), C.byref(nr)) == 0:
+            k = int(nr.value)
+            res.reg_off = np.ctypeslib.as_array(ro, shape=(n + 1,)).copy()
+            res.regs = np.frombuffer((C.c_char * (max(k, 1) * 64)).from_address(rg.value), dtype=np.uint8)[:k * 64].copy()
         return res
 
     def close(self) -> None:

@@ -623,3 +623,101 @@ def read_smkr(data: bytes) -> np.ndarray:
         raise ValueError("not an SMKR file")
     (n,) = struct.unpack_from("<Q", data, 8)
     return np.frombuffer(data, dtype=KSW_RESULT, count=n, offset=16).copy()
+
+
+# ---- ksw_align2 problems (mem_chain2aln_short, software/bwamem.c:805-852) ----
+KSWA_TASK = np.dtype([("q_off", "<u8"), ("t_off", "<u8"), ("qlen", "<i4"), ("tlen", "<i4"), ("xtra", "<i4"),
+                      ("pad", "<i4")])   # smem_ksw_atask_t, 32 B
+KSWA_RESULT = np.dtype([(k, "<i4") for k in ("score", "te", "qe", "score2", "te2", "tb", "qb")])  # kswr_t
+KSW_XBYTE, KSW_XSTOP, KSW_XSUBO, KSW_XSTART = 0x10000, 0x20000, 0x40000, 0x80000
+
+
+def make_kswa_tasks(genome_codes: np.ndarray, n: int, seed: int = 1, a: int = 1, b: int = 4, o: int = 6, e: int = 1,
+                    min_seed_len: int = 19) -> "KswBatch":
+    """ksw_align2 problems shaped like mem_chain2aln_short's: the query span of a
+    chain plus MEM_SHORT_EXT = 50 on both sides (< 200 bp) against the
+    reference span of its seeds plus 50 (lengths within 50 of each other),
+    with substitutions, small indels and Ns; xtra = KSW_XSUBO | KSW_XSTART |
+    (KSW_XBYTE when qlen * a < 250) | min_seed_len * a, as software/bwamem.c:835.
+    Some problems are unrelated sequence, tiny, or run with other flag sets
+    (no start pass, no suboptimal threshold, a threshold above the score)."""
+    rng = np.random.default_rng(seed)
+    G = genome_codes
+    tasks = np.zeros(n, dtype=KSWA_TASK)
+    qs, ts = [], []
+    qo = to = 0
+    for k in range(n):
+        kind = rng.random()
+        if kind < 0.05:      # tiny
+            q = rng.integers(0, 5, size=int(rng.integers(1, 8))).astype(np.uint8)
+            t = rng.integers(0, 5, size=int(rng.integers(0, 10))).astype(np.uint8)
+        elif kind < 0.15:    # unrelated
+            q = rng.integers(0, 4, size=int(rng.integers(20, 200))).astype(np.uint8)
+            t = rng.integers(0, 4, size=int(rng.integers(0, 250))).astype(np.uint8)
+        else:
+            ql = int(rng.integers(60, 200))
+            pos = int(rng.integers(300, G.size - ql - 300))
+            read = _mutated_copy(G[pos:pos + ql], rng, float(rng.choice([0.0, 0.01, 0.03, 0.06])),
+                                 float(rng.choice([0.0, 0.005, 0.02])))[:199]
+            if rng.random() < 0.15:
+                read[rng.random(read.size) < 0.02] = 4
+            d = int(rng.integers(-50, 51))
+            lo = pos - int(rng.integers(0, 40))
+            t = G[lo:lo + max(1, min(256, read.size + d + (pos - lo)))].copy()
+            q = read if read.size else G[pos:pos + 1].copy()
+            if rng.random() < 0.3:   # the reverse strand
+                q = np.where(q < 4, 3 - q, 4)[::-1].astype(np.uint8)
+                t = (3 - t)[::-1].astype(np.uint8)
+        q = q[:199] if q.size else np.zeros(1, np.uint8)
+        t = t[:256]
+        xtra = KSW_XSUBO | KSW_XSTART | (KSW_XBYTE if q.size * a < 250 else 0) | (min_seed_len * a)
+        r = rng.random()
+        if r < 0.05:
+            xtra &= ~KSW_XSTART
+        elif r < 0.10:
+            xtra = KSW_XSTART | (KSW_XBYTE if q.size * a < 250 else 0)
+        elif r < 0.13:
+            xtra = KSW_XSUBO | KSW_XSTART | (KSW_XBYTE if q.size * a < 250 else 0) | 200
+        tasks[k] = (qo, to, q.size, t.size, xtra, 0)
+        qs.append(q)
+        ts.append(t)
+        qo += q.size
+        to += t.size
+    qpool = np.concatenate(qs).astype(np.uint8) if qs else np.zeros(0, np.uint8)
+    tpool = np.concatenate(ts).astype(np.uint8) if ts else np.zeros(0, np.uint8)
+    return KswBatch(tasks, qpool, tpool, bwa_scmat(a, b), o, e, o, e)
+
+
+def write_smat(path: str, b: "KswBatch") -> None:
+    with open(path, "wb") as fh:
+        fh.write(b"SMAT0001")
+        fh.write(struct.pack("<QQQ", b.tasks.size, b.q.size, b.t.size))
+        fh.write(np.asarray(b.mat, dtype=np.int8).tobytes() + b"\0\0\0")
+        fh.write(struct.pack("<4i", b.o_del, b.e_del, b.o_ins, b.e_ins))
+        fh.write(b.tasks.astype(KSWA_TASK).tobytes())
+        fh.write(b.q.astype(np.uint8).tobytes())
+        fh.write(b.t.astype(np.uint8).tobytes())
+
+
+def read_smat(data: bytes) -> "KswBatch":
+    if data[:8] != b"SMAT0001":
+        raise ValueError("not an SMAT file")
+    n, qb, tb = struct.unpack_from("<QQQ", data, 8)
+    o = 32
+    mat = np.frombuffer(data, dtype=np.int8, count=25, offset=o).copy()
+    o += 28
+    o_del, e_del, o_ins, e_ins = struct.unpack_from("<4i", data, o)
+    o += 16
+    tasks = np.frombuffer(data, dtype=KSWA_TASK, count=n, offset=o).copy()
+    o += n * KSWA_TASK.itemsize
+    q = np.frombuffer(data, dtype=np.uint8, count=qb, offset=o).copy()
+    o += qb
+    t = np.frombuffer(data, dtype=np.uint8, count=tb, offset=o).copy()
+    return KswBatch(tasks, q, t, mat, o_del, e_del, o_ins, e_ins)
+
+
+def read_smar(data: bytes) -> np.ndarray:
+    if data[:8] != b"SMAR0001":
+        raise ValueError("not an SMAR file")
+    (n,) = struct.unpack_from("<Q", data, 8)
+    return np.frombuffer(data, dtype=KSWA_RESULT, count=n, offset=16).copy()

@@ -282,6 +282,26 @@ int  smem_ksw_extend(smem_gpu_t *gpu, int n, const smem_ksw_task_t *tasks, const
                      const uint8_t *t, uint64_t t_bytes, const smem_ksw_opt_t *opt, smem_ksw_result_t *out,
                      double *kernel_ms);
 
+/* one ksw_align2 call (software/ksw.c:342) as mem_chain2aln_short makes it
+ * (software/bwamem.c:835-836): xtra = KSW_XSUBO | KSW_XSTART | (KSW_XBYTE when
+ * qlen * a < 250) | min_seed_len * a; query / target offsets into code pools */
+typedef struct {
+	uint64_t q_off, t_off;
+	int32_t qlen, tlen;       /* 1 <= qlen <= 256, 0 <= tlen <= 256 */
+	int32_t xtra, pad;        /* KSW_XBYTE 0x10000, KSW_XSTOP 0x20000, KSW_XSUBO 0x40000, KSW_XSTART 0x80000 */
+} smem_ksw_atask_t;
+/* kswr_t (software/ksw.h:13-15) */
+typedef struct {
+	int32_t score, te, qe, score2, te2, tb, qb;
+} smem_ksw_aresult_t;
+/* ksw_align2 (striped local SW: ksw_u8 with KSW_XBYTE, else ksw_i16; the start
+ * pass with KSW_XSTART) of every task on the GPU, one wave per problem: the
+ * kswr_t the reference returns.  The device routine is the one
+ * smem_chain2aln / smem_batch_chain2aln run for mem_chain2aln_short. */
+int  smem_ksw_align2(smem_gpu_t *gpu, int n, const smem_ksw_atask_t *tasks, const uint8_t *q, uint64_t q_bytes,
+                     const uint8_t *t, uint64_t t_bytes, const smem_ksw_opt_t *opt, smem_ksw_aresult_t *out,
+                     double *kernel_ms);
+
 /* ------------------------------------------- chains -> alignment regions */
 /* mem_alnreg_t (software/bwamem.h:62-74); hash / sub / sub_n / secondary are
  * left 0 here, as mem_chain2aln leaves them (mem_mark_primary sets them later) */
@@ -314,6 +334,22 @@ int  smem_chain2aln(smem_gpu_t *gpu, int n_reads, const uint8_t *codes, const ui
                     const smem_chain_t *chains, const uint64_t *chain_off, const smem_seed_t *seeds, uint64_t n_seeds,
                     const uint8_t *pac, int64_t l_pac, const smem_aln_opt_t *opt, smem_alnreg_t *regs,
                     uint64_t *reg_off, double *kernel_ms);
+/* (pac may be NULL when smem_gpu_load_pac made this l_pac's .pac resident.
+ * Query codes must be 0..4 and no two chains may share seeds: SMEM_E_ARG.) */
+
+/* Keep the 2-bit forward-strand .pac of the uploaded index resident in HBM
+ * (bwa_idx_load's idx->pac, software/bwa.c:325-330); 2 * l_pac must equal the
+ * index's seq_len. */
+int  smem_gpu_load_pac(smem_gpu_t *gpu, const uint8_t *pac, int64_t l_pac);
+/* Device-resident twin of smem_chain2aln: after smem_batch_chain (filter = 1,
+ * as mem_align1_core_batched filters before extending, software/bwamem.c:1414-1422),
+ * mem_chain2aln_short / mem_chain2aln of every chain of every read of the batch
+ * over the reads, chains and seeds still in HBM and the resident .pac: no host
+ * round trip, no per-call allocation once the batch has grown.  smem_batch_fetch
+ * copies the regions; smem_batch_aln_results returns them with reg_off[n_reads + 1]. */
+int  smem_batch_chain2aln(smem_batch_t *b, const smem_aln_opt_t *opt);
+int  smem_batch_aln_results(const smem_batch_t *b, const smem_alnreg_t **regs, const uint64_t **reg_off,
+                            uint64_t *n_regs);
 
 /* ---------------------------------------------------------- telemetry */
 typedef struct {
@@ -327,6 +363,8 @@ typedef struct {
 	uint64_t n_occ;          /* seed occurrences resolved by smem_batch_sa */
 	double chain_ms;         /* smem_batch_chain kernels */
 	uint64_t n_chains;       /* chains kept by smem_batch_chain */
+	double aln_ms;           /* smem_batch_chain2aln kernels */
+	uint64_t n_regs;         /* regions made by smem_batch_chain2aln */
 } smem_batch_stats_t;
 int  smem_batch_stats(const smem_batch_t *b, smem_batch_stats_t *st);
 

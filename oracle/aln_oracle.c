@@ -151,6 +151,21 @@ end_lazy:
 }
 
 /* ksw_align2 (software/ksw.c:342-364) */
+static swr_t sw_align(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const orc_aln_opt_t *o, int xtra);
+
+/* ksw_align2 of one problem, for the tests: out = kswr_t {score, te, qe, score2, te2, tb, qb} */
+void orc_ksw_align2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat, int o_del,
+		int e_del, int o_ins, int e_ins, int xtra, int32_t out[7])
+{
+	orc_aln_opt_t o;
+	swr_t r;
+	memset(&o, 0, sizeof(o));
+	memcpy(o.mat, mat, 25);
+	o.o_del = o_del, o.e_del = e_del, o.o_ins = o_ins, o.e_ins = e_ins;
+	r = sw_align(qlen, query, tlen, target, &o, xtra);
+	out[0] = r.score, out[1] = r.te, out[2] = r.qe, out[3] = r.score2, out[4] = r.te2, out[5] = r.tb, out[6] = r.qb;
+}
+
 static swr_t sw_align(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const orc_aln_opt_t *o, int xtra)
 {
 	const int p = (xtra & XBYTE) ? 16 : 8;

@@ -95,6 +95,9 @@ def load() -> C.CDLL:
         lib.orc_aln_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p]
         lib.orc_aln_batch.restype = C.c_int
+        lib.orc_ksw_align2.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_int, C.POINTER(C.c_int32)]
+        lib.orc_ksw_align2.restype = None
         _lib = lib
     return _lib
 
@@ -333,6 +336,38 @@ def ksw(batch) -> np.ndarray:
     if rc != 0:
         raise RuntimeError("orc_ksw_batch failed")
     return out[:tasks.size]
+
+
+def ksw_align2(batch) -> np.ndarray:
+    """The restatement's ksw_align2 (aln_oracle.c sw_align) of every task of a
+    synth.KswBatch of KSWA_TASK problems, as synth.KSWA_RESULT."""
+    from smemgpu import synth
+    lib = load()
+    mat = np.ascontiguousarray(batch.mat, dtype=np.int8)
+    out = np.zeros(batch.tasks.size, dtype=synth.KSWA_RESULT)
+    r = (C.c_int32 * 7)()
+    for i, t in enumerate(batch.tasks):
+        q = np.ascontiguousarray(batch.q[int(t["q_off"]):int(t["q_off"]) + int(t["qlen"])])
+        tg = np.ascontiguousarray(batch.t[int(t["t_off"]):int(t["t_off"]) + int(t["tlen"])])
+        lib.orc_ksw_align2(int(t["qlen"]), q.ctypes.data, int(t["tlen"]), tg.ctypes.data if tg.size else None,
+                           mat.ctypes.data, batch.o_del, batch.e_del, batch.o_ins, batch.e_ins, int(t["xtra"]), r)
+        out[i] = tuple(r)
+    return out
+
+
+def ref_aln_time(bwt: str, sa: str, pac: str, smrd: str, min_seed_len=19, w=100) -> dict:
+    """The reference's mem_chain + mem_chain_flt + chain2aln loop over a read
+    file (ref_harness aln), returning the time of the chain2aln loop alone."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        p = subprocess.run([REF, "aln", bwt, sa, pac, smrd, os.path.join(d, "o.smrg"), str(min_seed_len), "1.5", "10",
+                            "1", "10000", str(w), "10000", "0.5", "0.5"], check=True, capture_output=True, text=True)
+    line = [l for l in p.stderr.split("\n") if l.startswith("chain2aln_seconds=")][-1]
+    return {k: float(v) for k, v in (t.split("=") for t in line.split())}
+
+
+def ref_kswa(smat: str, out: str) -> None:
+    subprocess.run([REF, "kswa", smat, out], check=True, capture_output=True)
 
 
 def ref_ksw(smkt: str, out: str) -> None:

@@ -32,9 +32,14 @@
  *         <max_chain_gap> <mask_level> <drop_ratio>
  *       mem_chain + mem_chain_flt as for chain (filter on), then per chain
  *       mem_chain2aln_short and, when it declines, mem_chain2aln
- *       (software/bwamem.c:1452-1460); every read's regions written as SMRG:
+ *       (software/bwamem.c:1452-1460); every read's regions written as SMRG (and the
+ *       wall time of the chain2aln loop alone on stderr: "chain2aln_seconds=..."):
  *       "SMRG0001", u64 n_reads, per read u32 n then n x {i64 rb, re;
  *       i32 qb, qe, score, truesc, sub, csub, sub_n, w, seedcov, secondary}.
+ *   kswa  <tasks.smat> <out.smar>
+ *       the reference's own ksw_align2 (software/ksw.c:342) on every task
+ *       (SMAT: as SMKT with per task {u64 q_off, t_off; i32 qlen, tlen, xtra, pad}),
+ *       results as SMAR: "SMAR0001", u64 n, n x i32 {score, te, qe, score2, te2, tb, qb}.
  *   mem   <prefix> <reads.fq> <n_threads> <batch_size> <pe> [<pg>]
  *       The body of the reference's main_mem (software/fastmap.c:193-230) on the
  *       unmodified pipeline: bwa_print_sam_hdr, then bseq_read chunks through
@@ -62,6 +67,7 @@
 #include "bntseq.h"
 #include "kseq.h"
 #include "utils.h"
+#include "ksw.h"
 #include "smem_formats.h"
 KSEQ_DECLARE(gzFile)
 
@@ -337,6 +343,8 @@ static int cmd_aln(int argc, char **argv)
 	uint64_t i;
 	int64_t l_pac;
 	uint8_t *pac;
+	double t_aln = 0.0;
+	uint64_t n_regs = 0;
 	if (argc < 15) {
 		fprintf(stderr, "usage: aln <bwt> <sa> <pac> <reads> <out> <k> <r> <s> <sw> <max_occ> <w> <gap> <mask> <drop>\n");
 		return 1;
@@ -369,9 +377,12 @@ static int cmd_aln(int argc, char **argv)
 		mem_alnreg_v av = { 0, 0, 0 };
 		uint32_t j, n;
 		c.n = mem_chain_flt(opt, (int)c.n, c.a);
+		t_aln -= now_s();
 		for (j = 0; j < c.n; ++j)   /* software/bwamem.c:1452-1460 */
 			if (mem_chain2aln_short(opt, l_pac, pac, r.len[i], q, &c.a[j], &av) > 0)
 				mem_chain2aln(opt, l_pac, pac, r.len[i], q, &c.a[j], &av);
+		t_aln += now_s();
+		n_regs += av.n;
 		n = (uint32_t)av.n;
 		fwrite(&n, 4, 1, out);
 		for (j = 0; j < n; ++j) {
@@ -387,6 +398,9 @@ static int cmd_aln(int argc, char **argv)
 		free(c.a);
 	}
 	fclose(out);
+	/* the chains -> regions loop alone, one thread: the alignment stage's CPU baseline */
+	fprintf(stderr, "chain2aln_seconds=%.6f reads=%llu regions=%llu\n", t_aln, (unsigned long long)r.n_reads,
+			(unsigned long long)n_regs);
 	smrd_free(&r);
 	free(pac);
 	free(opt);
@@ -430,6 +444,43 @@ static int cmd_ksw(int argc, char **argv)
 		r[0] = ksw_extend2(T[i].qlen, q + T[i].q_off, T[i].tlen, t + T[i].t_off, 5, mat, pen[0], pen[1], pen[2], pen[3],
 				T[i].w, T[i].end_bonus, T[i].zdrop, T[i].h0, &r[1], &r[2], &r[3], &r[4], &r[5]);
 		fwrite(r, 4, 6, out);
+	}
+	fclose(out);
+	free(T); free(q); free(t);
+	return 0;
+}
+
+typedef struct { uint64_t q_off, t_off; int32_t qlen, tlen, xtra, pad; } kswa_task_t;
+
+static int cmd_kswa(int argc, char **argv)
+{
+	char magic[8];
+	uint64_t n, qb, tb, i;
+	int8_t mat[28];
+	int32_t pen[4];
+	kswa_task_t *T;
+	uint8_t *q, *t;
+	FILE *fp, *out;
+	if (argc < 3) { fprintf(stderr, "usage: kswa <tasks.smat> <out.smar>\n"); return 1; }
+	fp = fopen(argv[1], "rb");
+	if (!fp) return 1;
+	if (fread(magic, 1, 8, fp) != 8 || memcmp(magic, "SMAT0001", 8) != 0) return 1;
+	if (fread(&n, 8, 1, fp) != 1 || fread(&qb, 8, 1, fp) != 1 || fread(&tb, 8, 1, fp) != 1) return 1;
+	if (fread(mat, 1, 28, fp) != 28 || fread(pen, 4, 4, fp) != 4) return 1;
+	T = malloc(sizeof(kswa_task_t) * (n ? n : 1));
+	q = malloc(qb ? qb : 1);
+	t = malloc(tb ? tb : 1);
+	if (fread(T, sizeof(kswa_task_t), n, fp) != n || fread(q, 1, qb, fp) != qb || fread(t, 1, tb, fp) != tb) return 1;
+	fclose(fp);
+	out = fopen(argv[2], "wb");
+	if (!out) return 1;
+	fwrite("SMAR0001", 1, 8, out);
+	fwrite(&n, 8, 1, out);
+	for (i = 0; i < n; ++i) {
+		kswr_t r = ksw_align2(T[i].qlen, q + T[i].q_off, T[i].tlen, t + T[i].t_off, 5, mat, pen[0], pen[1], pen[2], pen[3],
+				T[i].xtra, 0);
+		int32_t v[7] = { r.score, r.te, r.qe, r.score2, r.te2, r.tb, r.qb };
+		fwrite(v, 4, 7, out);
 	}
 	fclose(out);
 	free(T); free(q); free(t);
@@ -523,6 +574,7 @@ int main(int argc, char **argv)
 	if (strcmp(argv[1], "ksw") == 0) return cmd_ksw(argc - 1, argv + 1);
 	if (strcmp(argv[1], "aln") == 0) return cmd_aln(argc - 1, argv + 1);
 	if (strcmp(argv[1], "mem") == 0) return cmd_mem(argc - 1, argv + 1);
+	if (strcmp(argv[1], "kswa") == 0) return cmd_kswa(argc - 1, argv + 1);
 	fprintf(stderr, "unknown command %s\n", argv[1]);
 	return 1;
 }

@@ -153,6 +153,8 @@ typedef struct {
 } orc_alnreg_t;                      /* mem_alnreg_t, the layout of smem_alnreg_t */
 typedef struct { int64_t pos; uint64_t seed_off; int32_t n, pad; } orc_aln_chain_t;   /* smem_chain_t */
 void orc_sw_shift_top(const int8_t *mat, int *shift, int *top);
+void orc_ksw_align2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat, int o_del,
+		int e_del, int o_ins, int e_ins, int xtra, int32_t out[7]);
 int orc_aln_read(const orc_aln_opt_t *o, int64_t l_pac, const uint8_t *pac, int l_query, const uint8_t *query,
 		int n_chains, const orc_aln_chain_t *chains, const orc_seed_t *seeds, orc_alnreg_t **out);
 int orc_aln_batch(const orc_aln_opt_t *o, int64_t l_pac, const uint8_t *pac, int64_t n_reads, const uint8_t *codes,

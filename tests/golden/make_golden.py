@@ -28,6 +28,9 @@ reference code itself:
     python tests/golden/make_golden.py --chains-only   # (re)make only the g1 .smch files
     python tests/golden/make_golden.py --g2-only       # (re)make only the g2 set
     python tests/golden/make_golden.py --ksw-only      # (re)make only the ksw set
+    python tests/golden/make_golden.py --kswa-only     # (re)make only the ksw_align2 sets
+  kswa_a<1|2>.smat.gz 3000 ksw_align2 problems shaped like mem_chain2aln_short's (a = 1, 2)
+  kswa_a<1|2>.smar.gz the reference's own ksw_align2 on each (software/ksw.c:342)
 """
 import gzip
 import hashlib
@@ -269,6 +272,32 @@ def make_ksw():
         shutil.rmtree(tmp)
 
 
+# ksw_align2 (software/ksw.c:342), the DP of mem_chain2aln_short: mem_opt_init's
+# scoring (a 1, b 4, gaps 6 + 1: byte problems) and -A 2 scaled (a 2, b 8,
+# gaps 12 + 2: queries of 125 bp and more take ksw_i16)
+KSWA_SETS = [("kswa_a1", 1, 4, 6, 1, 151), ("kswa_a2", 2, 8, 12, 2, 152)]
+
+
+def make_kswa():
+    if not oracle.ref_available():
+        oracle.build(ref=True)
+    tmp = tempfile.mkdtemp()
+    try:
+        with gzip.open(os.path.join(HERE, "g1.fa.gz"), "rb") as fh:
+            from tests import golden_data
+            g = golden_data.fasta_codes(fh.read())
+        for name, a, b, o, e, seed in KSWA_SETS:
+            kb = synth.make_kswa_tasks(g, 3000, seed=seed, a=a, b=b, o=o, e=e)
+            p = os.path.join(tmp, name + ".smat")
+            synth.write_smat(p, kb)
+            oracle.ref_kswa(p, os.path.join(tmp, name + ".smar"))
+            for ext in (".smat", ".smar"):
+                with open(os.path.join(tmp, name + ext), "rb") as fh:
+                    gz_write(os.path.join(HERE, name + ext + ".gz"), fh.read())
+    finally:
+        shutil.rmtree(tmp)
+
+
 # chains -> regions (mem_chain2aln_short / mem_chain2aln, software/bwamem.c:805-852,
 # 1040-1188): the reference's own regions for every read of a seeding case,
 # over the chains the matching filtered SMCH fixture holds
@@ -325,6 +354,8 @@ if __name__ == "__main__":
     elif "--ksw-only" in sys.argv:
         make_ksw()
         make_aln()
+    elif "--kswa-only" in sys.argv:
+        make_kswa()
     elif "--chains-only" in sys.argv:
         chains_only()
     elif "--g2-only" in sys.argv:
@@ -333,3 +364,4 @@ if __name__ == "__main__":
         main()
         make_g2()
         make_ksw()
+        make_kswa()

@@ -108,11 +108,15 @@ def test_pack_matches_reference_pac():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w", [100, 20])
-def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w):
+@pytest.mark.parametrize("w,a", [(100, 1), (20, 1), (100, 2)])
+def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a):
     """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
     kernel instantiations) with substitutions and Ns; chains from the GPU
-    chain stage; GPU regions == restatement."""
+    chain stage; GPU regions == restatement, through the host API
+    (smem_chain2aln, explicit .pac and resident .pac) and the device-resident
+    batch stage (smem_batch_chain2aln over the chains left in HBM).  a = 2
+    (-A 2 scaling, b 8, gaps 12 + 2) sends the short path's longer queries
+    through ksw_align2's 16-bit branch."""
     import smemgpu
     from smemgpu import synth
     g = synth.make_genome(600_000, seed=91, repeat_frac=0.6, n_families=5, exact_frac=0.01, tandem_frac=0.01)
@@ -124,23 +128,73 @@ def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w):
                                     synth.make_reads(g.codes, 1000, (70, 250), seed=93, n_rate=0.01, sub_rate=0.03),
                                     synth.make_reads(g.codes, 600, (257, 700), seed=94, sub_rate=0.02),
                                     synth.make_reads(g.codes, 400, 101, seed=95, random_frac=0.3)])
+        opt = oracle.aln_opt(w=w) if a == 1 else oracle.aln_opt(w=w, a=2, b=8, o_del=12, e_del=2, o_ins=12, e_ins=2)
+        pac = _pack(g.codes)
+        l_pac = int(g.codes.size)
+        gpu.load_pac(pac, l_pac)
         b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
         try:
             b.set_reads(reads.codes, reads.offs)
             b.run(smemgpu.Options())
             b.sa(19, 10000)
-            l_pac = int(g.codes.size)
             b.chain(l_pac, w=w)
+            b.chain2aln(opt)   # device-resident: chains, seeds, reads and .pac already in HBM
             res = b.fetch()
             chains, chain_off, seeds = res.chains, res.chain_off, res.seeds
+            assert b.stats()["n_regs"] == int(res.reg_off[-1])
         finally:
             b.close()
-        opt = oracle.aln_opt(w=w)
-        pac = _pack(g.codes)
         raw, off, ms = gpu.chain2aln(pac, l_pac, reads.codes, reads.offs, chains, chain_off, seeds, opt)
+        raw2, off2, _ = gpu.chain2aln(None, l_pac, reads.codes, reads.offs, chains, chain_off, seeds, opt)
     finally:
         gpu.close()
     want, want_off = oracle.aln(pac, l_pac, reads.codes, reads.offs, chains, chain_off, seeds, opt)
     assert want.size > 1000
-    got = np.frombuffer(raw.tobytes(), dtype=golden_data.ALNREG_DT)
-    _assert_same(got, off, want, want_off)
+    for r, o in ((raw, off), (raw2, off2), (res.regs, res.reg_off)):
+        got = np.frombuffer(r.tobytes(), dtype=golden_data.ALNREG_DT)
+        _assert_same(got, o, want, want_off)
+
+
+@pytest.mark.gpu
+def test_aln_gpu_argument_checks(gpu_device):
+    """The host API refuses query codes > 4 (they would index past the scoring
+    matrix), chains sharing seeds (they would share sort scratch), a short
+    .pac and a missing resident .pac; the batch stage needs filtered chains."""
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(50_000, seed=3)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        reads = synth.make_reads(g.codes, 50, 150, seed=4)
+        b = gpu.batch(reads.n, reads.codes.size, 150)
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        b.sa(19, 10000)
+        b.chain(g.codes.size, filter=False)
+        with pytest.raises(smemgpu.SmemError):   # unfiltered chains
+            b.chain2aln(oracle.aln_opt())
+        b.chain(g.codes.size)
+        with pytest.raises(smemgpu.SmemError):   # no resident .pac
+            b.chain2aln(oracle.aln_opt())
+        res = b.fetch()
+        b.close()
+        opt = oracle.aln_opt()
+        pac = _pack(g.codes)
+        l_pac = int(g.codes.size)
+        with pytest.raises(smemgpu.SmemError):   # no pac given, none resident
+            gpu.chain2aln(None, l_pac, reads.codes, reads.offs, res.chains, res.chain_off, res.seeds, opt)
+        with pytest.raises(smemgpu.SmemError):   # short pac
+            gpu.chain2aln(pac[:10], l_pac, reads.codes, reads.offs, res.chains, res.chain_off, res.seeds, opt)
+        bad = reads.codes.copy()
+        bad[5] = 7
+        with pytest.raises(smemgpu.SmemError):   # code > 4
+            gpu.chain2aln(pac, l_pac, bad, reads.offs, res.chains, res.chain_off, res.seeds, opt)
+        ch = res.chains.copy()
+        k = int(np.nonzero(ch["n"] > 0)[0][1])
+        ch["seed_off"][k] = ch["seed_off"][int(np.nonzero(ch["n"] > 0)[0][0])]
+        with pytest.raises(smemgpu.SmemError):   # chains sharing seeds
+            gpu.chain2aln(pac, l_pac, reads.codes, reads.offs, ch, res.chain_off, res.seeds, opt)
+    finally:
+        gpu.close()
