@@ -422,7 +422,15 @@ __device__ __forceinline__ uint64_t stamp() {
 }
 
 // STAMP: diagnostic build only (variant 9) — per-wave cycle split written to P.dbg_buf
-template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false>
+// FRING: the forward list goes to the LDS list slots too, as a ring of the
+// last NLIST pushes (an older entry is written to the arena when the ring
+// wraps), so that the first backward step reads prev[0 .. NLIST) from LDS and
+// only longer forward lists touch HBM.  List index k < NLIST of every list of
+// one bwt_smem1 call then lives in slot (R - k) mod NLIST, R = the slot of the
+// last forward push (prev[0]): curr[k] still overwrites prev[k] only after it
+// was read.
+template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
+          bool FRING = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -464,6 +472,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // list beyond its first NL entries (which live in LDS).  curr is written in
     // place over prev: curr[k] is pushed after prev[j >= k] has been read.
     uint32_t fwd_n = 0, prev_off = 0, prev_n = 0, curr_n = 0;
+    // FRING: the ring position (forward phase), then the slot of list index 0
+    uint32_t lr = 0;
+    constexpr bool RING = FRING && NL > 0;
     bool prev_lds = false;  // prev is the backward list (LDS + region 2), not the forward list
     uint32_t mem_n = 0, mem_last_start = 0, m_n = 0;
     uint64_t curr_last_x2 = 0;
@@ -482,6 +493,23 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     if constexpr (STAMP) st_t0 = rtstamp();
 
 #define QBLK(pos) ((o0 + (uint32_t)(pos)) & ~15u)
+// one forward-list push: the arena (pushed downward: ascending order is the
+// reversed list) or, RING, the LDS ring, spilling the entry it displaces
+#define FWD_PUSH(e_)                                                                        \
+    {                                                                                       \
+        const uint4 fe_ = (e_);                                                             \
+        if constexpr (RING) {                                                               \
+            if (fwd_n >= (uint32_t)NL)                                                      \
+                *reinterpret_cast<uint4*>(bp + cap - 1 - (fwd_n - NL)) = WLs->e[lr][vlane()]; \
+            WLs->e[lr][vlane()] = fe_;                                                      \
+            lr = lr + 1 == (uint32_t)NL ? 0u : lr + 1;                                      \
+        } else {                                                                            \
+            *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = fe_;                          \
+        }                                                                                   \
+        ++fwd_n;                                                                            \
+    }
+// the LDS slot of list index k (< NL) of the current bwt_smem1 call
+#define LSLOT(r_, k_) (RING ? ((r_) >= (k_) ? (r_) - (k_) : (r_) + (uint32_t)NL - (k_)) : (k_))
 #define YIELD_FOR(pos)            \
     {                             \
         qwant = QBLK(pos);        \
@@ -638,6 +666,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
                         ikend = (uint32_t)(x + 1);
                         fwd_n = 0;
+                        lr = 0;
                         i = x + 1;
                         phase = P_FWD;
                     }
@@ -679,7 +708,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     } else if (curr_n == 0 || ns != curr_last_x2) {
                         const uint4 e = pack_p(na, nb, ns, ikend);
                         if (NL > 0 && curr_n < (uint32_t)NL)
-                            WLs->e[curr_n][vlane()] = e;
+                            WLs->e[LSLOT(lr, curr_n)][vlane()] = e;
                         else
                             *reinterpret_cast<uint4*>(bp + cap + curr_n) = e;
                         if (curr_n == 0) head = e;  // prev[0] of the next step
@@ -714,8 +743,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (phase == P_FWD_RES) {  // software/bwt.c:795-799; na = x[1], nb = x[0]
                 bool stop = false;
                 if (ns != ik2) {
-                    *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = pack_p(ik0, ik1, ik2, ikend);
-                    ++fwd_n;
+                    FWD_PUSH(pack_p(ik0, ik1, ik2, ikend));
                     stop = ns < (uint64_t)min_intv;
                 }
                 if (stop) {
@@ -746,8 +774,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     }
                 }
                 if (push) {  // ambiguous base, or end of query: push ik and stop
-                    *reinterpret_cast<uint4*>(bp + cap - 1 - fwd_n) = pack_p(ik0, ik1, ik2, ikend);
-                    ++fwd_n;
+                    FWD_PUSH(pack_p(ik0, ik1, ik2, ikend));
                     phase = P_FWD_DONE;
                 }
             }
@@ -758,7 +785,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 ret = (int)ikend;
                 prev_off = cap - fwd_n;  // pushed downward: ascending = reversed
                 prev_n = fwd_n;
-                prev_lds = false;
+                prev_lds = RING;         // RING: prev[0 .. NL) in the LDS ring
+                if constexpr (RING) lr = lr == 0 ? (uint32_t)NL - 1 : lr - 1;  // slot of the last push
                 i = x - 1;
                 phase = P_BWD_STEP;
             }
@@ -836,7 +864,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 const uint32_t nidle = (uint32_t)__popcll(idle);
                 const int me = vlane();
                 const uint32_t r = (uint32_t)__popcll(idle & ((1ull << me) - 1));
-                uint32_t base = 0, he = 0, hpoff = 0;
+                uint32_t base = 0, he = 0, hpoff = 0, hlr = 0;
                 int ho = -1, hplds = 0;
                 while (elig && base < nidle) {
                     // o is wave-uniform: its state is read with v_readlane (valid
@@ -848,6 +876,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     const uint32_t poff_o = __builtin_amdgcn_readlane((int)prev_off, o);
                     const int plds_o = __builtin_amdgcn_readlane((int)prev_lds, o);
                     const int c_o = __builtin_amdgcn_readlane(cur_c, o);
+                    const uint32_t lr_o = RING ? __builtin_amdgcn_readlane((int)lr, o) : 0u;
                     const uint32_t m = min(nidle - base, pno - jo - 1);
                     const bool mine = phase == P_EXIT && r >= base && r < base + m;
                     if (mine) {
@@ -856,6 +885,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         hc = c_o;
                         hpoff = poff_o;
                         hplds = plds_o;
+                        hlr = lr_o;
                     }
                     const uint64_t hmask = __ballot(mine);
                     if (me == o) {
@@ -869,7 +899,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     // the owner's list: its first NL entries in LDS (after the first
                     // step), the rest in its arena; prev_off / prev_lds are per owner
                     if (NL > 0 && hplds && he < (uint32_t)NL) {
-                        hent = WLs->e[he][ho];
+                        hent = WLs->e[LSLOT(hlr, he)][ho];
                     } else {
                         const PIntv* obp = reinterpret_cast<const PIntv*>(
                             P.scratch + ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + ho) * 2ull * cap);
@@ -916,7 +946,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         }
         if (ld_pn) pn = W->pn[vlane()];
         if constexpr (NL > 0) {  // prev[pidx] from the LDS list: read here, off the advance's critical path
-            if (phase == P_BWD_RES && prev_lds && pidx < prev_n && pidx < (uint32_t)NL) pn = WLs->e[pidx][vlane()];
+            if (phase == P_BWD_RES && prev_lds && pidx < prev_n && pidx < (uint32_t)NL)
+                pn = WLs->e[LSLOT(lr, pidx)][vlane()];
         }
         if (ld_q) {
             qv = W->q[vlane()];
@@ -942,6 +973,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             st_comp += stamp() - tc;
         }
     }
+#undef FWD_PUSH
+#undef LSLOT
     if constexpr (STAMP) {
         st_t1 = rtstamp();
         if (lane == 0 && P.dbg_buf) {
@@ -1046,9 +1079,13 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 8: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 10: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 11: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 12: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 13: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+        // default (2): Occ64, 7 list entries in LDS, the forward list in the LDS ring
+        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }

@@ -376,7 +376,9 @@ int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement:
  * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
  * device at init), per-lane LDS-DMA fetch with bucket reuse, the first 7
- * backward-list entries per lane in LDS; 3 reference-layout buckets,
+ * entries of every list in LDS (the forward list as a ring of its last 7
+ * pushes); 11 = 2; 12 the same with 12 LDS entries at 2 blocks per CU; 13 the
+ * round-1 default (forward list in the arena); 3 reference-layout buckets,
  * cooperative fetch, lists in global memory; 4 reference layout, per-lane
  * fetch; 5 as 2 with 12 list entries in LDS (2 blocks per CU); 6 as 2 with
  * lists in global memory; 9 the default with per-wave cycle stamps

@@ -212,6 +212,7 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 		ik.info = (uint64_t)(i + 1);
 	}
 	if (i == len) iv_push(&w->fwd, &ik);
+	w->st.n_fwd_push += w->fwd.n;
 	iv_reverse(&w->fwd);                 /* longest match first (software/bwt.c:806) */
 	ret = (int)w->fwd.a[0].info;
 
@@ -224,6 +225,7 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 		had_u1 = has_u1; has_u1 = 0;
 		for (j = 0; j < (int)prev->n; ++j) {
 			orc_intv_t *p = &prev->a[j];
+			if (i < x - 1 && j >= 7) w->st.n_bwd_read_hi++;
 			orc_extend(b, p, ok, 1);
 			count_extend(b, p, 1, c >= 0, &w->st);
 			if (c >= 0) { int sl = (int)(uint32_t)p->info - i; w->st.n_ext_len[sl < 32 ? sl : 32]++; }
@@ -241,6 +243,7 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 					iv_push(mem, &e);
 				}
 			} else if (curr->n == 0 || ok[c].x[2] != curr->a[curr->n - 1].x[2]) {
+				if (curr->n >= 7) w->st.n_bwd_push_hi++;
 				ok[c].info = p->info;
 				iv_push(curr, &ok[c]);
 			}
@@ -383,6 +386,7 @@ static void add_stats(orc_stats_t *d, const orc_stats_t *s)
 	d->n_ext_fwd += s->n_ext_fwd; d->n_ext_u1_fwd += s->n_ext_u1_fwd; d->n_ext_u1_bwd += s->n_ext_u1_bwd;
 	d->n_run_u1 += s->n_run_u1; d->n_ext_fwd_k12 += s->n_ext_fwd_k12;
 	{ int k; for (k = 0; k < 33; ++k) d->n_ext_len[k] += s->n_ext_len[k]; }
+	d->n_fwd_push += s->n_fwd_push; d->n_bwd_push_hi += s->n_bwd_push_hi; d->n_bwd_read_hi += s->n_bwd_read_hi;
 }
 
 int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,

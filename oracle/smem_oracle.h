@@ -58,6 +58,9 @@ typedef struct {
 	uint64_t n_run_u1;      /* maximal runs of size-1 extends of one interval (fwd or bwd) */
 	uint64_t n_ext_fwd_k12; /* forward extends at depth i - x < 12 with no N before them */
 	uint64_t n_ext_len[33]; /* used extends by the length of the string they produce (32 = 32 or more) */
+	uint64_t n_fwd_push;    /* forward-list pushes (software/bwt.c:798, 801, 804) */
+	uint64_t n_bwd_push_hi; /* backward-list (curr) pushes at index >= 7 */
+	uint64_t n_bwd_read_hi; /* backward-list (prev, steps >= 2) reads at index >= 7 */
 } orc_stats_t;
 
 orc_bwt_t *orc_bwt_load(const char *fn);

@@ -146,18 +146,24 @@ def test_few_lanes_many_reads_per_lane(world, gpu_device):
         gpu.close()
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 6, 9, 10])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 9, 10, 11, 12, 13])
 def test_kernel_variants(world, gpu_device, variant):
-    """The A/B builds (reference-layout fetches, stamped) are bit-exact too."""
+    """The A/B builds (reference-layout fetches, stamped, forward-list LDS
+    ring) are bit-exact too."""
     import smemgpu
     gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant)
     try:
-        reads = _reads(world["genome"], "mixed", seed=11)
-        for opt in (OPTS["default"], OPTS["reseed"]):
+        reads = synth_concat(_reads(world["genome"], "mixed", seed=11), _reads(world["genome"], "250bp5", seed=12))
+        for opt in ((OPTS["default"], OPTS["reseed"]) if variant < 11 else OPTS.values()):
             want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4, **opt)
             assert smemgpu.seed(gpu, reads.codes, reads.offs, smemgpu.Options(**opt)).to_smgo() == want
     finally:
         gpu.close()
+
+
+def synth_concat(*parts):
+    from smemgpu import synth
+    return synth.concat_reads(list(parts))
 
 
 def test_batch_reuse(world):
