@@ -289,7 +289,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 13))) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 21))) return SMEM_E_ARG;
     if (variant == 10 && !g->d_occ192) {
         // the Occ192 layout (variant 10 only), built from Occ64 on first use
         std::lock_guard<std::mutex> lk(g->mu);

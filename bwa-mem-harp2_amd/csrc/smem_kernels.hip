@@ -128,6 +128,11 @@ struct WaveLdsT {
     uint4 pn[64];
     uint4 q[64];
 };
+template <>
+struct WaveLdsT<0> {  // VSLOT: the bucket slots live in registers
+    uint4 pn[64];
+    uint4 q[64];
+};
 
 // the backward-list entries kept in LDS, per wave [entry][lane].  A separate
 // __shared__ object from the LDS-DMA targets above, so the compiler can see
@@ -386,6 +391,36 @@ __device__ __forceinline__ void fetch_occ64_issue(const uint32_t* __restrict__ o
     }
 }
 
+// The same slot policy with the two slots in registers (VSLOT): the missing
+// buckets are loaded straight into s0 / s1 (the lanes that hit keep theirs)
+__device__ __forceinline__ void fetch_occ64_issue_regs(const uint32_t* __restrict__ occ, uint64_t kk, uint64_t ll,
+                                                       uint32_t& t0, uint32_t& t1, int& ks, int& ls, uint4& s0a,
+                                                       uint4& s0b, uint4& s1a, uint4& s1b) {
+    const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
+    const bool needl = bk != bl;
+    ks = bk == t0 ? 0 : (bk == t1 ? 1 : -1);
+    ls = !needl ? ks : (bl == t0 ? 0 : (bl == t1 ? 1 : -1));
+    const bool kmiss = ks < 0, lmiss = needl && ls < 0;
+    if (kmiss) ks = (needl && ls == 0) ? 1 : 0;  // keep the slot l hits
+    if (!needl) ls = ks;
+    else if (lmiss) ls = ks ^ 1;
+    const bool f0 = (kmiss && ks == 0) || (lmiss && ls == 0);
+    const bool f1 = (kmiss && ks == 1) || (lmiss && ls == 1);
+    const uint32_t b0 = (kmiss && ks == 0) ? bk : bl, b1 = (kmiss && ks == 1) ? bk : bl;
+    if (f0) {
+        const uint4* c = reinterpret_cast<const uint4*>(boff(occ, b0 >> 1, (b0 & 1) * 8));
+        s0a = c[0];
+        s0b = c[1];
+        t0 = b0;
+    }
+    if (f1) {
+        const uint4* c = reinterpret_cast<const uint4*>(boff(occ, b1 >> 1, (b1 & 1) * 8));
+        s1a = c[0];
+        s1b = c[1];
+        t1 = b1;
+    }
+}
+
 // after the wait: the lane's k and l buckets from its slots
 template <class WL>
 __device__ __forceinline__ void fetch_occ64_read(WL* W, int ks, int ls, Bucket32& vk, Bucket32& vl) {
@@ -429,12 +464,23 @@ __device__ __forceinline__ uint64_t stamp() {
 // one bwt_smem1 call then lives in slot (R - k) mod NLIST, R = the slot of the
 // last forward push (prev[0]): curr[k] still overwrites prev[k] only after it
 // was read.
+// DUAL: a lane in a backward step with two or more entries left extends
+// prev[j] and prev[j+1] in the same iteration (the entries of one step are
+// independent, software/bwt.c:812-826) and consumes both results in order
+// next iteration: half the iterations -- state-machine passes and memory
+// round trips -- for the multi-entry steps.  The second extend's buckets
+// come from the lane's LDS slots when the first fetched them, else straight
+// into registers.
+// VSLOT: the two bucket slots per lane in registers instead of LDS (4 KB of
+// LDS per wave back for list entries); with DUAL the second extend is issued
+// only when both its buckets are in the slots after the first one's fetch.
 template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
-          bool FRING = false>
+          bool FRING = false, bool DUAL = false, bool VSLOT = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
-    using WaveLds = WaveLdsT<FETCH == FETCH_OCC64 ? 4 : 8>;
+    constexpr bool VS = VSLOT && FETCH == FETCH_OCC64 && !L192 && !EARLY;
+    using WaveLds = WaveLdsT<VS ? 0 : (FETCH == FETCH_OCC64 ? 4 : 8)>;
     __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
     __shared__ WaveListT<NL> lists[4];
     __shared__ uint32_t scnt[STAMP ? 4 : 1][16];  // STAMP: per-wave block-execution counts
@@ -475,6 +521,12 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // FRING: the ring position (forward phase), then the slot of list index 0
     uint32_t lr = 0;
     constexpr bool RING = FRING && NL > 0;
+    constexpr bool DU = DUAL && RING && NL > 1 && FETCH == FETCH_OCC64 && !EARLY && !L192;
+    bool dq = false;                    // DU: the lane's request covers prev[j] and prev[j + 1]
+    uint4 pn2 = {0, 0, 0, 0};           // DU: prev[j + 1] for the next request
+    uint4 ent2 = {0, 0, 0, 0};          // DU: the second entry of the current request
+    uint64_t na2 = 0, nb2 = 0, ns2 = 0; // DU: its result
+    uint4 s0a = {0, 0, 0, 0}, s0b = {0, 0, 0, 0}, s1a = {0, 0, 0, 0}, s1b = {0, 0, 0, 0};  // VS: the slots
     bool prev_lds = false;  // prev is the backward list (LDS + region 2), not the forward list
     uint32_t mem_n = 0, mem_last_start = 0, m_n = 0;
     uint64_t curr_last_x2 = 0;
@@ -675,10 +727,14 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (phase == P_BWD_RES) {  // software/bwt.c:815-825; na = x[0], nb = x[1]
                 // the lane's own result for prev[j], then (helped owner only) the
                 // results idle lanes computed for prev[j+1 .. j+bat_m], in order
-                const int nres = 1 + bat_m;
+                const int own = DU && dq ? 2 : 1;
+                const int nres = own + bat_m;
                 uint64_t hm = bat_h;
                 for (int r = 0; r < nres; ++r) {
-                    if (r > 0) {
+                    if (DU && r == 1 && own == 2) {  // the lane's own second result, prev[j + 1]
+                        ik0 = p_x0(ent2); ik1 = p_x1(ent2); ik2 = p_x2(ent2); ikend = p_end(ent2);
+                        na = na2; nb = nb2; ns = ns2;
+                    } else if (r > 0) {
                         const int h = __builtin_ctzll(hm);
                         hm &= hm - 1;
                         const uint4 ent = W->pn[h], res = W->q[h];
@@ -721,6 +777,10 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     if ((uint32_t)j < prev_n) {  // extend prev[j] (read into pn last iteration) right away
                         ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
                         out = true;
+                        if constexpr (DU) {  // and prev[j + 1] (in pn2) with it
+                            dq = (uint32_t)j + 1 < prev_n;
+                            ent2 = pn2;
+                        }
                         if constexpr (FETCH == FETCH_OCC64 && EARLY) {
                             // issue its bucket fetch now: it overlaps the rest of the pass
                             const uint64_t k = ik0 - 1, l = k + ik2;
@@ -804,6 +864,10 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         if (i > 0) qwant = QBLK(i - 1);  // the next step's base
                         phase = P_BWD_RES;  // -> extend prev[0]; prev[1] is fetched meanwhile
                         out = true;
+                        if constexpr (DU) {  // prev[1] is in its LDS slot (ring or last step's curr)
+                            dq = prev_n > 1;
+                            if (dq) ent2 = WLs->e[LSLOT(lr, 1u)][vlane()];
+                        }
                     } else {
                         // nothing extends: prev[0] is the only candidate
                         phase = P_SMEM_END;
@@ -844,6 +908,19 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             st_active += __popcll(__ballot(want));
         }
         if (!__any(live)) break;
+        // DU with VS: the second extend is kept only when both its buckets are
+        // the first extend's (no extra loads); otherwise prev[j + 1] waits for
+        // the next iteration.  Decided before the helpers and the prefetch
+        // index, which depend on it.
+        if constexpr (DU && VS) {
+            if (dq && phase == P_BWD_RES && out) {
+                const uint64_t k1 = ik0 - 1, l1 = k1 + ik2;
+                const uint32_t b1k = (uint32_t)((k1 - (k1 >= P.primary)) >> 6), b1l = (uint32_t)((l1 - (l1 >= P.primary)) >> 6);
+                const uint64_t k2 = p_x0(ent2) - 1, l2 = k2 + p_x2(ent2);
+                const uint32_t b2k = (uint32_t)((k2 - (k2 >= P.primary)) >> 6), b2l = (uint32_t)((l2 - (l2 >= P.primary)) >> 6);
+                dq = (b2k == b1k || b2k == b1l) && (b2l == b1k || b2l == b1l);
+            }
+        }
         // Lanes that found the work queue empty help: when the wave has idle
         // lanes and a lane in a backward step with more entries left, each idle
         // lane extends one of those entries (same base, independent of each
@@ -860,7 +937,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (idle) {
                 // owners in lane order take the idle lanes in rank order, each as
                 // many as it has entries left in its step
-                uint64_t elig = __ballot(phase == P_BWD_RES && (uint32_t)j + 1 < prev_n);
+                uint64_t elig = __ballot(phase == P_BWD_RES && (uint32_t)j + 1 + (DU && dq ? 1u : 0u) < prev_n);
                 const uint32_t nidle = (uint32_t)__popcll(idle);
                 const int me = vlane();
                 const uint32_t r = (uint32_t)__popcll(idle & ((1ull << me) - 1));
@@ -877,11 +954,12 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     const int plds_o = __builtin_amdgcn_readlane((int)prev_lds, o);
                     const int c_o = __builtin_amdgcn_readlane(cur_c, o);
                     const uint32_t lr_o = RING ? __builtin_amdgcn_readlane((int)lr, o) : 0u;
-                    const uint32_t m = min(nidle - base, pno - jo - 1);
+                    const uint32_t dq_o = DU ? (uint32_t)__builtin_amdgcn_readlane((int)dq, o) : 0u;
+                    const uint32_t m = min(nidle - base, pno - jo - 1 - dq_o);
                     const bool mine = phase == P_EXIT && r >= base && r < base + m;
                     if (mine) {
                         ho = o;
-                        he = jo + 1 + (r - base);
+                        he = jo + 1 + dq_o + (r - base);
                         hc = c_o;
                         hpoff = poff_o;
                         hplds = plds_o;
@@ -915,7 +993,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         // prev[j+1] (the owner of a helped batch: prev[j+1+bat_m]) and the query
         // window land in LDS slots (no VGPR-destination load the compiler would
         // wait on right away); read back after the wait
-        const uint32_t pidx = (uint32_t)j + 1 + (uint32_t)bat_m;
+        const uint32_t pidx = (uint32_t)j + 1 + (DU && dq ? 1u : 0u) + (uint32_t)bat_m;
         const bool ld_pn = phase == P_BWD_RES && pidx < prev_n && !(NL > 0 && prev_lds && pidx < (uint32_t)NL);
         const bool ld_q = qwant != qb && qwant != ~0u;
         if (ld_pn)
@@ -935,10 +1013,59 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
         Bucket vk, vl;
         Bucket32 wk, wl;
-        if constexpr (FETCH == FETCH_OCC64) {
+        // DU: the second extend (prev[j + 1], same base) and the next pn2
+        const bool want2 = DU && want && !helper && phase == P_BWD_RES && dq;
+        uint64_t ra2 = 0, rb2 = 0, rs2 = 0, kk2 = 0, ll2 = 0;
+        int s_k2 = -1, s_l2 = -1;
+        uint4 v2k0 = {0, 0, 0, 0}, v2k1 = {0, 0, 0, 0}, v2l0 = {0, 0, 0, 0}, v2l1 = {0, 0, 0, 0};
+        const bool ld_pn2 = DU && phase == P_BWD_RES && pidx + 1 < prev_n;
+        const bool pn2_lds = NL > 0 && prev_lds && pidx + 1 < (uint32_t)NL;
+        uint4 pn2_g = {0, 0, 0, 0};
+        if constexpr (DU) {
+            if (ld_pn2 && !pn2_lds) pn2_g = *reinterpret_cast<const uint4*>(bp + prev_off + pidx + 1);
+        }
+        if constexpr (VS) {
+            if (want) fetch_occ64_issue_regs(P.occ64, kk, ll, tag0, tag1, fks, fls, s0a, s0b, s1a, s1b);
+            if constexpr (DU) {
+                if (want2) {
+                    ra2 = p_x0(ent2), rb2 = p_x1(ent2), rs2 = p_x2(ent2);
+                    const uint64_t k2 = ra2 - 1, l2 = k2 + rs2;
+                    kk2 = k2 - (k2 >= P.primary), ll2 = l2 - (l2 >= P.primary);
+                    const uint32_t bk2 = (uint32_t)(kk2 >> 6), bl2 = (uint32_t)(ll2 >> 6);
+                    s_k2 = bk2 == tag0 ? 0 : 1;  // both are in the slots (checked above)
+                    s_l2 = bl2 == tag0 ? 0 : 1;
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int ks = fks < 0 ? 0 : fks, ls = fls < 0 ? 0 : fls;
+            wk = ks == 0 ? Bucket32{s0a, s0b} : Bucket32{s1a, s1b};
+            wl = ls == 0 ? Bucket32{s0a, s0b} : Bucket32{s1a, s1b};
+        } else if constexpr (FETCH == FETCH_OCC64) {
             // lanes whose fetch was not issued early in BWD_RES issue it now
             if (want && !early)
                 fetch_occ64_issue<WaveLds, L192>(L192 ? P.occ192 : P.occ64, W, kk, ll, tag0, tag1, fks, fls);
+            if constexpr (DU) {
+                if (want2) {
+                    ra2 = p_x0(ent2), rb2 = p_x1(ent2), rs2 = p_x2(ent2);
+                    const uint64_t k2 = ra2 - 1, l2 = k2 + rs2;
+                    kk2 = k2 - (k2 >= P.primary), ll2 = l2 - (l2 >= P.primary);
+                    const uint32_t bk2 = (uint32_t)(kk2 >> 6), bl2 = (uint32_t)(ll2 >> 6);
+                    s_k2 = bk2 == tag0 ? 0 : (bk2 == tag1 ? 1 : -1);
+                    s_l2 = bl2 == tag0 ? 0 : (bl2 == tag1 ? 1 : (bl2 == bk2 ? 2 : -1));
+                    if (s_k2 < 0) {
+                        const uint32_t *c0, *c1;
+                        block_chunks<false>(P.occ64, bk2, c0, c1);
+                        v2k0 = *reinterpret_cast<const uint4*>(c0);
+                        v2k1 = *reinterpret_cast<const uint4*>(c1);
+                    }
+                    if (s_l2 < 0) {
+                        const uint32_t *c0, *c1;
+                        block_chunks<false>(P.occ64, bl2, c0, c1);
+                        v2l0 = *reinterpret_cast<const uint4*>(c0);
+                        v2l1 = *reinterpret_cast<const uint4*>(c1);
+                    }
+                }
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             fetch_occ64_read(W, fks, fls, wk, wl);
         } else {
@@ -949,6 +1076,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (phase == P_BWD_RES && prev_lds && pidx < prev_n && pidx < (uint32_t)NL)
                 pn = WLs->e[LSLOT(lr, pidx)][vlane()];
         }
+        if constexpr (DU) {
+            if (ld_pn2) pn2 = pn2_lds ? WLs->e[LSLOT(lr, pidx + 1)][vlane()] : pn2_g;
+        }
         if (ld_q) {
             qv = W->q[vlane()];
             qb = qwant;
@@ -957,6 +1087,23 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         if constexpr (STAMP) {
             tc = stamp();
             st_fetch += tc - tb;
+        }
+        if constexpr (DU && VS) {
+            if (want2) {
+                const Bucket32 wk2 = s_k2 == 0 ? Bucket32{s0a, s0b} : Bucket32{s1a, s1b};
+                const Bucket32 wl2 = s_l2 == 0 ? Bucket32{s0a, s0b} : Bucket32{s1a, s1b};
+                extend_counts64<false>(P, ra2, rb2, rs2, cur_c, kk2, ll2, wk2, wl2, na2, nb2, ns2);
+            }
+        } else if constexpr (DU) {
+            if (want2) {
+                const int lane2 = vlane();
+                const Bucket32 wk2 = s_k2 >= 0 ? Bucket32{W->img[2 * s_k2][lane2], W->img[2 * s_k2 + 1][lane2]}
+                                               : Bucket32{v2k0, v2k1};
+                const Bucket32 wl2 = s_l2 == 2 ? wk2
+                                     : s_l2 >= 0 ? Bucket32{W->img[2 * s_l2][lane2], W->img[2 * s_l2 + 1][lane2]}
+                                                 : Bucket32{v2l0, v2l1};
+                extend_counts64<false>(P, ra2, rb2, rs2, cur_c, kk2, ll2, wk2, wl2, na2, nb2, ns2);
+            }
         }
         if (want) {
             if constexpr (FETCH == FETCH_OCC64)
@@ -1079,13 +1226,23 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 8: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 10: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 11: the first round-2 layout (LDS bucket slots, 7 list entries, forward ring)
         case 11: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 12: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 17: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 18: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 13, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 19: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 20: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 21: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 7, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 16: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 14: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 15: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 3, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 13: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
-        // default (2): Occ64, 7 list entries in LDS, the forward list in the LDS ring
-        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // default (2): Occ64, the two bucket slots per lane in registers, 11 list
+        // entries per lane in LDS (the forward list as a ring of its last 11 pushes)
+        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }

@@ -375,10 +375,14 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement:
  * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
- * device at init), per-lane LDS-DMA fetch with bucket reuse, the first 7
- * entries of every list in LDS (the forward list as a ring of its last 7
- * pushes); 11 = 2; 12 the same with 12 LDS entries at 2 blocks per CU; 13 the
- * round-1 default (forward list in the arena); 3 reference-layout buckets,
+ * device at init), per-lane fetch into two register slots with bucket reuse,
+ * the first 11 entries of every list in LDS (the forward list as a ring of its
+ * last 11 pushes); 11 the same with LDS-DMA slots and 7 list entries; 12 that
+ * with 12 LDS entries at 2 blocks per CU; 13 the round-1 default (LDS-DMA
+ * slots, 7 entries, forward list in the arena); 16-18 variant 11 with two
+ * backward extends per lane per iteration (16; 17/18 at 2 blocks per CU with
+ * 12/13 entries); 19 the default with two extends when both hit the slots;
+ * 20 = 2; 21 register slots, 7 entries, 4 blocks per CU; 3 reference-layout buckets,
  * cooperative fetch, lists in global memory; 4 reference layout, per-lane
  * fetch; 5 as 2 with 12 list entries in LDS (2 blocks per CU); 6 as 2 with
  * lists in global memory; 9 the default with per-wave cycle stamps
