@@ -26,8 +26,8 @@ smem_gpu_seed_stream (chunks staged into pinned memory, H2D, seeding, D2H of
 every interval into pinned memory, several workers overlapping) -- reported
 beside `value`, never as it.  --config c3/c4/c5 stream the north_star's
 target sizes (12.5M pairs = one GPU's shard of C3's 100M pairs, 10M x 250 bp,
-10M x 150 bp at 5 %); `value` stays the device-resident rate on a 1M-read
-batch of the same reads.
+10M x 150 bp at 5 %; c2 streams 4M); `value` stays the device-resident rate
+on a 1M-read batch of the same reads.
 
 roofline: dominant kernel = seed_kernel.  achieved = algorithmic bytes per
 launch (64 B x distinct Occ buckets per extend + read length
@@ -65,8 +65,8 @@ BLOCK = 1 << 18          # reads per block of the read stream (shards are whole 
 
 # BASELINE.json configs: per-GPU shapes
 CONFIGS = {
-    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=0,
-               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1])"),
+    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=4_000_000,
+               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1]); 4M streamed"),
     "c3": dict(read_len=150, sub=0.02, k=19, pairs=True, stream_reads=25_000_000,
                what="C3 on one GPU: its shard of 100M x 150 bp PE on 8 GPUs = 12.5M pairs, insert N(500, 50), "
                     "mates interleaved in one chunk"),

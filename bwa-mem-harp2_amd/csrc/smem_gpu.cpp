@@ -1405,7 +1405,7 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
         if (!bs[w]) rc = smem_batch_create(g, want_reads, max_bases, max_len, &bs[w]);
     std::atomic<int64_t> next{0};
     std::atomic<int> err{SMEM_OK};
-    std::atomic<uint64_t> n_intv{0}, h2d{0}, d2h{0};
+    std::atomic<uint64_t> n_intv{0}, h2d{0}, d2h{0}, t_stage{0}, t_run{0}, t_fetch{0};
     std::mutex emu;
     std::string emsg;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1417,9 +1417,16 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
             if (c >= n_chunks || err.load() != SMEM_OK) break;
             const int64_t a = c * chunk_reads, e = std::min<int64_t>(n_reads, a + chunk_reads);
             const int n = (int)(e - a);
+            const auto c0 = std::chrono::steady_clock::now();
             int r = smem_batch_set_reads_packed(b, n, codes, offs + a);
+            const auto c1 = std::chrono::steady_clock::now();
             if (!r) r = smem_batch_run(b, opt);
+            const auto c2 = std::chrono::steady_clock::now();
             if (!r) r = smem_batch_fetch(b);
+            const auto c3 = std::chrono::steady_clock::now();
+            t_stage += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(c1 - c0).count();
+            t_run += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(c2 - c1).count();
+            t_fetch += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(c3 - c2).count();
             if (!r) {
                 n_intv += b->tot_intv;
                 h2d += (offs[e] - offs[a]) + 8ull * (uint64_t)(n + 1);
@@ -1465,6 +1472,9 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
         stats->h2d_bytes = h2d.load();
         stats->d2h_bytes = d2h.load();
         stats->workers = nw;
+        stats->stage_s = t_stage.load() * 1e-6;
+        stats->run_s = t_run.load() * 1e-6;
+        stats->fetch_s = t_fetch.load() * 1e-6;
     }
     return SMEM_OK;
 }

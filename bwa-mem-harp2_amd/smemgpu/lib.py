@@ -91,7 +91,8 @@ class BatchStats(C.Structure):
 class StreamStats(C.Structure):
     """smem_stream_stats_t"""
     _fields_ = [("wall_s", C.c_double), ("n_reads", C.c_uint64), ("n_chunks", C.c_uint64), ("n_intv", C.c_uint64),
-                ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64), ("workers", C.c_int)]
+                ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64), ("workers", C.c_int), ("stage_s", C.c_double),
+                ("run_s", C.c_double), ("fetch_s", C.c_double)]
 
 
 # int (*smem_chunk_fn)(void *ctx, int64_t chunk, int64_t first_read, int n_reads, const smem_batch_t *b)

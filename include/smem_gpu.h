@@ -161,6 +161,7 @@ typedef struct {
 	uint64_t h2d_bytes;      /* reads + offsets copied host -> device */
 	uint64_t d2h_bytes;      /* intervals + list sizes + offsets copied device -> host */
 	int workers;
+	double stage_s, run_s, fetch_s;  /* summed over chunks: staging + H2D issue, smem_batch_run, smem_batch_fetch */
 } smem_stream_stats_t;
 int  smem_gpu_seed_stream(smem_gpu_t *gpu, int64_t n_reads, const uint8_t *codes, const uint64_t *offs,
                           const smem_opt_t *opt, int chunk_reads, int n_workers, int flags, smem_chunk_fn fn,

@@ -67,7 +67,9 @@ def main():
             s, _ = gpu.seed_stream(reads.codes, reads.offs, opt, chunk_reads=c, workers=w, pairs=a.pairs, packed=pk)
             print(json.dumps({"packed": pk, "chunk": c, "workers": w, "reads_per_s": round(s["n_reads"] / s["wall_s"], 1),
                               "wall_s": round(s["wall_s"], 3), "d2h_GB": round(s["d2h_bytes"] / 1e9, 2),
-                              "d2h_GBps_eff": round(s["d2h_bytes"] / s["wall_s"] / 1e9, 1)}), flush=True)
+                              "d2h_GBps_eff": round(s["d2h_bytes"] / s["wall_s"] / 1e9, 1),
+                              "stage_s": round(s["stage_s"], 3), "run_s": round(s["run_s"], 3),
+                              "fetch_s": round(s["fetch_s"], 3)}), flush=True)
     gpu.close()
 
 
