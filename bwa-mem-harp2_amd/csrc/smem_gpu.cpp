@@ -289,8 +289,8 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 21))) return SMEM_E_ARG;
-    if (variant == 10 && !g->d_occ192) {
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 22))) return SMEM_E_ARG;
+    if ((variant == 10 || variant == 22) && !g->d_occ192) {
         // the Occ192 layout (variant 10 only), built from Occ64 on first use
         std::lock_guard<std::mutex> lk(g->mu);
         HIP_TRY(hipSetDevice(g->device));

@@ -393,6 +393,7 @@ __device__ __forceinline__ void fetch_occ64_issue(const uint32_t* __restrict__ o
 
 // The same slot policy with the two slots in registers (VSLOT): the missing
 // buckets are loaded straight into s0 / s1 (the lanes that hit keep theirs)
+template <bool L192 = false>
 __device__ __forceinline__ void fetch_occ64_issue_regs(const uint32_t* __restrict__ occ, uint64_t kk, uint64_t ll,
                                                        uint32_t& t0, uint32_t& t1, int& ks, int& ls, uint4& s0a,
                                                        uint4& s0b, uint4& s1a, uint4& s1b) {
@@ -408,15 +409,17 @@ __device__ __forceinline__ void fetch_occ64_issue_regs(const uint32_t* __restric
     const bool f1 = (kmiss && ks == 1) || (lmiss && ls == 1);
     const uint32_t b0 = (kmiss && ks == 0) ? bk : bl, b1 = (kmiss && ks == 1) ? bk : bl;
     if (f0) {
-        const uint4* c = reinterpret_cast<const uint4*>(boff(occ, b0 >> 1, (b0 & 1) * 8));
-        s0a = c[0];
-        s0b = c[1];
+        const uint32_t *a0, *a1;
+        block_chunks<L192>(occ, b0, a0, a1);
+        s0a = *reinterpret_cast<const uint4*>(a0);
+        s0b = *reinterpret_cast<const uint4*>(a1);
         t0 = b0;
     }
     if (f1) {
-        const uint4* c = reinterpret_cast<const uint4*>(boff(occ, b1 >> 1, (b1 & 1) * 8));
-        s1a = c[0];
-        s1b = c[1];
+        const uint32_t *a0, *a1;
+        block_chunks<L192>(occ, b1, a0, a1);
+        s1a = *reinterpret_cast<const uint4*>(a0);
+        s1b = *reinterpret_cast<const uint4*>(a1);
         t1 = b1;
     }
 }
@@ -479,7 +482,7 @@ template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EA
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
-    constexpr bool VS = VSLOT && FETCH == FETCH_OCC64 && !L192 && !EARLY;
+    constexpr bool VS = VSLOT && FETCH == FETCH_OCC64 && !EARLY;
     using WaveLds = WaveLdsT<VS ? 0 : (FETCH == FETCH_OCC64 ? 4 : 8)>;
     __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
     __shared__ WaveListT<NL> lists[4];
@@ -1025,7 +1028,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (ld_pn2 && !pn2_lds) pn2_g = *reinterpret_cast<const uint4*>(bp + prev_off + pidx + 1);
         }
         if constexpr (VS) {
-            if (want) fetch_occ64_issue_regs(P.occ64, kk, ll, tag0, tag1, fks, fls, s0a, s0b, s1a, s1b);
+            if (want)
+                fetch_occ64_issue_regs<L192>(L192 ? P.occ192 : P.occ64, kk, ll, tag0, tag1, fks, fls, s0a, s0b, s1a, s1b);
             if constexpr (DU) {
                 if (want2) {
                     ra2 = p_x0(ent2), rb2 = p_x1(ent2), rs2 = p_x2(ent2);
@@ -1236,6 +1240,7 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 19: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 20: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 21: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 7, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 22: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, true, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 16: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 14: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 15: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 3, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
