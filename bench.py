@@ -97,6 +97,8 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu", help="index construction (same bytes)")
     p.add_argument("--lanes-per-cu", type=int, default=0)
+    p.add_argument("--variant", type=int, default=0, help="seeding kernel variant (smem_gpu_set_kernel_variant)")
+    p.add_argument("--kmer-k", type=int, default=0, help="k-mer bi-interval table of 1..K bases (variant 23)")
     p.add_argument("--streams", type=int, default=2, help="host workers, each with its own batch and HIP stream")
     p.add_argument("--stream-reads", type=int, default=None,
                    help="reads per GPU pushed through the streaming path (default: the config's; c2: the resident reads)")
@@ -574,7 +576,7 @@ def main():
 
     idx, idx_path, sa, genome_codes = get_index(args, rank, barrier, d.gpu)
     reads = make_reads(args, rank, genome_codes, world)
-    gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu)
+    gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu, variant=args.variant, kmer_k=args.kmer_k)
     gpu.load_sa(sa)
     # one batch object (own HIP stream, own buffers) per host worker, each
     # holding the whole read set: a step is one full pass over the reads

@@ -112,6 +112,8 @@ struct smem_gpu {
     uint32_t* d_bwt = nullptr;      // reference layout (variants 3, 4)
     uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
     uint32_t* d_occ192 = nullptr;   // Occ192 layout (variant 10)
+    uint4* d_kt = nullptr;          // k-mer bi-interval table (smem_gpu_set_kmer_table; variant 23)
+    int kt_k = 0;
     uint64_t* d_sa = nullptr;       // sampled SA (smem_gpu_load_sa), n_sa + 1 words
     uint8_t* d_pac = nullptr;       // 2-bit forward strand (smem_gpu_load_pac)
     int64_t l_pac = 0;
@@ -273,8 +275,6 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
     if (e != hipSuccess) {
         (void)hipFree(g->d_bwt);
         if (g->d_occ64) (void)hipFree(g->d_occ64);
-    if (g->d_occ192) (void)hipFree(g->d_occ192);
-        if (g->d_occ192) (void)hipFree(g->d_occ192);
         delete g;
         return fail(SMEM_E_DEVICE, "smem_gpu_init: Occ64 layout", e);
     }
@@ -289,7 +289,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 22))) return SMEM_E_ARG;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 23))) return SMEM_E_ARG;
     if ((variant == 10 || variant == 22) && !g->d_occ192) {
         // the Occ192 layout (variant 10 only), built from Occ64 on first use
         std::lock_guard<std::mutex> lk(g->mu);
@@ -307,6 +307,33 @@ int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
         g->d_occ192 = p;
     }
     g->variant = variant == 0 ? 2 : variant;
+    return SMEM_OK;
+}
+
+int smem_gpu_set_kmer_table(smem_gpu_t* g, int k) {
+    g_err[0] = 0;
+    if (!g || k < 0 || k > 15) return fail(SMEM_E_ARG, "smem_gpu_set_kmer_table: k must be 0..15");
+    std::lock_guard<std::mutex> lk(g->mu);
+    HIP_TRY(hipSetDevice(g->device));
+    if (g->d_kt) {
+        HIP_TRY(hipDeviceSynchronize());  // no batch may still read it
+        (void)hipFree(g->d_kt);
+        g->d_kt = nullptr;
+        g->kt_k = 0;
+    }
+    if (k == 0) return SMEM_OK;
+    const uint64_t n = ((1ull << (2 * (k + 1))) - 4) / 3;  // levels 1..k
+    uint4* p = nullptr;
+    hipError_t e = hipMalloc(&p, n * sizeof(uint4));
+    if (e != hipSuccess) return fail(SMEM_E_NOMEM, "smem_gpu_set_kmer_table: hipMalloc", e);
+    e = smem_launch_kmer_table(g->d_occ64, g->primary, g->L2, k, p, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return fail(SMEM_E_DEVICE, "smem_gpu_set_kmer_table: build", e);
+    }
+    g->d_kt = p;
+    g->kt_k = k;
     return SMEM_OK;
 }
 
@@ -353,6 +380,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     if (g->d_bwt) (void)hipFree(g->d_bwt);
     if (g->d_occ64) (void)hipFree(g->d_occ64);
     if (g->d_occ192) (void)hipFree(g->d_occ192);
+    if (g->d_kt) (void)hipFree(g->d_kt);
     if (g->d_sa) (void)hipFree(g->d_sa);
     if (g->d_pac) (void)hipFree(g->d_pac);
     delete g;
@@ -469,6 +497,8 @@ static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& 
     P.bwt = b->g->d_bwt;
     P.occ64 = b->g->d_occ64;
     P.occ192 = b->g->d_occ192;
+    P.kt = b->g->d_kt;
+    P.kt_k = b->g->kt_k;
     P.primary = b->g->primary;
     std::memcpy(P.L2, b->g->L2, sizeof(P.L2));
     P.codes = b->d_codes.p;
@@ -519,6 +549,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->stats.grid = grid;
     HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
+    if (g->variant == 23 && !g->d_kt) return fail(SMEM_E_ARG, "smem_batch_run: variant 23 needs smem_gpu_set_kmer_table");
     if (g->variant == 9) {
         HIP_TRY(b->d_dbg.ensure((size_t)grid * 4 * 32));
         HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, (size_t)grid * 4 * 32 * sizeof(uint64_t), b->st));

@@ -46,6 +46,8 @@ struct SeedParams {
     uint32_t cap_list;
     int dbg;                   // debug switches (0 in production)
     uint64_t* dbg_buf;         // stamped diagnostic variant: 8 x u64 per wave
+    const uint4* kt;           // k-mer bi-interval table (smem_launch_kmer_table; variant 23), nullptr: none
+    int kt_k;                  // its longest k-mer
 };
 
 // bwt_sa over the seeding output (software/bwamem.c:462-474, software/bwt.c:104-114)
@@ -96,6 +98,11 @@ hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int 
 // reference interleaved words (n_ref_buckets x 64 B) -> 2 * n_ref_buckets 32-B buckets
 hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32_t* out, hipStream_t st);
 hipError_t smem_launch_occ192(const uint32_t* occ64, uint64_t n_blocks, uint32_t* out, hipStream_t st);
+// the bi-intervals of every string of 1..k bases (k <= 15): table L at entry
+// (4^L - 4) / 3, index = the string's 2-bit codes, first base highest; 16-B
+// packed entries (x0, x1, x2 low words, bits 32-33 in word 3), x2 = 0 when absent
+hipError_t smem_launch_kmer_table(const uint32_t* occ64, uint64_t primary, const uint64_t* L2, int k, uint4* kt,
+                                  hipStream_t st);
 hipError_t smem_launch_finalize(const smem::FinalizeParams* F, int write, hipStream_t st);
 hipError_t smem_launch_fill_i32(int32_t* p, int32_t v, int n, hipStream_t st);
 hipError_t smem_launch_pack_intv(const smem::Intv* in, uint64_t n, uint4* out, hipStream_t st);

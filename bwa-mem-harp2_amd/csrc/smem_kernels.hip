@@ -72,7 +72,7 @@ struct PIntv {
     uint32_t x0, x1, x2, hi;  // hi = x0>>32 | x1>>32 << 2 | x2>>32 << 4 | end << 6
 };
 
-__device__ __forceinline__ uint4 pack_p(uint64_t x0, uint64_t x1, uint64_t x2, uint32_t end) {
+__host__ __device__ __forceinline__ uint4 pack_p(uint64_t x0, uint64_t x1, uint64_t x2, uint32_t end) {
     return make_uint4((uint32_t)x0, (uint32_t)x1, (uint32_t)x2,
                       (uint32_t)(x0 >> 32) | (uint32_t)(x1 >> 32) << 2 | (uint32_t)(x2 >> 32) << 4 | end << 6);
 }
@@ -477,12 +477,19 @@ __device__ __forceinline__ uint64_t stamp() {
 // VSLOT: the two bucket slots per lane in registers instead of LDS (4 KB of
 // LDS per wave back for list entries); with DUAL the second extend is issued
 // only when both its buckets are in the slots after the first one's fetch.
+// KT: an extend whose result is a string of at most P.kt_k bases reads that
+// string's bi-interval from the k-mer table (one 16-B probe, no rank) instead
+// of two Occ buckets: a bi-interval is a function of the string alone, so the
+// result is the one bwt_extend computes.  The lane keeps the 2-bit codes of
+// its forward string (first kt_k bases) and, in the backward phase, of the
+// kt_k bases from the current position (rolled one base per step).
 template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
-          bool FRING = false, bool DUAL = false, bool VSLOT = false>
+          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
     constexpr bool VS = VSLOT && FETCH == FETCH_OCC64 && !EARLY;
+    constexpr bool KT = KTAB && VS && !DUAL;
     using WaveLds = WaveLdsT<VS ? 0 : (FETCH == FETCH_OCC64 ? 4 : 8)>;
     __shared__ WaveLds lds[4];  // one per wave of the 256-thread block
     __shared__ WaveListT<NL> lists[4];
@@ -530,6 +537,10 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     uint4 ent2 = {0, 0, 0, 0};          // DU: the second entry of the current request
     uint64_t na2 = 0, nb2 = 0, ns2 = 0; // DU: its result
     uint4 s0a = {0, 0, 0, 0}, s0b = {0, 0, 0, 0}, s1a = {0, 0, 0, 0}, s1b = {0, 0, 0, 0};  // VS: the slots
+    // KT: codes of the forward string (its first K bases), of the requested
+    // forward string, and of the K bases from backward position i
+    uint32_t kc = 0, kreq = 0, kb = 0;
+    const int K = KT ? P.kt_k : 0;
     bool prev_lds = false;  // prev is the backward list (LDS + region 2), not the forward list
     uint32_t mem_n = 0, mem_last_start = 0, m_n = 0;
     uint64_t curr_last_x2 = 0;
@@ -720,6 +731,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         ik2 = lq1 - lq;
                         ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
                         ikend = (uint32_t)(x + 1);
+                        if constexpr (KT) kc = (uint32_t)qx;
                         fwd_n = 0;
                         lr = 0;
                         i = x + 1;
@@ -814,6 +826,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 } else {
                     ik0 = nb; ik1 = na; ik2 = ns;
                     ikend = (uint32_t)(i + 1);
+                    if constexpr (KT) {
+                        if (i + 1 - x <= K) kc = kreq;  // saturates at the first K bases
+                    }
                     ++i;
                     phase = P_FWD;
                 }
@@ -829,6 +844,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                         const int qi = qsel(o0, i, qv);
                         if (qi < 4) {
                             cur_c = 3 - qi;
+                            if constexpr (KT) kreq = kc << 2 | (uint32_t)qi;
                             if (i + 1 < len) qwant = QBLK(i + 1);
                             phase = P_FWD_RES;  // -> extend (forward)
                             out = true;
@@ -850,6 +866,10 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 prev_n = fwd_n;
                 prev_lds = RING;         // RING: prev[0 .. NL) in the LDS ring
                 if constexpr (RING) lr = lr == 0 ? (uint32_t)NL - 1 : lr - 1;  // slot of the last push
+                if constexpr (KT) {  // the K bases from x (those past the forward string are never read)
+                    const uint32_t lf = ikend - (uint32_t)x;
+                    kb = lf >= (uint32_t)K ? kc : kc << (2 * ((uint32_t)K - lf));
+                }
                 i = x - 1;
                 phase = P_BWD_STEP;
             }
@@ -864,6 +884,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     if (cur_c >= 0) {
                         j = 0;
                         ik0 = p_x0(pn); ik1 = p_x1(pn); ik2 = p_x2(pn); ikend = p_end(pn);
+                        if constexpr (KT) kb = (uint32_t)cur_c << (2 * (K - 1)) | kb >> 2;
                         if (i > 0) qwant = QBLK(i - 1);  // the next step's base
                         phase = P_BWD_RES;  // -> extend prev[0]; prev[1] is fetched meanwhile
                         out = true;
@@ -1027,8 +1048,20 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         if constexpr (DU) {
             if (ld_pn2 && !pn2_lds) pn2_g = *reinterpret_cast<const uint4*>(bp + prev_off + pidx + 1);
         }
+        // KT: the result string's length and codes; a short one is one table probe
+        bool ktp = false;
+        uint4 ktv = {0, 0, 0, 0};
+        if constexpr (KT) {
+            const int lq = fwd ? i + 1 - x : (int)ikend - i;
+            ktp = want && !helper && lq <= K;
+            if (ktp) {
+                const uint32_t code = fwd ? kreq : kb >> (2 * (K - lq));
+                const uint64_t base = ((1ull << (2 * lq)) - 4) / 3;
+                ktv = P.kt[base + code];
+            }
+        }
         if constexpr (VS) {
-            if (want)
+            if (want && !ktp)
                 fetch_occ64_issue_regs<L192>(L192 ? P.occ192 : P.occ64, kk, ll, tag0, tag1, fks, fls, s0a, s0b, s1a, s1b);
             if constexpr (DU) {
                 if (want2) {
@@ -1109,7 +1142,11 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 extend_counts64<false>(P, ra2, rb2, rs2, cur_c, kk2, ll2, wk2, wl2, na2, nb2, ns2);
             }
         }
-        if (want) {
+        if (ktp) {  // forward: na is the x[1] side (ik1), backward: the x[0] side
+            na = fwd ? p_x1(ktv) : p_x0(ktv);
+            nb = fwd ? p_x0(ktv) : p_x1(ktv);
+            ns = p_x2(ktv);
+        } else if (want) {
             if constexpr (FETCH == FETCH_OCC64)
                 extend_counts64<L192>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
             else
@@ -1241,6 +1278,8 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 20: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 21: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 7, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 22: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, true, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 23: the default with the k-mer table (P->kt)
+        case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 16: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 14: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 15: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 3, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
@@ -1333,6 +1372,32 @@ __global__ __launch_bounds__(256) void occ64_kernel(const uint32_t* __restrict__
 }  // namespace smem
 
 namespace smem {
+// k-mer table level L from level L - 1: one thread per (L-1)-mer W extends
+// its bi-interval backward by each base c (bwt_extend, software/bwt.c:416-429)
+// and writes cW's entry at index c << 2(L-1) | code(W)
+__global__ __launch_bounds__(256) void kmer_table_kernel(SeedParams P, uint4* __restrict__ kt, int L) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n_par = 1ull << (2 * (L - 1));
+    if (w >= n_par) return;
+    const uint4* par = kt + ((1ull << (2 * (L - 1))) - 4) / 3;
+    uint4* lev = kt + ((1ull << (2 * L)) - 4) / 3;
+    const uint4 e = par[w];
+    const uint64_t a = p_x0(e), b = p_x1(e), s = p_x2(e);
+    if (s == 0) {  // absent string: so are its extensions
+        for (int c = 0; c < 4; ++c) lev[(uint64_t)c << (2 * (L - 1)) | w] = make_uint4(0, 0, 0, 0);
+        return;
+    }
+    const uint64_t k = a - 1, l = k + s;
+    const uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
+    const uint4* o = reinterpret_cast<const uint4*>(P.occ64);  // block b: o[2b] counts, o[2b + 1] symbols
+    const Bucket32 vk{o[2 * (kk >> 6)], o[2 * (kk >> 6) + 1]}, vl{o[2 * (ll >> 6)], o[2 * (ll >> 6) + 1]};
+    for (int c = 0; c < 4; ++c) {
+        uint64_t na, nb, ns;
+        extend_counts64<false>(P, a, b, s, c, kk, ll, vk, vl, na, nb, ns);
+        lev[(uint64_t)c << (2 * (L - 1)) | w] = ns ? pack_p(na, nb, ns, 0) : make_uint4(0, 0, 0, 0);
+    }
+}
+
 // Occ64 -> Occ192 (see rank192); one thread per 64-B line of 192 symbols
 __global__ __launch_bounds__(256) void occ192_kernel(const uint32_t* __restrict__ occ64, uint64_t n_blocks,
                                                       uint64_t n_lines, uint32_t* __restrict__ out) {
@@ -1364,6 +1429,27 @@ __global__ __launch_bounds__(256) void occ192_kernel(const uint32_t* __restrict_
     w[3] = sym[2];
 }
 }  // namespace smem
+
+extern "C" hipError_t smem_launch_kmer_table(const uint32_t* occ64, uint64_t primary, const uint64_t* L2, int k,
+                                              uint4* kt, hipStream_t st) {
+    if (k < 1 || k > 15) return hipErrorInvalidValue;
+    smem::SeedParams P;
+    memset(&P, 0, sizeof(P));
+    P.occ64 = occ64;
+    P.primary = primary;
+    for (int c = 0; c < 5; ++c) P.L2[c] = L2[c];
+    uint4 lev1[4];  // bwt_set_intv (software/bwt.h:80)
+    for (int c = 0; c < 4; ++c)
+        lev1[c] = smem::pack_p(L2[c] + 1, L2[3 - c] + 1, L2[c + 1] - L2[c], 0);
+    hipError_t e = hipMemcpyAsync(kt, lev1, sizeof(lev1), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);  // lev1 is on this stack
+    for (int L = 2; L <= k && e == hipSuccess; ++L) {
+        const uint64_t n = 1ull << (2 * (L - 1));
+        hipLaunchKernelGGL(smem::kmer_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, kt, L);
+        e = hipGetLastError();
+    }
+    return e;
+}
 
 extern "C" hipError_t smem_launch_occ192(const uint32_t* occ64, uint64_t n_blocks, uint32_t* out, hipStream_t st) {
     const uint64_t n_lines = (n_blocks + 2) / 3;

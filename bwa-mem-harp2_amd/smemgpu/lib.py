@@ -25,7 +25,7 @@ EXPORTED = [
     "smem_gpu_device_count", "smem_gpu_init", "smem_gpu_shutdown", "smem_gpu_collect",
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
-    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_batch_debug", "smem_strerror",
+    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_gpu_set_kmer_table", "smem_batch_debug", "smem_strerror",
     "smem_gpu_build_id",
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
@@ -184,6 +184,7 @@ def load() -> C.CDLL:
     lib.smem_gpu_set_lanes_per_cu.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_set_intv_cap.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_set_kernel_variant.argtypes = [C.c_void_p, C.c_int]
+    lib.smem_gpu_set_kmer_table.argtypes = [C.c_void_p, C.c_int]
     if hasattr(lib, "smem_batch_debug"):  # absent from older A/B builds
         lib.smem_batch_debug.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     lib.smem_strerror.argtypes = [C.c_int]
@@ -397,7 +398,8 @@ class Results:
 class Gpu:
     """One HIP device with the index resident in HBM (smem_gpu_init)."""
 
-    def __init__(self, index: Index, device: int = 0, lanes_per_cu: int = 0, intv_cap: int = 0, variant: int = 0):
+    def __init__(self, index: Index, device: int = 0, lanes_per_cu: int = 0, intv_cap: int = 0, variant: int = 0,
+                 kmer_k: int = 0):
         lib = load()
         self._h = C.c_void_p()
         words = index.words
@@ -408,9 +410,19 @@ class Gpu:
             _check(lib.smem_gpu_set_lanes_per_cu(self._h, lanes_per_cu), "smem_gpu_set_lanes_per_cu")
         if intv_cap:
             _check(lib.smem_gpu_set_intv_cap(self._h, intv_cap), "smem_gpu_set_intv_cap")
+        if kmer_k:
+            self.set_kmer_table(kmer_k)
         if variant:
             _check(lib.smem_gpu_set_kernel_variant(self._h, variant), "smem_gpu_set_kernel_variant")
         self.device = device
+
+    def set_variant(self, variant: int) -> None:
+        """Seeding-kernel variant (0 = default; see smem_gpu_set_kernel_variant)."""
+        _check(load().smem_gpu_set_kernel_variant(self._h, variant), "smem_gpu_set_kernel_variant")
+
+    def set_kmer_table(self, k: int) -> None:
+        """Build (k = 1..15) or free (0) the device k-mer bi-interval table."""
+        _check(load().smem_gpu_set_kmer_table(self._h, k), "smem_gpu_set_kmer_table")
 
     def load_sa(self, sa: "SA") -> None:
         _check(load().smem_gpu_load_sa(self._h, C.byref(sa._raw)), "smem_gpu_load_sa")

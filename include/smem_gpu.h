@@ -388,8 +388,16 @@ int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
  * fetch; 5 as 2 with 12 list entries in LDS (2 blocks per CU); 6 as 2 with
  * lists in global memory; 9 the default with per-wave cycle stamps
  * (smem_batch_debug); 10 the default on the Occ192 layout (64-B lines of
- * 192 symbols, built on first use: exact, 7 % slower at human size) */
+ * 192 symbols, built on first use: exact, 7 % slower at human size); 22
+ * register slots on Occ192; 23 the default reading the bi-interval of every
+ * extend result of at most k bases from the k-mer table (needs
+ * smem_gpu_set_kmer_table) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
+/* build (k = 1..15) or free (k = 0) the device table of the bi-intervals of
+ * every string of 1..k bases, built on the device from the resident index:
+ * 16 B x (4^(k+1) - 4) / 3 (k = 12: 358 MB, 14: 5.7 GB); a table of a string
+ * is the interval bwt_extend reaches for it on any path (software/bwt.c:416-429) */
+int  smem_gpu_set_kmer_table(smem_gpu_t *gpu, int k);
 /* variant 9 (stamped diagnostic build): copy the per-wave cycle split
  * {advance, fetch, compute, iterations, active lanes, t0, t1, 0} of the last
  * run; returns the number of words copied or a negative code */

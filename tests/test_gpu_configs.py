@@ -136,6 +136,23 @@ def test_human_c5_5pct(human):
 
 
 @pytest.mark.timeout(900)
+def test_human_kmer_table(human, gpu_device):
+    """Variant 23 with a 12-mer table at human size (34-bit table entries)."""
+    from smemgpu import synth
+    gpu = human["gpu"]
+    reads = synth.make_reads(human["codes"], 4_000, 150, seed=7, sub_rate=0.03, n_rate=0.001)
+    gpu.set_kmer_table(12)
+    try:
+        gpu.set_variant(23)
+        for opt in ({}, dict(split_factor=1.0, split_width=500)):
+            res, _ = _seed_and_compare(gpu, human["oidx"], reads, opt)
+            assert _high_bits(res) > 100
+    finally:
+        gpu.set_variant(0)
+        gpu.set_kmer_table(0)
+
+
+@pytest.mark.timeout(900)
 def test_human_sa_lookup(human):
     """bwt_sa of every seed occurrence at human size (positions past 2^32)."""
     from smemgpu import synth

@@ -161,6 +161,47 @@ def test_kernel_variants(world, gpu_device, variant):
         gpu.close()
 
 
+@pytest.mark.parametrize("k", [1, 2, 7, 10, 12])
+def test_kmer_table_variant(world, gpu_device, k):
+    """Variant 23: extends whose result has <= k bases read the k-mer table;
+    the lists must be the oracle's bit for bit (a bi-interval does not depend
+    on the extension path), edge-case reads included."""
+    import smemgpu
+    from smemgpu import synth
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=23, kmer_k=k)
+    try:
+        g = world["genome"].codes
+        edge = synth.Reads(np.array([120], np.int32), np.where(np.arange(120) % 7 == 0, 4, g[9000:9120]).astype(np.uint8),
+                           np.array([0, 120], np.int64))
+        reads = synth_concat(_reads(world["genome"], "mixed", seed=13), _reads(world["genome"], "250bp5", seed=14), edge)
+        for opt in OPTS.values():
+            want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4, **opt)
+            assert smemgpu.seed(gpu, reads.codes, reads.offs, smemgpu.Options(**opt)).to_smgo() == want
+    finally:
+        gpu.close()
+
+
+def test_kmer_table_arguments(world, gpu_device):
+    import smemgpu
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=23)
+    try:
+        reads = _reads(world["genome"], "150bp", seed=15)
+        with pytest.raises(RuntimeError, match="kmer"):
+            smemgpu.seed(gpu, reads.codes, reads.offs)
+        for bad in (-1, 16):
+            with pytest.raises(RuntimeError):
+                gpu.set_kmer_table(bad)
+        gpu.set_kmer_table(6)
+        gpu.set_kmer_table(9)  # rebuilt in place
+        want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4)
+        assert smemgpu.seed(gpu, reads.codes, reads.offs).to_smgo() == want
+        gpu.set_kmer_table(0)
+        with pytest.raises(RuntimeError, match="kmer"):
+            smemgpu.seed(gpu, reads.codes, reads.offs)
+    finally:
+        gpu.close()
+
+
 def synth_concat(*parts):
     from smemgpu import synth
     return synth.concat_reads(list(parts))

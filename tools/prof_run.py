@@ -5,7 +5,7 @@ seeds and options), seeded --launches times.  Meant to run under
     rocprofv3 --pmc <counters> --kernel-include-regex seed_kernel -- python tools/prof_run.py [bench args]
 
 Any bench.py argument selects the workload (--config, --genome-profile,
---reads, --genome-mbp ...); --launches / --variant are this tool's own.
+--reads, --genome-mbp ...); --launches is this tool's own (--variant / --kmer-k are bench's).
 """
 import os
 import sys
@@ -20,14 +20,13 @@ def main():
     import argparse
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--launches", type=int, default=1)
-    p.add_argument("--variant", type=int, default=0)
     own, rest = p.parse_known_args()
     import bench
     import smemgpu
     a = bench.parse(rest)
     idx, _, _, codes = bench.get_index(a, 0, lambda: None, 0)
     reads = bench.make_reads(a, 0, codes, 1)
-    gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu, variant=own.variant)
+    gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu, variant=a.variant, kmer_k=a.kmer_k)
     b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
     b.set_reads(reads.codes, reads.offs)
     opt = smemgpu.Options(min_seed_len=a.min_seed_len)

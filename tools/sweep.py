@@ -30,7 +30,8 @@ def main():
     p.add_argument("--read-len", type=int, default=150)
     p.add_argument("--sub", type=float, default=0.02)
     p.add_argument("--lanes", default="256,512,1024")
-    p.add_argument("--variants", default="2", help="seeding kernel variants to compare (1 per-lane fetch, 2 coop)")
+    p.add_argument("--variants", default="2",
+                   help="seeding kernel variants to compare; V:K = variant V with a K-mer table (e.g. 23:12)")
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
     a = p.parse_args()
@@ -47,9 +48,12 @@ def main():
     idx = smemgpu.Index.read(key)
     reads = synth.make_reads(g.codes, a.reads, a.read_len, seed=1000 + a.seed * 7919, sub_rate=a.sub, n_rate=0.001)
     ref_hash = None
-    confs = [(v, l) for v in [int(x) for x in a.variants.split(",")] for l in [int(x) for x in a.lanes.split(",")]]
-    for variant, lanes in confs:
-        gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=lanes, variant=variant)
+    confs = [(v, l) for v in a.variants.split(",") for l in [int(x) for x in a.lanes.split(",")]]
+    for vspec, lanes in confs:
+        variant, kmer_k = (int(x) for x in (vspec + ":0").split(":")[:2])
+        t = time.time()
+        gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=lanes, variant=variant, kmer_k=kmer_k)
+        t_init = time.time() - t
         b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
         b.set_reads(reads.codes, reads.offs)
         b.run()
@@ -60,7 +64,8 @@ def main():
             b.run()
             ks.append(b.stats()["kernel_ms"])
         st = b.stats()
-        print(json.dumps({"genome_mbp": a.genome_mbp, "variant": variant, "lanes_per_cu": lanes, "grid": st["grid"],
+        print(json.dumps({"genome_mbp": a.genome_mbp, "variant": variant, "kmer_k": kmer_k, "init_s": round(t_init, 2),
+                          "lanes_per_cu": lanes, "grid": st["grid"],
                           "kernel_ms_min": round(min(ks), 3), "kernel_ms_med": round(float(np.median(ks)), 3),
                           "reads_per_s": round(reads.n / (min(ks) * 1e-3)), "same_result": h == ref_hash}),
               flush=True)
