@@ -65,8 +65,8 @@ BLOCK = 1 << 18          # reads per block of the read stream (shards are whole 
 
 # BASELINE.json configs: per-GPU shapes
 CONFIGS = {
-    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=4_000_000,
-               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1]); 4M streamed"),
+    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=8_000_000,
+               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1]); 8M streamed"),
     "c3": dict(read_len=150, sub=0.02, k=19, pairs=True, stream_reads=25_000_000,
                what="C3 on one GPU: its shard of 100M x 150 bp PE on 8 GPUs = 12.5M pairs, insert N(500, 50), "
                     "mates interleaved in one chunk"),
@@ -101,13 +101,17 @@ def parse(argv=None):
     p.add_argument("--kmer-k", type=int, default=0, help="k-mer bi-interval table of 1..K bases (variant 23)")
     p.add_argument("--streams", type=int, default=2, help="host workers, each with its own batch and HIP stream")
     p.add_argument("--stream-reads", type=int, default=None,
-                   help="reads per GPU pushed through the streaming path (default: the config's; c2: the resident reads)")
-    p.add_argument("--stream-chunk", type=int, default=1 << 17)
-    p.add_argument("--stream-workers", type=int, default=4)
+                   help="reads per GPU pushed through the streaming path (default: the config's; 0: the resident "
+                        "reads; -1: no streaming leg)")
+    p.add_argument("--stream-chunk", type=int, default=1 << 20)
+    p.add_argument("--stream-workers", type=int, default=2)
     p.add_argument("--stream-packed", type=int, default=1, help="1: 16-B wire entries (SMEM_STREAM_PACKED)")
     p.add_argument("--side-stages", type=int, default=1, help="0: skip the sa / chain / sw side reports")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--stats-sample", type=int, default=20000, help="reads counted by the oracle for bytes/read")
+    p.add_argument("--parity", type=int, default=1,
+                   help="1: seed the stats sample on the GPU too and compare (0: every seed_kernel launch is a "
+                        "full resident batch, for rocprofv3 summaries)")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch TCC_EA0_RDREQ / FETCH_SIZE recorded by tools/traffic.py for this build + workload")
@@ -207,15 +211,17 @@ def cpu_leg(args, gpu, opt, idx, idx_path, reads, cores, sw_tasks=None):
                                 min_seed_len=opt.min_seed_len)
     bpr = float(per["bytes"].mean())
     b64 = (32.0 * st["n_bkt64"] + st["n_bases"] + 32.0 * st["n_intv"]) / max(n, 1)
-    b = gpu.batch(s.n, int(s.codes.size), int(s.lens.max()))
-    try:
-        b.set_reads(s.codes, s.offs)
-        b.run(opt)
-        got = b.fetch().to_smgo()
-    finally:
-        b.close()
-    parity = {"reads": n, "intervals": int(st["n_intv"]), "bit_exact": got == want,
-              "against": "C restatement of the seeding loop (oracle/, pinned to the compiled reference's streams)"}
+    parity = None
+    if args.parity:
+        b = gpu.batch(s.n, int(s.codes.size), int(s.lens.max()))
+        try:
+            b.set_reads(s.codes, s.offs)
+            b.run(opt)
+            got = b.fetch().to_smgo()
+        finally:
+            b.close()
+        parity = {"reads": n, "intervals": int(st["n_intv"]), "bit_exact": got == want,
+                  "against": "C restatement of the seeding loop (oracle/, pinned to the compiled reference's streams)"}
     cpu = None
     if args.cpu_seconds > 0:
         # calibrate on a small slice, then size the sample for ~cpu_seconds
@@ -644,12 +650,16 @@ def main():
 
     # streaming (PCIe-inclusive) on every rank, then its aggregate; the
     # config's target read count, or the resident reads (c2)
-    sreads = reads if args.stream_reads <= 0 else make_reads(args, rank, genome_codes, world, args.stream_reads, salt=1)
-    barrier()
-    srep = streaming_report(gpu, sreads, opt, args, value / world)
-    s_rate = d.allsum(float(srep["reads"])) / d.allmax(srep["wall_s"])
-    srep["reads_per_s_all_ranks"] = round(s_rate, 1)
-    del sreads
+    # (--stream-reads -1: no streaming leg)
+    srep = None
+    if args.stream_reads >= 0:
+        sreads = reads if args.stream_reads == 0 else make_reads(args, rank, genome_codes, world, args.stream_reads,
+                                                                 salt=1)
+        barrier()
+        srep = streaming_report(gpu, sreads, opt, args, value / world)
+        s_rate = d.allsum(float(srep["reads"])) / d.allmax(srep["wall_s"])
+        srep["reads_per_s_all_ranks"] = round(s_rate, 1)
+        del sreads
 
     sa_rep = chain_rep = sw_rep = sw_tasks = aln_rep = None
     if rank == 0 and args.side_stages:
@@ -701,6 +711,7 @@ def main():
                                f"replicated, no collectives; {args.streams} host workers per GPU, each running whole "
                                f"steps on its own stream",
                 "grid": st["grid"], "block": st["block"],
+                "kernel_variant": args.variant or 2, "kmer_k": args.kmer_k,
             },
             "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, k_ms, a_ms, smemgpu.build_id()),
             "cpu_baseline": cpu,

@@ -26,6 +26,7 @@
 //    happen in finalize_kernel, off the latency-bound loop.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 #include "smem_kernels.h"
 
 namespace smem {
@@ -1332,16 +1333,110 @@ extern "C" hipError_t smem_launch_ovf_slot(const int32_t* items, int n_ovf, int3
 }
 
 // ---------------------------------------------------------------- scans
-#include <hipcub/hipcub.hpp>
+// Size -> offset scans with (almost) no LDS: three small launches (tile sums,
+// one-block scan of the tile sums, tile rescans with carry-in), wave scans by
+// shuffles and 32 B of LDS per block.  The persistent seeding kernel of
+// another worker's chunk holds all but 4 KB of every CU's LDS; a library scan
+// (16 KB+ of LDS per block) then waits for that whole kernel, and with it the
+// chunk's copies and the next chunk (profiles/r02/stream/).
+namespace smem {
+constexpr int SCAN_T = 256, SCAN_I = 8, SCAN_TILE = SCAN_T * SCAN_I;
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// exclusive prefix of this thread's SCAN_I elements within the block, and the block total
+__device__ __forceinline__ uint64_t block_excl(uint64_t tsum, uint64_t& total) {
+    __shared__ uint64_t ws[SCAN_T / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan(tsum, lane);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint64_t before = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_T / 64; ++k) {
+        before += k < w ? ws[k] : 0;
+        total += ws[k];
+    }
+    __syncthreads();  // ws is reused by the next call
+    return before + inc - tsum;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_tile_sums(const uint64_t* __restrict__ in, int n, uint64_t* __restrict__ bsum) {
+    const int64_t b0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) t += b0 + k < n ? in[b0 + k] : 0;
+    uint64_t total;
+    (void)block_excl(t, total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// one block: bsum[0..nb) -> exclusive offsets in place
+__global__ __launch_bounds__(SCAN_T) void scan_tile_offsets(uint64_t* __restrict__ bsum, int nb) {
+    uint64_t carry = 0;
+    for (int base = 0; base < nb; base += SCAN_TILE) {
+        const int b0 = base + (int)threadIdx.x * SCAN_I;
+        uint64_t v[SCAN_I], t = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_I; ++k) {
+            v[k] = b0 + k < nb ? bsum[b0 + k] : 0;
+            t += v[k];
+        }
+        uint64_t total;
+        uint64_t run = carry + block_excl(t, total);
+#pragma unroll
+        for (int k = 0; k < SCAN_I; ++k) {
+            if (b0 + k < nb) bsum[b0 + k] = run;
+            run += v[k];
+        }
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_tiles(const uint64_t* __restrict__ in, int n,
+                                                     const uint64_t* __restrict__ boff, uint64_t* __restrict__ out) {
+    const int64_t b0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+    uint64_t v[SCAN_I], t = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+        v[k] = b0 + k < n ? in[b0 + k] : 0;
+        t += v[k];
+    }
+    uint64_t total;
+    uint64_t run = boff[blockIdx.x] + block_excl(t, total);
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+        run += v[k];
+        if (b0 + k < n) out[b0 + k + 1] = run;
+    }
+}
+}  // namespace smem
 
 // out[0] = 0, out[1..n] = inclusive sums of in[0..n-1]; temp == nullptr
 // queries the temporary size into *temp_bytes
 extern "C" hipError_t smem_launch_offsets(const uint64_t* in, uint64_t* out, int n, void* temp, size_t* temp_bytes,
                                           hipStream_t st) {
-    if (temp == nullptr) return hipcub::DeviceScan::InclusiveSum(nullptr, *temp_bytes, in, out + 1, n > 0 ? n : 1, st);
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
-    if (e != hipSuccess || n <= 0) return e;
-    return hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, in, out + 1, n, st);
+    const int nb = n > 0 ? (n + smem::SCAN_TILE - 1) / smem::SCAN_TILE : 1;
+    if (temp == nullptr) {
+        *temp_bytes = sizeof(uint64_t) * (size_t)(nb + 1);
+        return hipSuccess;
+    }
+    if (*temp_bytes < sizeof(uint64_t) * (size_t)nb) return hipErrorInvalidValue;
+    if (n <= 0) return hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    uint64_t* bsum = static_cast<uint64_t*>(temp);
+    hipLaunchKernelGGL(smem::scan_tile_sums, dim3(nb), dim3(smem::SCAN_T), 0, st, in, n, bsum);
+    hipLaunchKernelGGL(smem::scan_tile_offsets, dim3(1), dim3(smem::SCAN_T), 0, st, bsum, nb);
+    hipLaunchKernelGGL(smem::scan_tiles, dim3(nb), dim3(smem::SCAN_T), 0, st, in, n, bsum, out);
+    return hipGetLastError();
 }
 
 namespace smem {
