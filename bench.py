@@ -59,6 +59,7 @@ sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC = "SMEM reads/sec on human_g1k_v37 150bp at 1/2/4/8 MI355X; achieved HBM GB/s"
+RT_TICKS_PER_MS = 1e5  # s_memrealtime: 100 MHz (checked against HIP events: chip_clock_check)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 HUMAN_MBP = 3101.804739  # human_g1k_v37 l_pac
 BLOCK = 1 << 18          # reads per block of the read stream (shards are whole blocks)
@@ -528,8 +529,21 @@ def sw_cpu(kb) -> dict:
             "sample": f"{kb.tasks.size} problems, {secs:.2f} s incl. file I/O"}
 
 
-def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id) -> dict:
-    achieved = bpr * reads_n / (k_ms * 1e-3) / 1e9
+def span_union(spans) -> float:
+    """Total time covered by the [start, end) intervals (chip-clock ticks)."""
+    tot, cur = 0, None
+    for a, b in sorted(spans):
+        if cur is None or a > cur[1]:
+            if cur is not None:
+                tot += cur[1] - cur[0]
+            cur = [a, b]
+        else:
+            cur[1] = max(cur[1], b)
+    return float(tot + (cur[1] - cur[0] if cur else 0))
+
+
+def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id, busy_ms, clock_check) -> dict:
+    achieved = bpr * reads_n / (busy_ms * 1e-3) / 1e9
     out = {
         "bound": "hbm",
         "achieved": round(achieved, 2),
@@ -538,10 +552,17 @@ def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id)
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": None,
         "kernel": "seed_kernel",
+        "kernel_busy_ms": round(busy_ms, 3),
+        "kernel_busy_ms_source": "time the GPU spent in seed_kernel over the timed region (union of every launch's "
+                                 "first-wave-start .. last-wave-end on the chip's 100 MHz clock, s_memrealtime) / "
+                                 "launches: the two workers' launches overlap, so this is the per-launch time of the "
+                                 "kernel, and `achieved` = algorithmic bytes per launch / it",
         "kernel_ms": round(k_ms, 3),
         "kernel_ms_source": "HIP events on each worker's stream around every seed_kernel launch of the timed region "
-                            "(mean); with --streams > 1 two workers' launches overlap on the GPU, so a launch lasts "
-                            "longer than ms_per_step",
+                            "(mean; what rocprofv3 --stats averages): overlapping launches each last longer than the "
+                            "kernel's share of the GPU",
+        "frac_per_launch": round(bpr * reads_n / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "chip_clock_check": round(clock_check, 4) if clock_check else None,
         "kernel_ms_alone": round(a_ms, 3),
         "frac_alone": round(bpr * reads_n / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "bytes_per_read": round(bpr, 1),
@@ -597,16 +618,18 @@ def main():
     opt = smemgpu.Options(min_seed_len=args.min_seed_len)
     # warmup; launches that run alone on the GPU (no other stream's kernels
     # beside them) give kernel_ms_alone
-    alone_ms = []
+    alone_ms, alone_span = [], []
     compact_alone = 0.0
     for w in range(max(args.warmup, 2)):
         batch.run(opt)
         if w > 0:
-            alone_ms.append(batch.stats()["kernel_ms"])
-            compact_alone = batch.stats()["compact_ms"]
+            bs = batch.stats()
+            alone_ms.append(bs["kernel_ms"])
+            alone_span.append((bs["t_end"] - bs["t_start"]) / RT_TICKS_PER_MS)
+            compact_alone = bs["compact_ms"]
     # the roofline's kernel time: HIP events on each worker's own stream around
     # every seed_kernel launch of the timed region (what rocprofv3 sees too)
-    kernel_ms = []
+    kernel_ms, spans = [], []
     for b in batches[1:]:
         b.run(opt)
     barrier()
@@ -615,7 +638,9 @@ def main():
     if len(batches) == 1:
         for _ in range(args.steps):
             batch.run(opt)
-            kernel_ms.append(batch.stats()["kernel_ms"])
+            bs = batch.stats()
+            kernel_ms.append(bs["kernel_ms"])
+            spans.append((bs["t_start"], bs["t_end"]))
     else:
         # kt_for_batch-style workers (the reference's own host model,
         # software/kthread_batch.c:29-59): steps are dealt round-robin, each
@@ -628,7 +653,9 @@ def main():
             try:
                 for k in range(wi, args.steps, len(batches)):
                     batches[wi].run(opt)
-                    kernel_ms.append(batches[wi].stats()["kernel_ms"])
+                    bs = batches[wi].stats()
+                    kernel_ms.append(bs["kernel_ms"])
+                    spans.append((bs["t_start"], bs["t_end"]))
             except Exception as e:  # surfaced below
                 errs.append(e)
 
@@ -680,6 +707,8 @@ def main():
             aln_rep["cpu_baseline"] = aln_cpu(args, idx_path, reads, genome_codes, opt)
         k_ms = float(np.mean(kernel_ms))
         a_ms = float(np.mean(alone_ms))
+        busy_ms = span_union(spans) / RT_TICKS_PER_MS / max(len(spans), 1)
+        clock_check = float(np.mean(alone_span)) / a_ms if a_ms > 0 else None
         cfg = CONFIGS[args.config]
         out = {
             "metric": METRIC,
@@ -713,7 +742,8 @@ def main():
                 "grid": st["grid"], "block": st["block"],
                 "kernel_variant": args.variant or 2, "kmer_k": args.kmer_k,
             },
-            "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, k_ms, a_ms, smemgpu.build_id()),
+            "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, k_ms, a_ms, smemgpu.build_id(), busy_ms,
+                                 clock_check),
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "compact_ms": round(compact_alone, 3),

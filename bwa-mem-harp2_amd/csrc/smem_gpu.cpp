@@ -544,6 +544,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     P.head = b->d_ctr.p + 0;
     P.ovf_count = b->d_ctr.p + 1;
     P.ovf_items = b->d_ovf_items.p;
+    P.tspan = reinterpret_cast<uint64_t*>(b->d_ctr.p + 4);  // zeroed with the counters below
     const int lanes = std::min(b->lanes, std::max(256, (n + 255) / 256 * 256));
     const int grid = lanes / 256;
     b->stats.grid = grid;
@@ -646,6 +647,12 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     b->stats.compact_ms = ms;
     b->stats.n_intv = b->tot_intv;
     b->stats.n_calls = b->tot_calls;
+    {  // h_ctr was copied after the last seeding launch
+        uint64_t sp[2];
+        std::memcpy(sp, b->h_ctr.p + 4, sizeof(sp));
+        b->stats.t_start = n > 0 ? ~sp[0] : 0;
+        b->stats.t_end = n > 0 ? sp[1] : 0;
+    }
     b->ran = true;
     return SMEM_OK;
 }

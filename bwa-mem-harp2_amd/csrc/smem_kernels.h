@@ -46,6 +46,7 @@ struct SeedParams {
     uint32_t cap_list;
     int dbg;                   // debug switches (0 in production)
     uint64_t* dbg_buf;         // stamped diagnostic variant: 8 x u64 per wave
+    uint64_t* tspan;           // [0] max of ~(wave start), [1] max of wave end (s_memrealtime), nullptr: none
     const uint4* kt;           // k-mer bi-interval table (smem_launch_kmer_table; variant 23), nullptr: none
     int kt_k;                  // its longest k-mer
 };

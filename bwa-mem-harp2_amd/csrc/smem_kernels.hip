@@ -558,6 +558,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     uint64_t bat_h = 0;   // the lanes that computed them, in entry order
     uint64_t st_adv = 0, st_fetch = 0, st_comp = 0, st_iter = 0, st_active = 0, st_t0 = 0, st_t1 = 0;
     if constexpr (STAMP) st_t0 = rtstamp();
+    // the launch's span on the chip clock: first wave start, last wave end
+    if (P.tspan && lane == 0) atomicMax(reinterpret_cast<unsigned long long*>(P.tspan), ~(unsigned long long)rtstamp());
 
 #define QBLK(pos) ((o0 + (uint32_t)(pos)) & ~15u)
 // one forward-list push: the arena (pushed downward: ascending order is the
@@ -1164,6 +1166,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     }
 #undef FWD_PUSH
 #undef LSLOT
+    if (P.tspan && lane == 0) atomicMax(reinterpret_cast<unsigned long long*>(P.tspan) + 1, (unsigned long long)rtstamp());
     if constexpr (STAMP) {
         st_t1 = rtstamp();
         if (lane == 0 && P.dbg_buf) {

@@ -85,7 +85,7 @@ class BatchStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("compact_ms", C.c_double), ("n_intv", C.c_uint64),
                 ("n_calls", C.c_uint64), ("n_overflow", C.c_uint32), ("grid", C.c_int), ("block", C.c_int),
                 ("sa_ms", C.c_double), ("n_occ", C.c_uint64), ("chain_ms", C.c_double), ("n_chains", C.c_uint64),
-                ("aln_ms", C.c_double), ("n_regs", C.c_uint64)]
+                ("aln_ms", C.c_double), ("n_regs", C.c_uint64), ("t_start", C.c_uint64), ("t_end", C.c_uint64)]
 
 
 class StreamStats(C.Structure):

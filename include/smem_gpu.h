@@ -366,6 +366,8 @@ typedef struct {
 	uint64_t n_chains;       /* chains kept by smem_batch_chain */
 	double aln_ms;           /* smem_batch_chain2aln kernels */
 	uint64_t n_regs;         /* regions made by smem_batch_chain2aln */
+	uint64_t t_start, t_end; /* the seeding launches' first wave start and last wave end, chip-wide
+	                          * 100 MHz clock (s_memrealtime): comparable across batches and streams */
 } smem_batch_stats_t;
 int  smem_batch_stats(const smem_batch_t *b, smem_batch_stats_t *st);
 

@@ -118,3 +118,12 @@ def test_shard_blocks():
     import bench
     assert bench.shard_blocks(1_000_000, 0, 1) == [0, 1, 2, 3]
     assert bench.shard_blocks(1_000_000, 3, 8) == [3, 11, 19, 27]
+
+
+def test_span_union():
+    """bench.py's kernel busy time: the union of overlapping launch spans."""
+    import bench
+    assert bench.span_union([]) == 0
+    assert bench.span_union([(5, 9)]) == 4
+    assert bench.span_union([(0, 10), (5, 12), (20, 25), (21, 22)]) == 17
+    assert bench.span_union([(20, 25), (0, 10), (10, 11)]) == 16
