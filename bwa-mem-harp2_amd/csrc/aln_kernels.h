@@ -17,6 +17,8 @@ struct AlnReg {
 };
 static_assert(sizeof(AlnReg) == 64, "mem_alnreg_t layout");
 
+constexpr int ALN_CTRS = 16;
+
 struct AlnParams {
     // reads (nt4 codes, 4 = N) and the chains smem_batch_chain wrote
     const uint8_t* codes;
@@ -39,7 +41,22 @@ struct AlnParams {
     uint64_t* srt;     // per chain: the seed order (software/bwamem.c:1070-1073)
     AlnReg* raw;       // read r's regions at raw[seed_off[r] ..)
     uint64_t* n_regs;  // [n_reads]
-    uint32_t* ctr;     // [2] work-queue heads (reads <= 256 bp, longer)
+    uint32_t* ctr;     // [ALN_CTRS]: work-queue heads (reads <= 256 bp, longer), heavy-read count, heavy-path heads
+    uint64_t* cyc;     // diagnostics (SMEM_ALN_CYCLES): [n_reads] shader cycles per read, nullptr: off
+    // heavy reads (at least heavy_min chains or heavy_seeds seeds; 0 = none):
+    // every chain walked ahead on its own, one wave per chain, then the read's
+    // walk replays them (aln_heavy_kernel)
+    uint32_t heavy_min, heavy_seeds;
+    int32_t* heavy;           // [n_reads] heavy read ids (ctr[2] of them, any order)
+    uint64_t* hcnt;           // [n_reads] their chain counts, then
+    uint64_t* hoff;           // [n_heavy + 1] prefix: chain task t of the heavy reads
+    uint64_t* hscnt;          // [n_reads] their seed counts
+    int64_t* span;            // [2 n_chains] the chain's reference span (chain_span)
+    AlnReg* pre;              // [n_seeds] the region of each seed its chain's own walk extended, heavy reads only
+    uint8_t* pre_ok;          // [n_seeds] 1: pre holds it
+    AlnReg* loc;              // [n_seeds] the regions of each chain's own walk (scratch at the chain's seeds)
+    AlnReg* pre_short;        // [n_chains] mem_chain2aln_short's region, heavy reads only
+    uint8_t* short_ok;        // [n_chains] 1: that region was made (0: mem_chain2aln runs)
     // compaction
     const uint64_t* reg_off;  // [n_reads + 1]
     AlnReg* out;
@@ -71,4 +88,8 @@ hipError_t smem_launch_ksw_align2(const smem::KswAParams* K, int n_cu, hipStream
 // long_reads != 0: the batch holds reads of 257..1024 bp (second instantiation)
 hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st);
 hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st);
+// heavy reads: list them (ctr[2]), then, after the host scanned hcnt into
+// hoff, compute their chains' regions ahead and walk them
+hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st);
+hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st);
 }

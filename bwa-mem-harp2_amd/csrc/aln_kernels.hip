@@ -67,11 +67,23 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32;
 }
+// A wave-uniform value in an SGPR.  Loop bounds of the wave-cooperative
+// loops go through this: a bound the compiler keeps in a VGPR makes the loop
+// exit a per-lane compare, and a loop with an exit of that shape hung gfx950
+// waves (the seed-order loop of the heavy-read walk spun with no lane left
+// to leave it).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32;
+}
 
 // mem_chain2aln_short (software/bwamem.c:805-852): 0 when it wrote region
-// *out, 1 when it declines (then mem_chain2aln runs)
-__device__ int chain_short(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n, AlnReg* out,
-                           int lane) {
+// *out, 1 when it declines (then mem_chain2aln runs).  One exit: the
+// declines are flags, not early returns (an early return out of this wave-
+// cooperative body, inlined into a persistent loop, hung gfx950 waves).
+__device__ __forceinline__ int chain_short(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n,
+                                           AlnReg* out, int lane) {
     int64_t qb = L, qe = 0, rb = P.l_pac << 1, re = 0;
     int cov = 0;
     for (int i = lane; i < n; i += 64) {
@@ -85,42 +97,41 @@ __device__ int chain_short(const AlnParams& P, const uint8_t* query, int L, cons
     cov = wsum(cov);
     qb = wmin64(qb) - 50, qe = wmax64(qe) + 50;  // MEM_SHORT_EXT
     rb = wmin64(rb) - 50, re = wmax64(re) + 50;
-    if (qb <= 10 || qe >= L - 10) return 1;
+    bool decline = qb <= 10 || qe >= L - 10;
     rb = rb > 0 ? rb : 0;
     re = re < P.l_pac << 1 ? re : P.l_pac << 1;
     if (rb < P.l_pac && P.l_pac < re) {
         if (S[0].rbeg < P.l_pac) re = P.l_pac;
         else rb = P.l_pac;
     }
-    if ((re - rb) - (qe - qb) > 50 || (qe - qb) - (re - rb) > 50) return 1;
-    if (qe - qb >= P.w * 4 || re - rb >= P.w * 4) return 1;
-    if (qe - qb >= 200 || re - rb >= 200) return 1;  // MEM_SHORT_LEN
-    const int ql = (int)(qe - qb), tl = (int)(re - rb);
-    const int xtra = kswd::SW_XSUBO | kswd::SW_XSTART | (ql * P.a < 250 ? kswd::SW_XBYTE : 0) | (P.min_seed_len * P.a);
-    const uint8_t* qw = query + qb;
-    const int64_t r0 = rb;
-    const kswd::SwAlign x = kswd::sw_align_wave(
-        ql, [&](int q) { return (int)qw[q]; }, tl, [&](int i) { return ref_at(P, r0 + i); }, P.mat, P.o_del, P.e_del,
-        P.o_ins, P.e_ins, xtra, P.sw_shift, P.top);
-    if (x.tb < 25 || x.te > tl - 25) return 1;
-    if (lane == 0) {
-        AlnReg a;
-        a.rb = rb + x.tb, a.re = rb + x.te + 1;
-        a.qb = (int)qb + x.qb, a.qe = (int)qb + x.qe + 1;
-        a.score = x.score, a.truesc = 0, a.sub = 0, a.csub = x.score2, a.sub_n = 0, a.w = 0, a.seedcov = cov;
-        a.secondary = 0, a.hash = 0;
-        *out = a;
+    decline = decline || (re - rb) - (qe - qb) > 50 || (qe - qb) - (re - rb) > 50;
+    decline = decline || qe - qb >= P.w * 4 || re - rb >= P.w * 4;
+    decline = decline || qe - qb >= 200 || re - rb >= 200;  // MEM_SHORT_LEN
+    if (!decline) {
+        const int ql = (int)(qe - qb), tl = (int)(re - rb);
+        const int xtra =
+            kswd::SW_XSUBO | kswd::SW_XSTART | (ql * P.a < 250 ? kswd::SW_XBYTE : 0) | (P.min_seed_len * P.a);
+        const uint8_t* qw = query + qb;
+        const int64_t r0 = rb;
+        const kswd::SwAlign x = kswd::sw_align_wave(
+            ql, [&](int q) { return (int)qw[q]; }, tl, [&](int i) { return ref_at(P, r0 + i); }, P.mat, P.o_del,
+            P.e_del, P.o_ins, P.e_ins, xtra, P.sw_shift, P.top);
+        decline = x.tb < 25 || x.te > tl - 25;
+        if (!decline && lane == 0) {
+            AlnReg a;
+            a.rb = rb + x.tb, a.re = rb + x.te + 1;
+            a.qb = (int)qb + x.qb, a.qe = (int)qb + x.qe + 1;
+            a.score = x.score, a.truesc = 0, a.sub = 0, a.csub = x.score2, a.sub_n = 0, a.w = 0, a.seedcov = cov;
+            a.secondary = 0, a.hash = 0;
+            *out = a;
+        }
     }
-    return 0;
+    return decline ? 1 : 0;
 }
 
-// mem_chain2aln (software/bwamem.c:1040-1188); regs[0 .. nreg) are the read's
-// regions so far, srt the chain's n-word scratch
-template <int KC>
-__device__ void chain_full(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n, uint64_t* srt,
-                           AlnReg* regs, int& nreg, int lane) {
-    // the span of reference any extension may reach (software/bwamem.c:1050-1065)
-    int64_t r0 = P.l_pac << 1, r1 = 0;
+// the span of reference any extension of the chain may reach (software/bwamem.c:1050-1065)
+__device__ __forceinline__ void chain_span(const AlnParams& P, int L, const SeedRec* S, int n, int lane, int64_t& r0, int64_t& r1) {
+    r0 = P.l_pac << 1, r1 = 0;
     for (int i = lane; i < n; i += 64) {
         const SeedRec t = S[i];
         const int64_t b = t.rbeg - (t.qbeg + max_gap(P, t.qbeg));
@@ -135,7 +146,12 @@ __device__ void chain_full(const AlnParams& P, const uint8_t* query, int L, cons
         if (S[0].rbeg < P.l_pac) r1 = P.l_pac;
         else r0 = P.l_pac;
     }
-    // seeds ascending by (len, index): each key lands at its rank
+}
+
+// the chain's seeds ascending by (len, index) (software/bwamem.c:1070-1073):
+// each key lands at its rank in srt
+__device__ __forceinline__ void chain_order(const SeedRec* S, int n, uint64_t* srt, int lane) {
+    n = uni(n);
     for (int ib = 0; ib < n; ib += 64) {
         const int i = ib + lane;
         const uint64_t ki = i < n ? ((uint64_t)(uint32_t)S[i].len << 32 | (uint32_t)i) : ~0ull;
@@ -149,122 +165,181 @@ __device__ void chain_full(const AlnParams& P, const uint8_t* query, int L, cons
         if (i < n) srt[rank] = ki;
     }
     __threadfence_block();
-    for (int k = n - 1; k >= 0; --k) {
-        const SeedRec s = S[(uint32_t)srt[k]];
-        // is the seed (almost) contained in a region made before? (software/bwamem.c:1079-1094)
-        bool hit = false;
-        for (int ib = 0; ib < nreg && !hit; ib += 64) {
-            const int i = ib + lane;
-            bool ok = false;
-            if (i < nreg) {
-                const AlnReg p = regs[i];
-                if (!(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe)) {
-                    int qd = s.qbeg - p.qb;
-                    int64_t rd = s.rbeg - p.rb;
-                    int g = max_gap(P, (int)(qd < rd ? qd : rd));
-                    int w = g < P.w ? g : P.w;
-                    if (qd - rd < w && rd - qd < w) ok = true;
-                    qd = p.qe - (s.qbeg + s.len);
-                    rd = p.re - (s.rbeg + s.len);
-                    g = max_gap(P, (int)(qd < rd ? qd : rd));
-                    w = g < P.w ? g : P.w;
-                    if (qd - rd < w && rd - qd < w) ok = true;
+}
+
+// does seed s (srt position k) get extended?  Not when it is (almost)
+// contained in a region made before (software/bwamem.c:1079-1094), unless a
+// long overlapping seed later in the order disagrees with it (:1098-1109).
+// A skipped seed's srt entry is zeroed (the reference's srt[k] = 0).
+__device__ __forceinline__ bool seed_wanted(const AlnParams& P, const SeedRec* S, int n, uint64_t* srt, int k, const SeedRec& s,
+                            const AlnReg* regs, int nreg, int lane) {
+    n = uni(n), k = uni(k), nreg = uni(nreg);
+    bool hit = false;
+    // newest regions first: a seed is mostly contained in its own chain's
+    // region, made just before (any hit gives the same answer)
+    for (int ib = 0; ib < nreg && !hit; ib += 64) {
+        const int i = nreg - 1 - ib - lane;
+        bool ok = false;
+        if (i >= 0) {
+            const AlnReg p = regs[i];
+            if (!(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe)) {
+                int qd = s.qbeg - p.qb;
+                int64_t rd = s.rbeg - p.rb;
+                int g = max_gap(P, (int)(qd < rd ? qd : rd));
+                int w = g < P.w ? g : P.w;
+                if (qd - rd < w && rd - qd < w) ok = true;
+                qd = p.qe - (s.qbeg + s.len);
+                rd = p.re - (s.rbeg + s.len);
+                g = max_gap(P, (int)(qd < rd ? qd : rd));
+                w = g < P.w ? g : P.w;
+                if (qd - rd < w && rd - qd < w) ok = true;
+            }
+        }
+        hit = __ballot(ok) != 0;
+    }
+    bool brk = false;
+    for (int ib = k + 1; hit && ib < n && !brk; ib += 64) {
+        const int i = ib + lane;
+        bool ok = false;
+        if (i < n) {
+            const uint64_t v = srt[i];
+            if (v != 0) {
+                const SeedRec t = S[(uint32_t)v];
+                if (!(t.len < s.len * .95)) {
+                    if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
+                        (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg)
+                        ok = true;
+                    if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
+                        (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg)
+                        ok = true;
                 }
             }
-            hit = __ballot(ok) != 0;
         }
-        if (hit) {  // extend only if a long overlapping seed disagrees (software/bwamem.c:1098-1109)
-            bool brk = false;
-            for (int ib = k + 1; ib < n && !brk; ib += 64) {
-                const int i = ib + lane;
-                bool ok = false;
-                if (i < n) {
-                    const uint64_t v = srt[i];
-                    if (v != 0) {
-                        const SeedRec t = S[(uint32_t)v];
-                        if (!(t.len < s.len * .95)) {
-                            if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
-                                (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg)
-                                ok = true;
-                            if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
-                                (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg)
-                                ok = true;
-                        }
+        brk = __ballot(ok) != 0;
+    }
+    if (hit && !brk) {
+        if (lane == 0) srt[k] = 0;  // not extended
+        __threadfence_block();
+    }
+    return !hit || brk;
+}
+
+// the region mem_chain2aln makes of seed s (software/bwamem.c:1110-1186):
+// left and right ksw_extend2 with MAX_BAND_TRY, and the chain's seeds it
+// covers.  Depends on the chain, the read and the reference only -- not on
+// the regions made before -- so heavy reads compute it ahead, in parallel.
+template <int KC>
+__device__ __forceinline__ AlnReg seed_region(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n, const SeedRec& s,
+                              int64_t r0, int64_t r1, int lane) {
+    int aw0 = P.w, aw1 = P.w, score = -1, truesc = -1, aqb, aqe;
+    int64_t arb, are;
+    if (s.qbeg) {  // left: the reversed query against the reversed reference
+        const int64_t tmp = s.rbeg - r0;
+        KswResult x{};
+        for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY
+            const int prev = score;
+            aw0 = P.w << t;
+            x = kswd::extend_wave<KC>(
+                kswd::ExtIn{s.qbeg, (int)tmp, aw0, P.pen_clip5, P.zdrop, s.len * P.a},
+                [&](int j) { return (int)query[s.qbeg - 1 - j]; }, [&](int i) { return ref_at(P, s.rbeg - 1 - i); },
+                P.mat, P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
+            score = x.score;
+            if (score == prev || x.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+        }
+        if (x.gscore <= 0 || x.gscore <= score - P.pen_clip5) {  // local extension
+            aqb = s.qbeg - x.qle, arb = s.rbeg - x.tle;
+            truesc = score;
+        } else {  // to the query start
+            aqb = 0, arb = s.rbeg - x.gtle;
+            truesc = x.gscore;
+        }
+    } else {
+        score = truesc = s.len * P.a;
+        aqb = 0, arb = s.rbeg;
+    }
+    if (s.qbeg + s.len != L) {  // right
+        const int qe = s.qbeg + s.len, sc0 = score;
+        const int64_t rs = s.rbeg + s.len;
+        KswResult x{};
+        for (int t = 0; t < 2; ++t) {
+            const int prev = score;
+            aw1 = P.w << t;
+            x = kswd::extend_wave<KC>(kswd::ExtIn{L - qe, (int)(r1 - rs), aw1, P.pen_clip3, P.zdrop, sc0},
+                                      [&](int j) { return (int)query[qe + j]; },
+                                      [&](int i) { return ref_at(P, rs + i); }, P.mat, P.o_del, P.e_del, P.o_ins,
+                                      P.e_ins, P.top);
+            score = x.score;
+            if (score == prev || x.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+        }
+        if (x.gscore <= 0 || x.gscore <= score - P.pen_clip3) {
+            aqe = qe + x.qle, are = rs + x.tle;
+            truesc += score - sc0;
+        } else {
+            aqe = L, are = rs + x.gtle;
+            truesc += x.gscore - sc0;
+        }
+    } else {
+        aqe = L, are = s.rbeg + s.len;
+    }
+    int cov = 0;  // seeds inside the region (software/bwamem.c:1180-1184)
+    for (int i = lane; i < n; i += 64) {
+        const SeedRec t = S[i];
+        if (t.qbeg >= aqb && t.qbeg + t.len <= aqe && t.rbeg >= arb && t.rbeg + t.len <= are) cov += t.len;
+    }
+    cov = wsum(cov);
+    AlnReg a;
+    a.rb = arb, a.re = are, a.qb = aqb, a.qe = aqe;
+    a.score = score, a.truesc = truesc, a.sub = 0, a.csub = 0, a.sub_n = 0;
+    a.w = aw0 > aw1 ? aw0 : aw1, a.seedcov = cov, a.secondary = 0, a.hash = 0;
+    return a;
+}
+
+// the region of seed si of a chain, behind a call (see aln_heavy_task_kernel)
+template <int KC>
+__device__ __attribute__((noinline)) void seed_region_call(const AlnParams& P, const uint8_t* query, int L,
+                                                           const SeedRec* S, int n, int si, int64_t r0, int64_t r1,
+                                                           AlnReg* out) {
+    const AlnReg a = seed_region<KC>(P, query, L, S, n, S[si], r0, r1, threadIdx.x & 63);
+    if ((threadIdx.x & 63) == 0) *out = a;
+}
+
+enum ChainMode { CM_PLAIN = 0, CM_RECORD = 1, CM_REPLAY = 2 };
+
+// mem_chain2aln (software/bwamem.c:1040-1188); regs[0 .. nreg) are the read's
+// regions so far, srt the chain's n-word scratch.
+//  CM_RECORD: also leave each extended seed's region at pre[i] (pre_ok[i] = 1);
+//  CM_REPLAY: take a seed's region from pre[i] when pre_ok[i], else compute it
+//    (the heavy-read walk over the chain walks recorded ahead, r0 / r1 given).
+template <int KC, int MODE = CM_PLAIN>
+__device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n,
+                                           uint64_t* srt, AlnReg* regs, int& nreg, int lane, AlnReg* pre = nullptr,
+                                           uint8_t* pre_ok = nullptr, int64_t r0 = 0, int64_t r1 = 0) {
+    n = uni(n);
+    if constexpr (MODE != CM_REPLAY) chain_span(P, L, S, n, lane, r0, r1);
+    chain_order(S, n, srt, lane);
+    for (int k = n - 1; k >= 0; --k) {
+        const uint32_t si = (uint32_t)srt[k];
+        const SeedRec s = S[si];
+        if (seed_wanted(P, S, n, srt, k, s, regs, nreg, lane)) {
+            if constexpr (MODE == CM_REPLAY) {
+                if (uni((int)pre_ok[si])) {
+                    if (lane == 0) regs[nreg] = pre[si];
+                } else {
+                    seed_region_call<KC>(P, query, L, S, n, (int)si, r0, r1, regs + nreg);
+                }
+            } else {
+                const AlnReg a = seed_region<KC>(P, query, L, S, n, s, r0, r1, lane);
+                if (lane == 0) {
+                    regs[nreg] = a;
+                    if constexpr (MODE == CM_RECORD) {
+                        pre[si] = a;
+                        pre_ok[si] = 1;
                     }
                 }
-                brk = __ballot(ok) != 0;
             }
-            if (!brk) {
-                if (lane == 0) srt[k] = 0;  // not extended
-                __threadfence_block();
-                continue;
-            }
+            ++nreg;
+            __threadfence_block();
         }
-        int aw0 = P.w, aw1 = P.w, score = -1, truesc = -1, aqb, aqe;
-        int64_t arb, are;
-        if (s.qbeg) {  // left: the reversed query against the reversed reference
-            const int64_t tmp = s.rbeg - r0;
-            KswResult x{};
-            for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY
-                const int prev = score;
-                aw0 = P.w << t;
-                x = kswd::extend_wave<KC>(
-                    kswd::ExtIn{s.qbeg, (int)tmp, aw0, P.pen_clip5, P.zdrop, s.len * P.a},
-                    [&](int j) { return (int)query[s.qbeg - 1 - j]; }, [&](int i) { return ref_at(P, s.rbeg - 1 - i); },
-                    P.mat, P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
-                score = x.score;
-                if (score == prev || x.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
-            }
-            if (x.gscore <= 0 || x.gscore <= score - P.pen_clip5) {  // local extension
-                aqb = s.qbeg - x.qle, arb = s.rbeg - x.tle;
-                truesc = score;
-            } else {  // to the query start
-                aqb = 0, arb = s.rbeg - x.gtle;
-                truesc = x.gscore;
-            }
-        } else {
-            score = truesc = s.len * P.a;
-            aqb = 0, arb = s.rbeg;
-        }
-        if (s.qbeg + s.len != L) {  // right
-            const int qe = s.qbeg + s.len, sc0 = score;
-            const int64_t rs = s.rbeg + s.len;
-            KswResult x{};
-            for (int t = 0; t < 2; ++t) {
-                const int prev = score;
-                aw1 = P.w << t;
-                x = kswd::extend_wave<KC>(kswd::ExtIn{L - qe, (int)(r1 - rs), aw1, P.pen_clip3, P.zdrop, sc0},
-                                          [&](int j) { return (int)query[qe + j]; },
-                                          [&](int i) { return ref_at(P, rs + i); }, P.mat, P.o_del, P.e_del, P.o_ins,
-                                          P.e_ins, P.top);
-                score = x.score;
-                if (score == prev || x.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
-            }
-            if (x.gscore <= 0 || x.gscore <= score - P.pen_clip3) {
-                aqe = qe + x.qle, are = rs + x.tle;
-                truesc += score - sc0;
-            } else {
-                aqe = L, are = rs + x.gtle;
-                truesc += x.gscore - sc0;
-            }
-        } else {
-            aqe = L, are = s.rbeg + s.len;
-        }
-        int cov = 0;  // seeds inside the region (software/bwamem.c:1180-1184)
-        for (int i = lane; i < n; i += 64) {
-            const SeedRec t = S[i];
-            if (t.qbeg >= aqb && t.qbeg + t.len <= aqe && t.rbeg >= arb && t.rbeg + t.len <= are) cov += t.len;
-        }
-        cov = wsum(cov);
-        if (lane == 0) {
-            AlnReg a;
-            a.rb = arb, a.re = are, a.qb = aqb, a.qe = aqe;
-            a.score = score, a.truesc = truesc, a.sub = 0, a.csub = 0, a.sub_n = 0;
-            a.w = aw0 > aw1 ? aw0 : aw1, a.seedcov = cov, a.secondary = 0, a.hash = 0;
-            regs[nreg] = a;
-        }
-        ++nreg;
-        __threadfence_block();
     }
 }
 
@@ -283,11 +358,15 @@ __global__ __launch_bounds__(256) void aln_kernel(AlnParams P) {
             const int L = (int)(P.offs[r + 1] - q0);
             if ((L > 256) != (KC > 4)) continue;  // the other instantiation's read
             const uint8_t* query = P.codes + q0;
-            const uint64_t c0 = P.chain_off[r], c1 = P.chain_off[r + 1];
+            const uint64_t t_read = P.cyc ? __builtin_amdgcn_s_memtime() : 0;
+            const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
+            if (P.heavy_min && (c1 - c0 >= P.heavy_min || P.seed_off[r + 1] - P.seed_off[r] >= P.heavy_seeds))
+                continue;  // aln_heavy_kernel's read
             AlnReg* regs = P.raw + P.seed_off[r];
             int nreg = 0;
             for (uint64_t c = c0; c < c1; ++c) {
-                const OutChain ch = P.chains[c];
+                OutChain ch = P.chains[c];
+                ch.n = uni(ch.n);
                 if (ch.n <= 0) continue;  // mem_chain2aln_short returns -1, nothing is made
                 const SeedRec* S = P.seeds + ch.seed_off;
                 if (chain_short(P, query, L, S, ch.n, regs + nreg, lane) == 0) {
@@ -298,7 +377,139 @@ __global__ __launch_bounds__(256) void aln_kernel(AlnParams P) {
                 }
             }
             if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
+            if (P.cyc && lane == 0) P.cyc[r] = __builtin_amdgcn_s_memtime() - t_read;
         }
+    }
+}
+
+// heavy reads (at least heavy_min chains or heavy_seeds seeds), listed in
+// any order with their chain and seed counts
+__global__ __launch_bounds__(256) void aln_classify_kernel(AlnParams P) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= P.n_reads) return;
+    const uint64_t nc = P.chain_off[r + 1] - P.chain_off[r], ns = P.seed_off[r + 1] - P.seed_off[r];
+    if (nc >= P.heavy_min || ns >= P.heavy_seeds) {
+        const uint32_t h = atomicAdd(&P.ctr[2], 1u);
+        P.heavy[h] = r;
+        P.hcnt[h] = nc;
+        P.hscnt[h] = ns;
+    }
+}
+
+// the heavy read of task t: h with off[h] <= t < off[h + 1]
+__device__ __forceinline__ uint32_t heavy_of(const uint64_t* off, uint32_t nh, uint64_t t) {
+    uint32_t lo = 0, hi = nh;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    return (uint32_t)uni((int)lo);
+}
+
+// The heavy-path kernels are persistent loops that claim a task and run its
+// body.  Every loop bound and branch of the wave-cooperative bodies is made
+// an SGPR value (uni); the read walk is a call (see heavy_chain_walk).  A
+// call around the extensions cost 20 % (register save / restore).
+
+// chain task t of the heavy reads: mem_chain2aln_short's region (or its
+// decline) and, when it declines, the region of every seed of the chain
+// (pre, pre_ok = 1).  Measured against recording only the seeds the chain's
+// own walk extends (CM_RECORD): on the human-like profile that left more
+// extensions to the serial read walk and was 20 % slower.
+template <int KC>
+__device__ __forceinline__ void heavy_chain_task(const AlnParams& P, uint32_t nh, uint64_t t) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t h = heavy_of(P.hoff, nh, t);
+    const int r = uni(P.heavy[h]);
+    const uint64_t q0 = P.offs[r];
+    const int L = uni((int)(P.offs[r + 1] - q0));
+    const uint64_t c = uni64(P.chain_off[r] + (t - P.hoff[h]));
+    OutChain ch = P.chains[c];
+    ch.n = uni(ch.n);
+    if ((L > 256) == (KC > 4) && ch.n > 0) {  // this instantiation's read, a chain with seeds
+        const uint8_t* query = P.codes + q0;
+        const SeedRec* S = P.seeds + ch.seed_off;
+        const int ok = chain_short(P, query, L, S, ch.n, P.pre_short + c, lane) == 0;
+        int64_t r0, r1;
+        chain_span(P, L, S, ch.n, lane, r0, r1);
+        if (lane == 0) {
+            P.short_ok[c] = (uint8_t)ok;
+            P.span[2 * c] = r0;
+            P.span[2 * c + 1] = r1;
+        }
+        for (int i = lane; i < ch.n; i += 64) P.pre_ok[ch.seed_off + i] = (uint8_t)!ok;
+        __threadfence_block();
+        if (!ok) {  // every seed's region: the read's walk decides which of them are made
+            for (int i = 0; i < ch.n; ++i) {
+                const AlnReg a = seed_region<KC>(P, query, L, S, ch.n, S[i], r0, r1, lane);
+                if (lane == 0) P.pre[ch.seed_off + i] = a;
+            }
+        }
+    }
+}
+
+// one wave per chain of the heavy reads at a time
+template <int KC>
+__global__ __launch_bounds__(256) void aln_heavy_task_kernel(AlnParams P) {
+    const uint32_t nh = P.ctr[2];
+    const uint64_t total = P.hoff[nh];
+    unsigned long long* head = reinterpret_cast<unsigned long long*>(P.ctr + (KC > 4 ? 6 : 4));
+    for (;;) {
+        uint64_t t = 0;
+        if ((threadIdx.x & 63) == 0) t = atomicAdd(head, 1ull);
+        t = uni64(t);
+        if (t >= total) break;
+        heavy_chain_task<KC>(P, nh, t);
+    }
+}
+
+// one chain of a heavy read in the read's walk.  A call, not inlined:
+// inlined into aln_heavy_kernel's persistent loop this walk hung gfx950
+// waves (ROCm 7.2 compiler; the same code with a call in it ran).
+template <int KC>
+__device__ __attribute__((noinline)) void heavy_chain_walk(const AlnParams& P, const uint8_t* query, int L,
+                                                           const SeedRec* S, int n, uint64_t* srt, AlnReg* regs,
+                                                           int* nreg, AlnReg* pre, uint8_t* pre_ok, int64_t r0,
+                                                           int64_t r1) {
+    int k = *nreg;
+    chain_full<KC, CM_REPLAY>(P, query, L, S, n, srt, regs, k, threadIdx.x & 63, pre, pre_ok, r0, r1);
+    *nreg = k;
+}
+
+// one wave per heavy read: the chain walk of aln_kernel over the chains'
+// walks recorded ahead (containment tests and seed order, and the few
+// extensions the recorded walks did not make)
+template <int KC>
+__global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nh = P.ctr[2];
+    for (;;) {
+        uint32_t h = 0;
+        if (lane == 0) h = atomicAdd(&P.ctr[KC > 4 ? 13 : 3], 1u);
+        h = (uint32_t)__builtin_amdgcn_readfirstlane((int)h);
+        if (h >= nh) break;
+        const int r = uni(P.heavy[h]);
+        const int L = uni((int)(P.offs[r + 1] - P.offs[r]));
+        if ((L > 256) != (KC > 4)) continue;  // the other instantiation's read
+        const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
+        AlnReg* regs = P.raw + P.seed_off[r];
+        int nreg = 0;
+        for (uint64_t c = c0; c < c1; ++c) {
+            OutChain ch = P.chains[c];
+            ch.n = uni(ch.n);
+            if (ch.n <= 0) continue;
+            if (__builtin_amdgcn_readfirstlane((int)P.short_ok[c])) {
+                if (lane == 0) regs[nreg] = P.pre_short[c];
+                ++nreg;
+                __threadfence_block();
+            } else {
+                heavy_chain_walk<KC>(P, P.codes + P.offs[r], L, P.seeds + ch.seed_off, ch.n, P.srt + ch.seed_off, regs,
+                                     &nreg, P.pre + ch.seed_off, P.pre_ok + ch.seed_off, P.span[2 * c],
+                                     P.span[2 * c + 1]);
+            }
+        }
+        if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
     }
 }
 
@@ -347,6 +558,20 @@ extern "C" hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int lo
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !long_reads) return e;
     hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(std::max(1, std::min(n_cu * 2, blocks))), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st) {
+    if (P->n_reads <= 0 || !P->heavy_min) return hipSuccess;
+    hipLaunchKernelGGL(smem::aln_classify_kernel, dim3((P->n_reads + 255) / 256), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
+    hipLaunchKernelGGL(smem::aln_heavy_task_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
+    if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_task_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
+    hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu), dim3(256), 0, st, *P);
+    if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

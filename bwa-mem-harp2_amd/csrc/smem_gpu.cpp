@@ -127,6 +127,19 @@ struct smem_gpu {
     std::vector<smem_batch_t*> stream_pool;
 };
 
+// scratch of the heavy-read path of chains -> regions
+struct AlnHeavyBufs {
+    DevBuf<int32_t> heavy;
+    DevBuf<uint64_t> hcnt, hoff, hscnt;
+    DevBuf<int64_t> span;
+    DevBuf<smem::AlnReg> pre, pre_short, loc;
+    DevBuf<uint8_t> short_ok, pre_ok, tmp;
+    void release() {
+        heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); pre.release();
+        pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
+    }
+};
+
 struct smem_batch {
     smem_gpu_t* g = nullptr;
     hipStream_t st = nullptr;
@@ -195,6 +208,7 @@ struct smem_batch {
     DevBuf<uint64_t> d_aln_srt, d_aln_nregs, d_aln_regoff;
     DevBuf<smem::AlnReg> d_aln_raw, d_aln_out;
     DevBuf<uint32_t> d_aln_ctr;
+    AlnHeavyBufs aln_heavy;     // the heavy-read path's scratch
     HostBuf<uint64_t> h_aln_regoff;
     HostBuf<smem::AlnReg> h_aln_regs;
     bool aln_ran = false, aln_fetched = false;
@@ -360,7 +374,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release(); b->d_heavy.release();
     b->h_chain_off.release(); b->h_out_chain.release(); b->h_out_seed.release();
     b->d_aln_srt.release(); b->d_aln_nregs.release(); b->d_aln_regoff.release(); b->d_aln_raw.release();
-    b->d_aln_out.release(); b->d_aln_ctr.release(); b->h_aln_regoff.release(); b->h_aln_regs.release();
+    b->d_aln_out.release(); b->d_aln_ctr.release(); b->aln_heavy.release(); b->h_aln_regoff.release(); b->h_aln_regs.release();
     b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
     b->d_pintv.release(); b->h_pintv.release();
     b->h_intv_off.release(); b->h_call_off.release();
@@ -1194,6 +1208,60 @@ int smem_gpu_load_pac(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
     return SMEM_OK;
 }
 
+// reads with at least this many chains, or seeds, take the heavy path
+// (SMEM_ALN_HEAVY_MIN / SMEM_ALN_HEAVY_SEEDS override; a zero chain count =
+// never): tandem-repeat reads carry hundreds to thousands of chains or seeds,
+// and one wave walking them alone kept the whole launch waiting (0.5 s for
+// one read, profiles/r02/aln/)
+static uint32_t aln_heavy_min() {
+    const char* e = getenv("SMEM_ALN_HEAVY_MIN");
+    return e ? (uint32_t)atoi(e) : 17u;
+}
+static uint32_t aln_heavy_seeds() {
+    const char* e = getenv("SMEM_ALN_HEAVY_SEEDS");
+    return e ? (uint32_t)atoi(e) : 48u;
+}
+
+// mem_chain2aln of every chain of every read (P filled, ctr zeroed for
+// smem::ALN_CTRS): heavy reads listed, their chains' and seeds' regions
+// computed ahead one wave per chain and walked one wave per read; the other
+// reads one wave each
+static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_t n_seeds, bool long_reads,
+                   AlnHeavyBufs& H, hipStream_t st) {
+    const int n = P.n_reads;
+    P.heavy_min = aln_heavy_min();
+    P.heavy_seeds = aln_heavy_seeds();
+    uint32_t n_heavy = 0;
+    if (P.heavy_min && n > 0) {
+        HIP_TRY(H.heavy.ensure(n));
+        HIP_TRY(H.hcnt.ensure(n));
+        HIP_TRY(H.hscnt.ensure(n));
+        P.heavy = H.heavy.p, P.hcnt = H.hcnt.p, P.hscnt = H.hscnt.p;
+        HIP_TRY(smem_launch_aln_classify(&P, st));
+        HIP_TRY(hipMemcpyAsync(&n_heavy, P.ctr + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (n_heavy) {
+        HIP_TRY(H.hoff.ensure(n_heavy + 1));
+        size_t tb = 0;
+        HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)n_heavy, nullptr, &tb, st));
+        HIP_TRY(H.tmp.ensure(tb + 256));
+        tb = H.tmp.n;
+        HIP_TRY(smem_launch_offsets(H.hcnt.p, H.hoff.p, (int)n_heavy, H.tmp.p, &tb, st));
+        HIP_TRY(H.pre.ensure(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.loc.ensure(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.pre_ok.ensure(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.pre_short.ensure(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.short_ok.ensure(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.span.ensure(2 * std::max<uint64_t>(n_chains, 1)));
+        P.hoff = H.hoff.p, P.pre = H.pre.p, P.loc = H.loc.p, P.pre_ok = H.pre_ok.p, P.pre_short = H.pre_short.p;
+        P.short_ok = H.short_ok.p, P.span = H.span.p;
+        HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, st));
+    }
+    HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
+    return SMEM_OK;
+}
+
 int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     g_err[0] = 0;
     if (!b || !b->chain_ran || !b->chain_filtered)
@@ -1209,7 +1277,7 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     HIP_TRY(b->d_aln_raw.ensure(ns + 1));
     HIP_TRY(b->d_aln_nregs.ensure(std::max(n, 1)));
     HIP_TRY(b->d_aln_regoff.ensure(n + 1));
-    HIP_TRY(b->d_aln_ctr.ensure(2));
+    HIP_TRY(b->d_aln_ctr.ensure(smem::ALN_CTRS));
     size_t tmp = 0;
     HIP_TRY(smem_launch_offsets(nullptr, nullptr, std::max(n, 1), nullptr, &tmp, b->st));
     HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
@@ -1221,9 +1289,16 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     P.pac = g->d_pac, P.l_pac = g->l_pac, P.n_reads = n;
     aln_opt_params(opt, P);
     P.srt = b->d_aln_srt.p, P.raw = b->d_aln_raw.p, P.n_regs = b->d_aln_nregs.p, P.ctr = b->d_aln_ctr.p;
-    HIP_TRY(hipMemsetAsync(b->d_aln_ctr.p, 0, 2 * sizeof(uint32_t), b->st));
+    // diagnostics: SMEM_ALN_CYCLES=<file> writes the shader cycles each read took (u64 per read)
+    const char* cyc_path = getenv("SMEM_ALN_CYCLES");
+    DevBuf<uint64_t> d_cyc;
+    if (cyc_path) {
+        HIP_TRY(d_cyc.ensure(std::max(n, 1)));
+        P.cyc = d_cyc.p;
+    }
+    HIP_TRY(hipMemsetAsync(b->d_aln_ctr.p, 0, smem::ALN_CTRS * sizeof(uint32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
-    HIP_TRY(smem_launch_aln(&P, g->n_cu, b->max_len > 256 ? 1 : 0, b->st));
+    if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->st)) return rc;
     tmp = b->d_sa_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_aln_nregs.p, b->d_aln_regoff.p, n, b->d_sa_tmp.p, &tmp, b->st));
     HIP_TRY(hipMemcpyAsync(b->h_tot.p + 5, b->d_aln_regoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
@@ -1239,6 +1314,15 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
     b->stats.aln_ms = ms;
     b->stats.n_regs = b->tot_regs;
+    if (cyc_path && n > 0) {
+        std::vector<uint64_t> h(n);
+        HIP_TRY(hipMemcpy(h.data(), d_cyc.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(cyc_path, "wb")) {
+            fwrite(h.data(), sizeof(uint64_t), n, f);
+            fclose(f);
+        }
+    }
+    d_cyc.release();
     b->aln_ran = true;
     b->aln_fetched = false;
     return SMEM_OK;
@@ -1311,6 +1395,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     DevBuf<smem::SeedRec> dseeds;
     DevBuf<smem::AlnReg> draw, dout;
     DevBuf<uint32_t> dctr;
+    AlnHeavyBufs heavy;
     hipStream_t st = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     struct Guard {
@@ -1323,6 +1408,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
         dcodes.release(); dpac.release(); doffs.release(); dchoff.release(); dseedoff.release(); dsrt.release();
         dnregs.release(); dregoff.release(); dch.release(); dseeds.release(); draw.release(); dout.release();
         dctr.release();
+        heavy.release();
         if (ev[0]) (void)hipEventDestroy(ev[0]);
         if (ev[1]) (void)hipEventDestroy(ev[1]);
         if (st) (void)hipStreamDestroy(st);
@@ -1343,7 +1429,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     HIP_TRY(dseeds.ensure(n_seeds + 1));
     HIP_TRY(draw.ensure(n_cap + 1));
     HIP_TRY(dout.ensure(n_cap + 1));
-    HIP_TRY(dctr.ensure(2));
+    HIP_TRY(dctr.ensure(smem::ALN_CTRS));
     if (n_bases) HIP_TRY(hipMemcpyAsync(dcodes.p, codes, n_bases, hipMemcpyHostToDevice, st));
     if (pac) HIP_TRY(hipMemcpyAsync(dpac.p, pac, pac_bytes, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(doffs.p, offs, 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
@@ -1351,7 +1437,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     HIP_TRY(hipMemcpyAsync(dseedoff.p, cap.data(), 8 * (n_reads + 1), hipMemcpyHostToDevice, st));
     if (n_chains) HIP_TRY(hipMemcpyAsync(dch.p, chains, sizeof(smem::OutChain) * n_chains, hipMemcpyHostToDevice, st));
     if (n_seeds) HIP_TRY(hipMemcpyAsync(dseeds.p, seeds, sizeof(smem::SeedRec) * n_seeds, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(dctr.p, 0, 8, st));
+    HIP_TRY(hipMemsetAsync(dctr.p, 0, smem::ALN_CTRS * sizeof(uint32_t), st));
     smem::AlnParams P;
     std::memset(&P, 0, sizeof(P));
     P.codes = dcodes.p, P.offs = doffs.p, P.chains = dch.p, P.chain_off = dchoff.p, P.seeds = dseeds.p;
@@ -1359,7 +1445,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     aln_opt_params(opt, P);
     P.srt = dsrt.p, P.raw = draw.p, P.n_regs = dnregs.p, P.ctr = dctr.p;
     HIP_TRY(hipEventRecord(ev[0], st));
-    HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
+    if (int rc = run_aln(g, P, n_chains, n_seeds, long_reads, heavy, st)) return rc;
     HIP_TRY(hipEventRecord(ev[1], st));
     std::vector<uint64_t> nr(n_reads);
     HIP_TRY(hipMemcpyAsync(nr.data(), dnregs.p, 8 * n_reads, hipMemcpyDeviceToHost, st));

@@ -64,8 +64,12 @@ def test_aln_oracle_vs_reference(fix):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("heavy", [None, "1", "1000:2"], ids=["default", "all_heavy", "seed_heavy"])
 @pytest.mark.parametrize("fix", FIX, ids=[f["file"].split(".")[0] for f in FIX])
-def test_aln_gpu_vs_reference(gpu_device, fix):
+def test_aln_gpu_vs_reference(gpu_device, fix, heavy, monkeypatch):
+    """heavy = "1": every read takes the heavy-read path (regions computed
+    ahead per chain, then the read's walk), SMEM_ALN_HEAVY_MIN."""
+    _heavy_env(monkeypatch, heavy)
     import smemgpu
     from smemgpu import synth
     reads, chains, chain_off, seeds = _case_inputs(fix)
@@ -81,6 +85,16 @@ def test_aln_gpu_vs_reference(gpu_device, fix):
     got = np.frombuffer(raw.tobytes(), dtype=golden_data.ALNREG_DT)
     _assert_same(got, off, want, want_off)
     del synth
+
+
+def _heavy_env(monkeypatch, heavy):
+    """heavy = "min[:seeds]": SMEM_ALN_HEAVY_MIN / SMEM_ALN_HEAVY_SEEDS, the
+    chain / seed counts from which a read takes the heavy-read path."""
+    if heavy:
+        m, _, sd = heavy.partition(":")
+        monkeypatch.setenv("SMEM_ALN_HEAVY_MIN", m)
+        if sd:
+            monkeypatch.setenv("SMEM_ALN_HEAVY_SEEDS", sd)
 
 
 def _tmpdir():
@@ -108,15 +122,19 @@ def test_pack_matches_reference_pac():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,a", [(100, 1), (20, 1), (100, 2)])
-def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a):
+@pytest.mark.parametrize("w,a,heavy", [(100, 1, None), (20, 1, None), (100, 2, None), (100, 1, "1"), (100, 2, "1"),
+                                       (20, 1, "3"), (100, 1, "0"), (100, 1, "1000:3")])
+def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a, heavy, monkeypatch):
     """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
     kernel instantiations) with substitutions and Ns; chains from the GPU
     chain stage; GPU regions == restatement, through the host API
     (smem_chain2aln, explicit .pac and resident .pac) and the device-resident
     batch stage (smem_batch_chain2aln over the chains left in HBM).  a = 2
     (-A 2 scaling, b 8, gaps 12 + 2) sends the short path's longer queries
-    through ksw_align2's 16-bit branch."""
+    through ksw_align2's 16-bit branch.  heavy: SMEM_ALN_HEAVY_MIN (1: every
+    read through the heavy-read path, 3: reads with 3+ chains, 0: none,
+    1000:3 reads with 3+ seeds)."""
+    _heavy_env(monkeypatch, heavy)
     import smemgpu
     from smemgpu import synth
     g = synth.make_genome(600_000, seed=91, repeat_frac=0.6, n_families=5, exact_frac=0.01, tandem_frac=0.01)

@@ -1,0 +1,57 @@
+"""Alignment-stage workload for rocprofv3 (kernel trace or counter passes):
+the bench's index, reads and options, then seeding + SA + chaining once and
+smem_batch_chain2aln --launches times.
+
+    rocprofv3 --pmc <counters> --kernel-include-regex aln_kernel -- python tools/aln_prof.py [bench args]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import argparse
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--launches", type=int, default=2)
+    p.add_argument("--cycles", default=None, help="write per-read shader cycles of the last launch here (u64)")
+    own, rest = p.parse_known_args()
+    import torch
+    torch.cuda.device_count()  # as bench.py's Dist does, before libsmemgpu touches the device
+    import bench
+    import smemgpu
+    from oracle import oracle
+    a = bench.parse(rest)
+    idx, _, sa, codes = bench.get_index(a, 0, lambda: None, 0)
+    reads = bench.make_reads(a, 0, codes, 1)
+    gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu, variant=a.variant, kmer_k=a.kmer_k)
+    gpu.load_sa(sa)
+    gpu.load_pac(bench.pack_pac(codes), idx.seq_len // 2)
+    b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+    b.set_reads(reads.codes, reads.offs)
+    opt = smemgpu.Options(min_seed_len=a.min_seed_len)
+    b.run(opt)
+    b.sa(opt.min_seed_len, 10000)
+    b.chain(idx.seq_len // 2)
+    for k in range(own.launches):
+        if own.cycles and k == own.launches - 1:
+            os.environ["SMEM_ALN_CYCLES"] = own.cycles
+        t = time.time()
+        b.chain2aln(oracle.aln_opt(min_seed_len=opt.min_seed_len))
+        st = b.stats()
+        print(f"chain2aln: {st['aln_ms']:.3f} ms, {st['n_regs']} regions, {st['n_chains']} chains, "
+              f"wall {1e3 * (time.time() - t):.1f} ms", flush=True)
+    if own.cycles:  # per-read chain / seed counts beside the cycles
+        import numpy as np
+        res = b.fetch()
+        np.savez(own.cycles + ".chains.npz", chain_off=res.chain_off, chain_n=res.chains["n"],
+                 lens=np.diff(reads.offs.astype(np.int64)))
+    b.close()
+    gpu.close()
+
+
+if __name__ == "__main__":
+    main()

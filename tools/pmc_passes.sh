@@ -1,6 +1,7 @@
 #!/bin/bash
 # Counter passes for the seeding kernel (one rocprofv3 run per pass; no trace
 # domains combined with --pmc).  Usage: tools/pmc_passes.sh <outdir> [prof_run args]
+# PMC_PROG / PMC_KERNEL select another workload / kernel (e.g. tools/aln_prof.py, aln_kernel).
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift
 mkdir -p "$OUT"
@@ -16,6 +17,6 @@ PASSES=(
 SEL=${PMC_PASSES:-$(seq 0 $((${#PASSES[@]} - 1)))}  # e.g. PMC_PASSES="0 1 2"
 for i in $SEL; do
   P=${PASSES[$i]}
-  timeout -k 10 240 rocprofv3 --pmc $P --kernel-include-regex seed_kernel --output-format csv -d "$OUT" -o pass$i -- python tools/prof_run.py "$@" > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  timeout -k 10 240 rocprofv3 --pmc $P --kernel-include-regex ${PMC_KERNEL:-seed_kernel} --output-format csv -d "$OUT" -o pass$i -- python ${PMC_PROG:-tools/prof_run.py} "$@" > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
 done
 echo "all passes ok"
