@@ -343,8 +343,10 @@ __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* qu
     }
 }
 
+// KC = 4 at 4 waves per SIMD (128 VGPRs, 2 spilled): 3 waves at its free
+// allocation (136)
 template <int KC>
-__global__ __launch_bounds__(256) void aln_kernel(AlnParams P) {
+__global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
     const int lane = threadIdx.x & 63;
     constexpr uint32_t CLAIM = 4;  // reads per work-queue claim
     for (;;) {
@@ -451,7 +453,7 @@ __device__ __forceinline__ void heavy_chain_task(const AlnParams& P, uint32_t nh
 
 // one wave per chain of the heavy reads at a time
 template <int KC>
-__global__ __launch_bounds__(256) void aln_heavy_task_kernel(AlnParams P) {
+__global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_heavy_task_kernel(AlnParams P) {
     const uint32_t nh = P.ctr[2];
     const uint64_t total = P.hoff[nh];
     unsigned long long* head = reinterpret_cast<unsigned long long*>(P.ctr + (KC > 4 ? 6 : 4));
