@@ -466,52 +466,46 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_heavy_task_kernel(Aln
     }
 }
 
-// one chain of a heavy read in the read's walk.  A call, not inlined:
-// inlined into aln_heavy_kernel's persistent loop this walk hung gfx950
-// waves (ROCm 7.2 compiler; the same code with a call in it ran).
+// the walk of heavy read r: aln_kernel's chain loop over the regions
+// computed ahead (containment tests and seed order, and the extensions
+// mem_chain2aln_short's accepted chains did not leave).  A call, not inlined:
+// inlined into aln_heavy_kernel's persistent loop this walk hung gfx950 waves
+// (ROCm 7.2 compiler; the same code behind a call ran).
 template <int KC>
-__device__ __attribute__((noinline)) void heavy_chain_walk(const AlnParams& P, const uint8_t* query, int L,
-                                                           const SeedRec* S, int n, uint64_t* srt, AlnReg* regs,
-                                                           int* nreg, AlnReg* pre, uint8_t* pre_ok, int64_t r0,
-                                                           int64_t r1) {
-    int k = *nreg;
-    chain_full<KC, CM_REPLAY>(P, query, L, S, n, srt, regs, k, threadIdx.x & 63, pre, pre_ok, r0, r1);
-    *nreg = k;
+__device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, int r) {
+    const int lane = threadIdx.x & 63;
+    const int L = uni((int)(P.offs[r + 1] - P.offs[r]));
+    const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
+    AlnReg* regs = P.raw + P.seed_off[r];
+    int nreg = 0;
+    for (uint64_t c = c0; c < c1; ++c) {
+        OutChain ch = P.chains[c];
+        ch.n = uni(ch.n);
+        if (ch.n <= 0) continue;
+        if (uni((int)P.short_ok[c])) {
+            if (lane == 0) regs[nreg] = P.pre_short[c];
+            ++nreg;
+            __threadfence_block();
+        } else {
+            chain_full<KC, CM_REPLAY>(P, P.codes + P.offs[r], L, P.seeds + ch.seed_off, ch.n, P.srt + ch.seed_off, regs,
+                                      nreg, lane, P.pre + ch.seed_off, P.pre_ok + ch.seed_off, P.span[2 * c],
+                                      P.span[2 * c + 1]);
+        }
+    }
+    if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
 }
 
-// one wave per heavy read: the chain walk of aln_kernel over the chains'
-// walks recorded ahead (containment tests and seed order, and the few
-// extensions the recorded walks did not make)
+// one wave per heavy read at a time
 template <int KC>
 __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
-    const int lane = threadIdx.x & 63;
     const uint32_t nh = P.ctr[2];
     for (;;) {
         uint32_t h = 0;
-        if (lane == 0) h = atomicAdd(&P.ctr[KC > 4 ? 13 : 3], 1u);
-        h = (uint32_t)__builtin_amdgcn_readfirstlane((int)h);
+        if ((threadIdx.x & 63) == 0) h = atomicAdd(&P.ctr[KC > 4 ? 13 : 3], 1u);
+        h = (uint32_t)uni((int)h);
         if (h >= nh) break;
         const int r = uni(P.heavy[h]);
-        const int L = uni((int)(P.offs[r + 1] - P.offs[r]));
-        if ((L > 256) != (KC > 4)) continue;  // the other instantiation's read
-        const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
-        AlnReg* regs = P.raw + P.seed_off[r];
-        int nreg = 0;
-        for (uint64_t c = c0; c < c1; ++c) {
-            OutChain ch = P.chains[c];
-            ch.n = uni(ch.n);
-            if (ch.n <= 0) continue;
-            if (__builtin_amdgcn_readfirstlane((int)P.short_ok[c])) {
-                if (lane == 0) regs[nreg] = P.pre_short[c];
-                ++nreg;
-                __threadfence_block();
-            } else {
-                heavy_chain_walk<KC>(P, P.codes + P.offs[r], L, P.seeds + ch.seed_off, ch.n, P.srt + ch.seed_off, regs,
-                                     &nreg, P.pre + ch.seed_off, P.pre_ok + ch.seed_off, P.span[2 * c],
-                                     P.span[2 * c + 1]);
-            }
-        }
-        if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
+        if ((uni((int)(P.offs[r + 1] - P.offs[r])) > 256) == (KC > 4)) heavy_read_walk<KC>(P, r);
     }
 }
 
