@@ -105,7 +105,7 @@ def parse(argv=None):
                    help="reads per GPU pushed through the streaming path (default: the config's; 0: the resident "
                         "reads; -1: no streaming leg)")
     p.add_argument("--stream-chunk", type=int, default=1 << 20)
-    p.add_argument("--stream-workers", type=int, default=2)
+    p.add_argument("--stream-workers", type=int, default=3)
     p.add_argument("--stream-packed", type=int, default=1, help="1: 16-B wire entries (SMEM_STREAM_PACKED)")
     p.add_argument("--stream-passes", type=int, default=3, help="timed streaming passes; the median is reported")
     p.add_argument("--side-stages", type=int, default=1, help="0: skip the sa / chain / sw side reports")

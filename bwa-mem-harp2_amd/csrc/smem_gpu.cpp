@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <string>
 #include <cstdio>
 #include <cstdlib>
@@ -1532,6 +1533,14 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
     std::atomic<uint64_t> n_intv{0}, h2d{0}, d2h{0}, t_stage{0}, t_run{0}, t_fetch{0};
     std::mutex emu;
     std::string emsg;
+    // At most `slots` chunks seed at once (SMEM_STREAM_GPU_SLOTS, default 2):
+    // two persistent launches overlap each other's tails, as the resident
+    // bench's two workers do; a third worker stages / fetches meanwhile
+    // instead of queueing a third launch behind them.
+    const char* sl_env = getenv("SMEM_STREAM_GPU_SLOTS");
+    int slots = sl_env ? std::max(1, atoi(sl_env)) : 2;
+    std::mutex slot_mu;
+    std::condition_variable slot_cv;
     const auto t0 = std::chrono::steady_clock::now();
     auto worker = [&](int w) {
         smem_batch_t* b = bs[w];
@@ -1544,7 +1553,19 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
             const auto c0 = std::chrono::steady_clock::now();
             int r = smem_batch_set_reads_packed(b, n, codes, offs + a);
             const auto c1 = std::chrono::steady_clock::now();
-            if (!r) r = smem_batch_run(b, opt);
+            if (!r) {
+                {
+                    std::unique_lock<std::mutex> lk(slot_mu);
+                    slot_cv.wait(lk, [&] { return slots > 0; });
+                    --slots;
+                }
+                r = smem_batch_run(b, opt);
+                {
+                    std::lock_guard<std::mutex> lk(slot_mu);
+                    ++slots;
+                }
+                slot_cv.notify_one();
+            }
             const auto c2 = std::chrono::steady_clock::now();
             if (!r) r = smem_batch_fetch(b);
             const auto c3 = std::chrono::steady_clock::now();
