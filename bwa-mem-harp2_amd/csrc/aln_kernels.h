@@ -18,6 +18,8 @@ struct AlnReg {
 static_assert(sizeof(AlnReg) == 64, "mem_alnreg_t layout");
 
 constexpr int ALN_CTRS = 16;
+constexpr int ALN_HT = 65536;       // hash slots per walk wave
+constexpr int ALN_WALK_WAVES = 4;   // walk waves per CU (aln_heavy_kernel blocks of 256)
 
 struct AlnParams {
     // reads (nt4 codes, 4 = N) and the chains smem_batch_chain wrote
@@ -47,11 +49,14 @@ struct AlnParams {
     // every chain walked ahead on its own, one wave per chain, then the read's
     // walk replays them (aln_heavy_kernel)
     uint32_t heavy_min, heavy_seeds;
+    uint32_t hash_min;        // heavy reads with at least this many chains hash their regions by bin
     int32_t* heavy;           // [n_reads] heavy read ids (ctr[2] of them, any order)
     uint64_t* hcnt;           // [n_reads] their chain counts, then
     uint64_t* hoff;           // [n_heavy + 1] prefix: chain task t of the heavy reads
     uint64_t* hscnt;          // [n_reads] their seed counts
     int64_t* span;            // [2 n_chains] the chain's reference span (chain_span)
+    uint64_t* ht;             // [walk waves x ALN_HT] per-wave hash of a heavy read's regions by 512-bp bin
+    int32_t* rnext;           // [n_seeds] the next region of the same bin (index in the read), -1: none
     AlnReg* pre;              // [n_seeds] the region of each seed its chain's own walk extended, heavy reads only
     uint8_t* pre_ok;          // [n_seeds] 1: pre holds it
     AlnReg* loc;              // [n_seeds] the regions of each chain's own walk (scratch at the chain's seeds)

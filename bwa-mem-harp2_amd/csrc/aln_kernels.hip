@@ -466,30 +466,223 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_heavy_task_kernel(Aln
     }
 }
 
-// the walk of heavy read r: aln_kernel's chain loop over the regions
-// computed ahead (containment tests and seed order, and the extensions
-// mem_chain2aln_short's accepted chains did not leave).  A call, not inlined:
-// inlined into aln_heavy_kernel's persistent loop this walk hung gfx950 waves
+// is seed (s_rb, s_qb, s_len) (almost) contained in region p?
+// (software/bwamem.c:1079-1094, the test seed_wanted makes per region)
+__device__ __forceinline__ bool reg_contains(const AlnParams& P, int64_t s_rb, int s_qb, int s_len, int64_t p_rb,
+                                             int64_t p_re, int p_qb, int p_qe) {
+    if (s_rb < p_rb || s_rb + s_len > p_re || s_qb < p_qb || s_qb + s_len > p_qe) return false;
+    int qd = s_qb - p_qb;
+    int64_t rd = s_rb - p_rb;
+    int g = max_gap(P, (int)(qd < rd ? qd : rd));
+    int w = g < P.w ? g : P.w;
+    if (qd - rd < w && rd - qd < w) return true;
+    qd = p_qe - (s_qb + s_len);
+    rd = p_re - (s_rb + s_len);
+    g = max_gap(P, (int)(qd < rd ? qd : rd));
+    w = g < P.w ? g : P.w;
+    return qd - rd < w && rd - qd < w;
+}
+
+// A heavy read's regions hashed by 512-bp reference bin of their start, in
+// a per-wave table of ALN_HT slots in global memory: slot = bin << 20 |
+// (index of the bin's newest region + 1), 0 = empty; older regions of a bin
+// chain through rnext.  A region contains a seed only if it starts within
+// the read's longest region before the seed, so a containment test visits
+// one or two bins instead of every region made so far.
+constexpr int HT_BIN = 9;
+__device__ __forceinline__ uint32_t ht_home(uint64_t bin) { return ((uint32_t)bin * 2654435761u) >> 18; }
+
+// the slot of bin (found, or the empty slot where it goes): one 64-slot
+// window per round trip, the lanes probing in parallel
+__device__ __forceinline__ int ht_find(const uint64_t* ht, uint64_t bin, int lane, uint64_t& entry) {
+    uint32_t h = ht_home(bin);
+    for (int w = 0; w < ALN_HT / 64; ++w) {
+        const uint32_t sl = (h + (uint32_t)lane) & (ALN_HT - 1);
+        const uint64_t e = ht[sl];
+        const uint64_t m = __ballot(e == 0 || (e >> 20) == bin);
+        if (m) {
+            const int f = __builtin_ctzll(m);
+            entry = rl64(e, f);
+            return (int)((h + (uint32_t)f) & (ALN_HT - 1));
+        }
+        h += 64;
+    }
+    entry = 0;
+    return -1;  // full (not reached: the walk stops hashing a read before that)
+}
+
+__device__ __forceinline__ void ht_insert(uint64_t* ht, int32_t* rnext, int64_t rb, int idx, int lane) {
+    uint64_t e;
+    const uint64_t bin = (uint64_t)rb >> HT_BIN;
+    const int sl = uni(ht_find(ht, bin, lane, e));
+    if (lane == 0) {
+        rnext[idx] = e ? (int32_t)(e & 0xFFFFF) - 1 : -1;
+        if (sl >= 0) ht[sl] = bin << 20 | (uint64_t)(idx + 1);
+    }
+    __threadfence_block();  // the next probe of this wave must see the slot
+}
+
+__device__ __forceinline__ int64_t shr64(int64_t v, int64_t first) {  // wave_shr:1, lane 0 takes first
+    return (int64_t)((uint64_t)(uint32_t)kswd::wave_shr1((int)(uint32_t)v, (int)(uint32_t)first) |
+                     (uint64_t)(uint32_t)kswd::wave_shr1((int)(v >> 32), (int)(first >> 32)) << 32);
+}
+
+// The walk of heavy read r: aln_kernel's chain loop over the regions computed
+// ahead.  A heavy read walks thousands of chains one after the other, so the
+// walk keeps what it touches in registers instead of round trips to memory:
+//  * the newest 64 regions in a register ring (lane i: the i-th newest), so
+//    the containment test of a seed is one ballot unless it must look further
+//    back (then the older regions are scanned in memory, newest first);
+//  * a chain of <= 64 seeds in registers, lane k holding the seed of rank k in
+//    the reference's order (ks_introsort of len << 32 | index) and its region
+//    computed ahead, so the "long overlapping seed disagrees" test
+//    (software/bwamem.c:1098-1109) is one ballot over the lanes above k and a
+//    made region is one store from lane k.
+// Longer chains take chain_full (and empty the ring).  A call, not inlined:
+// inlined into aln_heavy_kernel's persistent loop the walk hung gfx950 waves
 // (ROCm 7.2 compiler; the same code behind a call ran).
 template <int KC>
 __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, int r) {
     const int lane = threadIdx.x & 63;
     const int L = uni((int)(P.offs[r + 1] - P.offs[r]));
+    const uint8_t* query = P.codes + P.offs[r];
     const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
     AlnReg* regs = P.raw + P.seed_off[r];
     int nreg = 0;
+    int64_t g_rb = 0, g_re = 0;  // the ring
+    int g_qb = 0, g_qe = 0, rc = 0;
+    // the bin hash, for reads with many regions (not with more than the
+    // table holds, or than 20-bit indices do)
+    const uint64_t cap = uni64(P.seed_off[r + 1] - P.seed_off[r]);
+    const bool hashed = c1 - c0 >= P.hash_min && cap < (1u << 20) - 1 && cap + (c1 - c0) < ALN_HT / 2;
+    uint64_t* ht = P.ht + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * ALN_HT;
+    int32_t* rnext = P.rnext + P.seed_off[r];
+    int64_t maxlen = 0;  // the longest region so far
+    if (hashed) {
+        for (int i = lane; i < ALN_HT; i += 64) ht[i] = 0;
+        __threadfence_block();
+    }
     for (uint64_t c = c0; c < c1; ++c) {
         OutChain ch = P.chains[c];
-        ch.n = uni(ch.n);
-        if (ch.n <= 0) continue;
+        const int n = uni(ch.n);
+        if (n <= 0) continue;
         if (uni((int)P.short_ok[c])) {
-            if (lane == 0) regs[nreg] = P.pre_short[c];
+            const AlnReg* a = P.pre_short + c;
+            if (lane == 0) regs[nreg] = *a;
+            g_rb = shr64(g_rb, uni64((uint64_t)a->rb)), g_re = shr64(g_re, uni64((uint64_t)a->re));
+            g_qb = kswd::wave_shr1(g_qb, uni(a->qb)), g_qe = kswd::wave_shr1(g_qe, uni(a->qe));
+            rc = rc < 64 ? rc + 1 : 64;
+            if (hashed) {
+                const int64_t rb = (int64_t)uni64((uint64_t)a->rb), re = (int64_t)uni64((uint64_t)a->re);
+                maxlen = re - rb > maxlen ? re - rb : maxlen;
+                ht_insert(ht, rnext, rb, nreg, lane);
+            }
             ++nreg;
+            continue;
+        }
+        const SeedRec* S = P.seeds + ch.seed_off;
+        if (n > 64) {
             __threadfence_block();
-        } else {
-            chain_full<KC, CM_REPLAY>(P, P.codes + P.offs[r], L, P.seeds + ch.seed_off, ch.n, P.srt + ch.seed_off, regs,
-                                      nreg, lane, P.pre + ch.seed_off, P.pre_ok + ch.seed_off, P.span[2 * c],
-                                      P.span[2 * c + 1]);
+            const int before = nreg;
+            chain_full<KC, CM_REPLAY>(P, query, L, S, n, P.srt + ch.seed_off, regs, nreg, lane, P.pre + ch.seed_off,
+                                      P.pre_ok + ch.seed_off, P.span[2 * c], P.span[2 * c + 1]);
+            rc = 0;
+            if (hashed) {
+                __threadfence_block();
+                for (int i = before; i < nreg; ++i) {
+                    const int64_t rb = (int64_t)uni64((uint64_t)regs[i].rb), re = (int64_t)uni64((uint64_t)regs[i].re);
+                    maxlen = re - rb > maxlen ? re - rb : maxlen;
+                    ht_insert(ht, rnext, rb, i, lane);
+                }
+            }
+            continue;
+        }
+        // the chain's seeds, rank-ordered across the lanes
+        SeedRec my{0, 0, 0};
+        if (lane < n) my = S[lane];
+        const uint64_t key = lane < n ? ((uint64_t)(uint32_t)my.len << 32 | (uint32_t)lane) : ~0ull;
+        int rank = 0;
+        for (int t = 0; t < n; ++t) rank += rl64(key, t) < key;
+        const int dst = (lane < n ? rank : lane) << 2;  // a permutation of the 64 lanes
+        const int64_t s_rb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)my.rbeg) |
+                                       (uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(my.rbeg >> 32)) << 32);
+        const int s_qb = __builtin_amdgcn_ds_permute(dst, my.qbeg);
+        const int s_len = __builtin_amdgcn_ds_permute(dst, my.len);
+        const int s_idx = __builtin_amdgcn_ds_permute(dst, lane);
+        AlnReg mine{};
+        int mine_ok = 0;
+        if (lane < n) {
+            mine = P.pre[ch.seed_off + s_idx];
+            mine_ok = P.pre_ok[ch.seed_off + s_idx];
+        }
+        bool skipped = false;
+        for (int k = n - 1; k >= 0; --k) {
+            const int64_t k_rb = (int64_t)rl64((uint64_t)s_rb, k);
+            const int k_qb = kswd::rl(s_qb, k), k_len = kswd::rl(s_len, k);
+            bool hit = __ballot(lane < rc && reg_contains(P, k_rb, k_qb, k_len, g_rb, g_re, g_qb, g_qe)) != 0;
+            const int older = nreg - rc;  // regions only in memory: regs[0 .. older)
+            if (!hit && older > 0 && hashed) {  // the bins a containing region can start in
+                __threadfence_block();
+                const uint64_t b1 = (uint64_t)k_rb >> HT_BIN;
+                const uint64_t b0 = (uint64_t)(k_rb - maxlen > 0 ? k_rb - maxlen : 0) >> HT_BIN;
+                for (uint64_t b = b0; b <= b1 && !hit; ++b) {
+                    uint64_t e;
+                    (void)ht_find(ht, b, lane, e);
+                    int i = e ? uni((int)(e & 0xFFFFF) - 1) : -1;
+                    while (i >= 0 && !hit) {
+                        const AlnReg* p = regs + i;
+                        hit = reg_contains(P, k_rb, k_qb, k_len, (int64_t)uni64((uint64_t)p->rb),
+                                           (int64_t)uni64((uint64_t)p->re), uni(p->qb), uni(p->qe));
+                        i = uni(rnext[i]);
+                    }
+                }
+            } else if (!hit && older > 0) {
+                __threadfence_block();
+                for (int ib = 0; ib < older && !hit; ib += 64) {
+                    const int i = older - 1 - ib - lane;
+                    bool ok = false;
+                    if (i >= 0) {
+                        const AlnReg p = regs[i];
+                        ok = reg_contains(P, k_rb, k_qb, k_len, p.rb, p.re, p.qb, p.qe);
+                    }
+                    hit = __ballot(ok) != 0;
+                }
+            }
+            bool wanted = !hit;
+            if (hit) {  // extended anyway if a longer overlapping seed above k disagrees with it
+                bool ok = false;
+                if (lane > k && lane < n && !skipped && !(s_len < k_len * .95)) {
+                    if (k_qb <= s_qb && k_qb + k_len - s_qb >= k_len >> 2 && (int64_t)(s_qb - k_qb) != s_rb - k_rb)
+                        ok = true;
+                    if (s_qb <= k_qb && s_qb + s_len - k_qb >= k_len >> 2 && (int64_t)(k_qb - s_qb) != k_rb - s_rb)
+                        ok = true;
+                }
+                wanted = __ballot(ok) != 0;
+                if (!wanted && lane == k) skipped = true;
+            }
+            if (!wanted) continue;
+            int64_t a_rb, a_re;
+            int a_qb, a_qe;
+            if (kswd::rl(mine_ok, k)) {
+                if (lane == k) regs[nreg] = mine;
+                a_rb = (int64_t)rl64((uint64_t)mine.rb, k), a_re = (int64_t)rl64((uint64_t)mine.re, k);
+                a_qb = kswd::rl(mine.qb, k), a_qe = kswd::rl(mine.qe, k);
+            } else {
+                __threadfence_block();
+                seed_region_call<KC>(P, query, L, S, n, kswd::rl(s_idx, k), P.span[2 * c], P.span[2 * c + 1],
+                                     regs + nreg);
+                __threadfence_block();
+                a_rb = (int64_t)uni64((uint64_t)regs[nreg].rb), a_re = (int64_t)uni64((uint64_t)regs[nreg].re);
+                a_qb = uni(regs[nreg].qb), a_qe = uni(regs[nreg].qe);
+            }
+            g_rb = shr64(g_rb, a_rb), g_re = shr64(g_re, a_re);
+            g_qb = kswd::wave_shr1(g_qb, a_qb), g_qe = kswd::wave_shr1(g_qe, a_qe);
+            rc = rc < 64 ? rc + 1 : 64;
+            if (hashed) {
+                maxlen = a_re - a_rb > maxlen ? a_re - a_rb : maxlen;
+                ht_insert(ht, rnext, a_rb, nreg, lane);
+            }
+            ++nreg;
         }
     }
     if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
@@ -566,8 +759,10 @@ extern "C" hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStre
 extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
     hipLaunchKernelGGL(smem::aln_heavy_task_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
     if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_task_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
-    hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu), dim3(256), 0, st, *P);
-    if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu), dim3(256), 0, st, *P);
+    // the walk kernels use the per-wave hash tables in turn (same stream)
+    hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
+    if (long_reads)
+        hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

@@ -133,10 +133,13 @@ struct AlnHeavyBufs {
     DevBuf<int32_t> heavy;
     DevBuf<uint64_t> hcnt, hoff, hscnt;
     DevBuf<int64_t> span;
+    DevBuf<uint64_t> ht;
+    DevBuf<int32_t> rnext;
     DevBuf<smem::AlnReg> pre, pre_short, loc;
     DevBuf<uint8_t> short_ok, pre_ok, tmp;
     void release() {
-        heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); pre.release();
+        heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); ht.release(); rnext.release();
+        pre.release();
         pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
     }
 };
@@ -1232,6 +1235,10 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
     const int n = P.n_reads;
     P.heavy_min = aln_heavy_min();
     P.heavy_seeds = aln_heavy_seeds();
+    {   // SMEM_ALN_HASH_MIN: chains from which a heavy read's walk hashes its regions (tests force 1)
+        const char* e = getenv("SMEM_ALN_HASH_MIN");
+        P.hash_min = e ? (uint32_t)std::max(1, atoi(e)) : 64u;
+    }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
         HIP_TRY(H.heavy.ensure(n));
@@ -1255,8 +1262,10 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.pre_short.ensure(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(H.short_ok.ensure(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(H.span.ensure(2 * std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.ht.ensure((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+        HIP_TRY(H.rnext.ensure(std::max<uint64_t>(n_seeds, 1)));
         P.hoff = H.hoff.p, P.pre = H.pre.p, P.loc = H.loc.p, P.pre_ok = H.pre_ok.p, P.pre_short = H.pre_short.p;
-        P.short_ok = H.short_ok.p, P.span = H.span.p;
+        P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
         HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, st));
     }
     HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));

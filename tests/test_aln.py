@@ -89,12 +89,14 @@ def test_aln_gpu_vs_reference(gpu_device, fix, heavy, monkeypatch):
 
 def _heavy_env(monkeypatch, heavy):
     """heavy = "min[:seeds]": SMEM_ALN_HEAVY_MIN / SMEM_ALN_HEAVY_SEEDS, the
-    chain / seed counts from which a read takes the heavy-read path."""
+    chain / seed counts from which a read takes the heavy-read path; its walk
+    then always uses the region bin hash (SMEM_ALN_HASH_MIN = 1)."""
     if heavy:
         m, _, sd = heavy.partition(":")
         monkeypatch.setenv("SMEM_ALN_HEAVY_MIN", m)
         if sd:
             monkeypatch.setenv("SMEM_ALN_HEAVY_SEEDS", sd)
+        monkeypatch.setenv("SMEM_ALN_HASH_MIN", "1")  # every heavy walk through the bin hash
 
 
 def _tmpdir():

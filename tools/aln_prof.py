@@ -18,11 +18,14 @@ def main():
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--launches", type=int, default=2)
     p.add_argument("--cycles", default=None, help="write per-read shader cycles of the last launch here (u64)")
+    p.add_argument("--lib", default=None, help="another libsmemgpu build (diagnostics)")
     own, rest = p.parse_known_args()
     import torch
     torch.cuda.device_count()  # as bench.py's Dist does, before libsmemgpu touches the device
     import bench
     import smemgpu
+    if own.lib:
+        smemgpu.lib.LIB_PATH = os.path.abspath(own.lib)
     from oracle import oracle
     a = bench.parse(rest)
     idx, _, sa, codes = bench.get_index(a, 0, lambda: None, 0)

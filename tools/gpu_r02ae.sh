@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r02ag
+O=gpurun_out/r02an
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_aln.py -m gpu -x -q --timeout 60 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
