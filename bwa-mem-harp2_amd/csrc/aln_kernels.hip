@@ -440,9 +440,14 @@ __device__ __forceinline__ void heavy_chain_task(const AlnParams& P, uint32_t nh
             P.span[2 * c] = r0;
             P.span[2 * c + 1] = r1;
         }
-        for (int i = lane; i < ch.n; i += 64) P.pre_ok[ch.seed_off + i] = (uint8_t)!ok;
+        const bool local = P.spec_local != 0;
+        for (int i = lane; i < ch.n; i += 64) P.pre_ok[ch.seed_off + i] = (uint8_t)(!ok && !local);
         __threadfence_block();
-        if (!ok) {  // every seed's region: the read's walk decides which of them are made
+        if (!ok && local) {  // the seeds the chain's own walk extends (the read's walk computes any other)
+            int nl = 0;
+            chain_full<KC, CM_RECORD>(P, query, L, S, ch.n, P.srt + ch.seed_off, P.loc + ch.seed_off, nl, lane,
+                                      P.pre + ch.seed_off, P.pre_ok + ch.seed_off);
+        } else if (!ok) {  // every seed's region: the read's walk decides which of them are made
             for (int i = 0; i < ch.n; ++i) {
                 const AlnReg a = seed_region<KC>(P, query, L, S, ch.n, S[i], r0, r1, lane);
                 if (lane == 0) P.pre[ch.seed_off + i] = a;

@@ -1238,6 +1238,8 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
     {   // SMEM_ALN_HASH_MIN: chains from which a heavy read's walk hashes its regions (tests force 1)
         const char* e = getenv("SMEM_ALN_HASH_MIN");
         P.hash_min = e ? (uint32_t)std::max(1, atoi(e)) : 64u;
+        const char* l = getenv("SMEM_ALN_SPEC_LOCAL");
+        P.spec_local = l ? (uint32_t)atoi(l) : 0u;
     }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
