@@ -66,8 +66,8 @@ BLOCK = 1 << 18          # reads per block of the read stream (shards are whole 
 
 # BASELINE.json configs: per-GPU shapes
 CONFIGS = {
-    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=8_000_000,
-               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1]); 8M streamed"),
+    "c2": dict(read_len=150, sub=0.02, k=19, pairs=False, stream_reads=16_000_000,
+               what="human_g1k_v37-sized index in HBM, 1M x 150 bp SE (BASELINE configs[1]); 16M streamed"),
     "c3": dict(read_len=150, sub=0.02, k=19, pairs=True, stream_reads=25_000_000,
                what="C3 on one GPU: its shard of 100M x 150 bp PE on 8 GPUs = 12.5M pairs, insert N(500, 50), "
                     "mates interleaved in one chunk"),
