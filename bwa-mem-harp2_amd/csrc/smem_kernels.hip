@@ -266,25 +266,20 @@ __device__ __forceinline__ uint64_t occ_cgt(const uint4& c, int i) {
     return (uint64_t)((c.w >> (2 * i)) & 3) << 32 | lo;
 }
 
-// C, G, T among the first pos+1 (pos < 64) symbols of the bucket
+// C, G, T among the first pos+1 (pos < 64) symbols of the bucket: the 64
+// MSB-first 2-bit symbols as two 64-bit halves, each masked to its share of
+// the prefix by one shift (8 fewer VALU per rank than four masked words)
 __device__ __forceinline__ void count_cgt4(const uint4& v, uint32_t pos, uint32_t& C, uint32_t& G, uint32_t& T) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    const uint32_t nfull = pos >> 4;
-    const uint32_t tail = ~((1u << ((15u - (pos & 15u)) << 1)) - 1u);
-    uint32_t sT = 0, sLo = 0, sHi = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-        const uint32_t m = i < nfull ? 0xFFFFFFFFu : (i == nfull ? tail : 0u);
-        const uint32_t x = w[i] & m;
-        const uint32_t lo = x & 0x55555555u;
-        const uint32_t hi = (x >> 1) & 0x55555555u;
-        sT += __popc(lo & hi);
-        sLo += __popc(lo);
-        sHi += __popc(hi);
-    }
-    T = sT;
-    C = sLo - sT;
-    G = sHi - sT;
+    const uint64_t a = (uint64_t)v.x << 32 | v.y, b = (uint64_t)v.z << 32 | v.w;
+    const uint32_t n = pos + 1;  // symbols counted, 1..64
+    const uint64_t ma = n >= 32 ? ~0ull : ~0ull << (64 - 2 * n);
+    const uint64_t mb = n <= 32 ? 0ull : ~0ull << (128 - 2 * n);
+    const uint64_t xa = a & ma, xb = b & mb;
+    constexpr uint64_t K = 0x5555555555555555ull;
+    const uint64_t loa = xa & K, hia = (xa >> 1) & K, lob = xb & K, hib = (xb >> 1) & K;
+    T = __popcll(loa & hia) + __popcll(lob & hib);
+    C = __popcll(loa) + __popcll(lob) - T;
+    G = __popcll(hia) + __popcll(hib) - T;
 }
 
 // ---- Occ192: 64-B lines of 192 BWT symbols (a third fewer index bytes than
