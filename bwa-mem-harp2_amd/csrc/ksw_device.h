@@ -195,6 +195,179 @@ __device__ __forceinline__ KswResult extend_wave(const ExtIn& T, QF qsym, TF tsy
     return KswResult{mx, max_j + 1, max_i + 1, max_ie + 1, gscore, max_off};
 }
 
+// ---- ksw_extend2 on 16-lane groups: four problems per wave ----
+// The same recurrences as extend_wave with the query columns of a problem on
+// the 16 lanes of one DPP row (j = 16 c + lane16, c < KC): the in-row prefix
+// max is four row_shr steps, the one-column shift a row_shr:1, and the row's
+// lane 15 reaches its lanes by ds_swizzle (and 0x10, or 0x0f).  Every group
+// walks its own problem's rows; a group whose problem ended (or that has
+// none) idles until the wave's last group is done.
+__device__ __forceinline__ int scan16_max(int v) {
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = imax(v, __builtin_amdgcn_update_dpp(NEG, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    return v;
+}
+__device__ __forceinline__ int row_shr1(int v, int first) {
+    return __builtin_amdgcn_update_dpp(first, v, 0x111, 0xf, 0xf, false);  // row_shr:1, lane16 0 takes first
+}
+__device__ __forceinline__ int bcast15(int v) { return __builtin_amdgcn_ds_swizzle(v, 0x1F0); }
+__device__ __forceinline__ int from16(int v, int l16) {  // lane l16 of this lane's group
+    return __builtin_amdgcn_ds_bpermute((((int)threadIdx.x & 0x30) | l16) << 2, v);
+}
+
+template <int KC, class QF, class TF>
+__device__ __forceinline__ KswResult extend_group16(const ExtIn& T, bool active, QF qsym, TF tsym, const int8_t* mat,
+                                                    int o_del, int e_del, int o_ins, int e_ins, int top) {
+    static_assert(KC <= 16, "columns < 256");
+    const int l16 = threadIdx.x & 15;
+    const int g = (threadIdx.x >> 4) & 3;
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    const int qlen = active ? T.qlen : 0, tlen = active ? T.tlen : 0;
+    const int h0 = T.h0 > 0 ? T.h0 : 0;
+    const int eh1 = h0 > oe_ins ? h0 - oe_ins : 0;
+    uint32_t sc[KC];
+    int sc4[KC], hp[KC], ee[KC];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+        const int j = 16 * c + l16;
+        const int qc = j < qlen ? (int)qsym(j) : 0;
+        sc[c] = (uint32_t)(uint8_t)mat[qc] | (uint32_t)(uint8_t)mat[5 + qc] << 8 |
+                (uint32_t)(uint8_t)mat[10 + qc] << 16 | (uint32_t)(uint8_t)mat[15 + qc] << 24;
+        sc4[c] = mat[20 + qc];
+        int h = 0;
+        if (j == 0) h = h0;
+        else if (j == 1) h = eh1;
+        else if (j <= qlen && eh1 - (j - 2) * e_ins > e_ins) h = eh1 - (j - 1) * e_ins;
+        hp[c] = h;
+        ee[c] = 0;
+    }
+    int w = T.w;
+    if (active) {  // band limit (software/ksw.c:401-406)
+        int lim = (int)((double)(qlen * top + T.end_bonus - o_ins) / e_ins + 1.);
+        lim = imax(lim, 1);
+        w = w < lim ? w : lim;
+        lim = (int)((double)(qlen * top + T.end_bonus - o_del) / e_del + 1.);
+        lim = imax(lim, 1);
+        w = w < lim ? w : lim;
+    }
+    int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+    int beg = 0, end = qlen;
+    bool done = !active || tlen <= 0;
+    int tcache = 0;
+    for (int i = 0;; ++i) {
+        if (__ballot(!done) == 0) break;
+        if ((i & 15) == 0) tcache = !done && i + l16 < tlen ? (int)tsym(i + l16) : 0;
+        const int tc = from16(tcache, i & 15);
+        if (!done) {
+            int h1 = h0 - (o_del + e_del * (i + 1));
+            if (h1 < 0) h1 = 0;
+            if (beg < i - w) beg = i - w;
+            if (end > i + w + 1) end = i + w + 1;
+            if (end > qlen) end = qlen;
+            // D and the in-chunk prefix of every chunk first (independent),
+            // then the carries across chunks from the chunk totals: the
+            // swizzles of the totals pipeline instead of chaining
+            int H[KC], D[KC], incl[KC], tot[KC];
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const int j = 16 * c + l16;
+                const bool valid = j >= beg && j < end;
+                const int sv = tc < 4 ? (int)(int8_t)(sc[c] >> (8 * tc)) : sc4[c];
+                D[c] = imax(hp[c] + sv, ee[c]);
+                incl[c] = NEG;
+                tot[c] = NEG;
+                if (16 * c >= end || 16 * c + 15 < beg) continue;  // chunk outside the band (group-uniform)
+                incl[c] = scan16_max(valid ? D[c] + j * e_ins : NEG);
+                tot[c] = bcast15(incl[c]);
+            }
+            int carry = NEG, key = NEG;
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const int j = 16 * c + l16;
+                H[c] = 0;
+                if (16 * c >= end || 16 * c + 15 < beg) continue;
+                const bool valid = j >= beg && j < end;
+                const int excl = imax(row_shr1(incl[c], NEG), carry);
+                carry = imax(carry, tot[c]);
+                const int f = imax(0, excl - oe_ins - (j - 1) * e_ins);
+                const int h = imax(D[c], f);
+                if (valid) {
+                    H[c] = h;
+                    key = imax(key, h << 8 | j);  // ascending j: ties keep the last column
+                }
+            }
+            const bool nonempty = beg < end;
+            int m = 0, mj = -1;
+            if (nonempty) {
+                const int kmax = bcast15(scan16_max(key));
+                m = kmax >> 8;
+                mj = kmax & 255;
+            }
+            int prev_last = 0;
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const int j = 16 * c + l16;
+                if (16 * c >= end || 16 * c + 15 < beg) {
+                    prev_last = 0;
+                    continue;
+                }
+                const int up = row_shr1(H[c], prev_last);
+                prev_last = bcast15(H[c]);
+                if (j >= beg && j < end) {
+                    ee[c] = imax(ee[c] - e_del, imax(H[c] - oe_del, 0));
+                    hp[c] = j == beg ? h1 : up;
+                }
+            }
+            int hlast = h1;
+            if (nonempty) {
+                const int ce = (end - 1) >> 4, le = (end - 1) & 15;
+#pragma unroll
+                for (int c = 0; c < KC; ++c)
+                    if (c == ce) hlast = from16(H[c], le);
+            }
+#pragma unroll
+            for (int c = 0; c < KC; ++c)
+                if (16 * c + l16 == end) {
+                    hp[c] = hlast;
+                    ee[c] = 0;
+                }
+            if ((nonempty ? end : beg) == qlen) {
+                if (hlast >= gscore) max_ie = i;
+                gscore = imax(gscore, hlast);
+            }
+            bool stop = m == 0;
+            if (!stop) {
+                if (m > mx) {
+                    mx = m, max_i = i, max_j = mj;
+                    const int o = mj > i ? mj - i : i - mj;
+                    max_off = imax(max_off, o);
+                } else if (T.zdrop > 0) {
+                    const int di = i - max_i, dj = mj - max_j;
+                    const int drop = di > dj ? mx - m - (di - dj) * e_del : mx - m - (dj - di) * e_ins;
+                    stop = drop > T.zdrop;
+                }
+            }
+            if (!stop) {  // refit the band around mj (software/ksw.c:463-466)
+                int zlo = -1, zhi = 0x7fffffff;
+#pragma unroll
+                for (int c = 0; c < KC; ++c) {
+                    const int j = 16 * c + l16;
+                    const uint32_t lo = (uint32_t)(__ballot(hp[c] == 0 && j >= beg && j <= mj) >> (16 * g)) & 0xFFFFu;
+                    const uint32_t hi = (uint32_t)(__ballot(hp[c] == 0 && j >= mj + 2 && j <= end) >> (16 * g)) & 0xFFFFu;
+                    if (lo) zlo = 16 * c + 31 - __builtin_clz(lo);
+                    if (hi && zhi == 0x7fffffff) zhi = 16 * c + __builtin_ctz(hi);
+                }
+                beg = zlo >= 0 ? zlo + 1 : beg;
+                end = zhi != 0x7fffffff ? zhi : end + 1;
+            }
+            done = stop || i + 1 >= tlen;
+        }
+    }
+    return KswResult{mx, max_j + 1, max_i + 1, max_ie + 1, gscore, max_off};
+}
+
 // ---- ksw_align2's local SW (software/ksw.c:110-364), one wave per problem ----
 constexpr int SW_XBYTE = 0x10000, SW_XSTOP = 0x20000, SW_XSUBO = 0x40000, SW_XSTART = 0x80000;
 

@@ -16,7 +16,10 @@
 // column on ties), the to-end score, z-drop and the band refit follow the
 // serial code step by step with wave reductions and ballots, so every output
 // (score, qle, tle, gtle, gscore, max_off) is the reference's.
+#include <stdlib.h>
+
 #include "ksw_kernels.h"
+#include "ksw_device.h"
 
 namespace smem {
 namespace {
@@ -189,10 +192,47 @@ __global__ __launch_bounds__(256) void ksw_extend_kernel(KswParams K) {
     }
 }
 
+// four problems per wave on 16-lane groups (kswd::extend_group16)
+__global__ __launch_bounds__(256) void ksw_extend_g16_kernel(KswParams K) {
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int n_waves = (int)((gridDim.x * blockDim.x) >> 6);
+    const int g = (threadIdx.x >> 4) & 3;
+    int top = 0;
+    for (int k = 0; k < 25; ++k) top = imax(top, (int)K.mat[k]);
+    for (int base = wave * 4; base < K.n; base += n_waves * 4) {
+        const int it = base + g;
+        const bool active = it < K.n;
+        const KswTask T = K.task[active ? it : base];
+        const uint8_t* q = K.q + T.q_off;
+        const uint8_t* tg = K.t + T.t_off;
+        // columns per lane by the longest query of the wave's four problems
+        int ql = active ? T.qlen : 0;
+        ql = imax(ql, __shfl_xor(ql, 16));
+        ql = imax(ql, __shfl_xor(ql, 32));
+        ql = __builtin_amdgcn_readfirstlane(ql);
+        const kswd::ExtIn E{T.qlen, T.tlen, T.w, T.end_bonus, T.zdrop, T.h0};
+        auto qf = [&](int j) { return (int)q[j]; };
+        auto tf = [&](int i) { return (int)tg[i]; };
+        KswResult r;
+        if (ql < 32) r = kswd::extend_group16<2>(E, active, qf, tf, K.mat, K.o_del, K.e_del, K.o_ins, K.e_ins, top);
+        else if (ql < 64) r = kswd::extend_group16<4>(E, active, qf, tf, K.mat, K.o_del, K.e_del, K.o_ins, K.e_ins, top);
+        else if (ql < 128) r = kswd::extend_group16<8>(E, active, qf, tf, K.mat, K.o_del, K.e_del, K.o_ins, K.e_ins, top);
+        else r = kswd::extend_group16<16>(E, active, qf, tf, K.mat, K.o_del, K.e_del, K.o_ins, K.e_ins, top);
+        if (active && (threadIdx.x & 15) == 0) K.out[it] = r;
+    }
+}
+
 }  // namespace smem
 
 extern "C" hipError_t smem_launch_ksw(const smem::KswParams* K, int n_cu, hipStream_t st) {
     if (K->n <= 0) return hipSuccess;
+    const char* g16e = getenv("SMEM_KSW_G16");  // the 16-lane group kernel (A/B)
+    const bool g16 = g16e && atoi(g16e);
+    if (g16) {  // four problems per wave
+        const int waves = (K->n + 3) / 4 < n_cu * 32 ? (K->n + 3) / 4 : n_cu * 32;
+        hipLaunchKernelGGL(smem::ksw_extend_g16_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, *K);
+        return hipGetLastError();
+    }
     const int waves = K->n < n_cu * 32 ? K->n : n_cu * 32;
     hipLaunchKernelGGL(smem::ksw_extend_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, *K);
     return hipGetLastError();

@@ -16,6 +16,15 @@ from tests import golden_data
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["wave", "g16"], autouse=True)
+def ksw_kernel(request, monkeypatch):
+    """Every test on both kernels: one problem per wave, and four per wave on
+    16-lane groups (SMEM_KSW_G16, kswd::extend_group16)."""
+    if request.param == "g16":
+        monkeypatch.setenv("SMEM_KSW_G16", "1")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def gpu(gpu_device):
     import smemgpu

@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r02ah
+O=gpurun_out/r02ao
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/u -o u -- python3 -u tools/aln_prof.py --launches 1 > $O/u.log 2>&1 || exit 1
