@@ -1304,6 +1304,10 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     // diagnostics: SMEM_ALN_CYCLES=<file> writes the shader cycles each read took (u64 per read)
     const char* cyc_path = getenv("SMEM_ALN_CYCLES");
     DevBuf<uint64_t> d_cyc;
+    struct Free {
+        DevBuf<uint64_t>& b;
+        ~Free() { b.release(); }  // every return path, HIP_TRY's included
+    } free_cyc{d_cyc};
     if (cyc_path) {
         HIP_TRY(d_cyc.ensure(std::max(n, 1)));
         P.cyc = d_cyc.p;
@@ -1334,7 +1338,6 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
             fclose(f);
         }
     }
-    d_cyc.release();
     b->aln_ran = true;
     b->aln_fetched = false;
     return SMEM_OK;
