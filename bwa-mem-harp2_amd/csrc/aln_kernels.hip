@@ -349,7 +349,10 @@ template <int KC>
 __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
     const int lane = threadIdx.x & 63;
     constexpr uint32_t CLAIM = 4;  // reads per work-queue claim
-    for (;;) {
+    // light_claims > 0: the wave leaves after that many claims (the grid then
+    // covers every read), so blocks retire while kernels of another stream wait
+    // for CU slots
+    for (uint32_t k = 0; P.light_claims == 0 || k < P.light_claims; ++k) {
         uint32_t r0 = 0;
         if (lane == 0) r0 = atomicAdd(&P.ctr[KC > 4 ? 1 : 0], CLAIM);
         r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0);
@@ -745,13 +748,18 @@ extern "C" hipError_t smem_launch_ksw_align2(const smem::KswAParams* K, int n_cu
 
 extern "C" hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;
-    // up to 8 blocks of 4 waves per CU, every wave claiming reads from the queue
+    // up to 8 blocks of 4 waves per CU, every wave claiming reads from the
+    // queue; with light_claims, enough blocks for every read
     const int waves = (P->n_reads + 3) / 4;
-    const int blocks = std::max(1, std::min(n_cu * 8, (waves + 3) / 4));
+    int blocks = std::max(1, std::min(n_cu * 8, (waves + 3) / 4)), blocks16 = std::max(1, std::min(n_cu * 2, blocks));
+    if (P->light_claims) {
+        const uint64_t per_block = 4ull * 4 * P->light_claims;  // 4 waves x 4 reads per claim
+        blocks = blocks16 = (int)std::max<uint64_t>(1, (P->n_reads + per_block - 1) / per_block);
+    }
     hipLaunchKernelGGL(smem::aln_kernel<4>, dim3(blocks), dim3(256), 0, st, *P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !long_reads) return e;
-    hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(std::max(1, std::min(n_cu * 2, blocks))), dim3(256), 0, st, *P);
+    hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(blocks16), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

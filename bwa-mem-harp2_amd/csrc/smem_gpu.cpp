@@ -148,6 +148,10 @@ struct smem_batch {
     smem_gpu_t* g = nullptr;
     hipStream_t st = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // chains -> regions: the light reads' kernel runs on st2 beside the heavy
+    // reads' kernels on st, joined by ev_join (created on first use)
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_join = nullptr;
     int max_reads = 0, max_len = 0;
     uint64_t max_bases = 0;
     uint32_t cap_intv = 0, cap_calls = 0, cap_list = 0;
@@ -384,6 +388,8 @@ void smem_batch_destroy(smem_batch_t* b) {
     b->h_intv_off.release(); b->h_call_off.release();
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (b->ev_join) (void)hipEventDestroy(b->ev_join);
+    if (b->st2) (void)hipStreamDestroy(b->st2);
     if (b->st) (void)hipStreamDestroy(b->st);
     delete b;
 }
@@ -1212,6 +1218,19 @@ int smem_gpu_load_pac(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
     return SMEM_OK;
 }
 
+// SMEM_ALN_STREAMS=1: the light and heavy reads' kernels one after the other
+// on the batch's stream (default 2: side by side)
+static bool aln_two_streams() {
+    const char* e = getenv("SMEM_ALN_STREAMS");
+    return !(e && atoi(e) == 1);
+}
+// SMEM_ALN_LIGHT_CLAIMS: beside the heavy kernels, a light wave's claims of 4
+// reads before it exits (default 1; 0: persistent)
+static uint32_t aln_light_claims() {
+    const char* e = getenv("SMEM_ALN_LIGHT_CLAIMS");
+    return e ? (uint32_t)std::max(0, atoi(e)) : 1u;
+}
+
 // reads with at least this many chains, or seeds, take the heavy path
 // (SMEM_ALN_HEAVY_MIN / SMEM_ALN_HEAVY_SEEDS override; a zero chain count =
 // never): tandem-repeat reads carry hundreds to thousands of chains or seeds,
@@ -1230,8 +1249,14 @@ static uint32_t aln_heavy_seeds() {
 // smem::ALN_CTRS): heavy reads listed, their chains' and seeds' regions
 // computed ahead one wave per chain and walked one wave per read; the other
 // reads one wave each
+// classify -> (heavy reads: chain tasks, then the walk, on st) beside (light
+// reads on st2), joined back into st.  The two sets of reads write disjoint
+// slots (regions and sort scratch at each read's seed offset, n_regs per read)
+// and claim from different counters, so they can share the GPU: the light
+// kernel fills the CUs the walk's few long reads leave idle.  st2 == nullptr:
+// everything on st.
 static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_t n_seeds, bool long_reads,
-                   AlnHeavyBufs& H, hipStream_t st) {
+                   AlnHeavyBufs& H, hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t ev_join = nullptr) {
     const int n = P.n_reads;
     P.heavy_min = aln_heavy_min();
     P.heavy_seeds = aln_heavy_seeds();
@@ -1268,6 +1293,18 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.rnext.ensure(std::max<uint64_t>(n_seeds, 1)));
         P.hoff = H.hoff.p, P.pre = H.pre.p, P.loc = H.loc.p, P.pre_ok = H.pre_ok.p, P.pre_short = H.pre_short.p;
         P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
+        if (st2 && ev_join) {
+            // the heavy kernels first (their chain tasks then the walk are the
+            // critical path); classify finished (synchronised above), so st2
+            // has nothing to wait for
+            HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, st));
+            P.light_claims = aln_light_claims();  // its blocks retire, so the walk finds CU slots
+            HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st2));
+            P.light_claims = 0;
+            HIP_TRY(hipEventRecord(ev_join, st2));
+            HIP_TRY(hipStreamWaitEvent(st, ev_join, 0));
+            return SMEM_OK;
+        }
         HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, st));
     }
     HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
@@ -1314,7 +1351,15 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     }
     HIP_TRY(hipMemsetAsync(b->d_aln_ctr.p, 0, smem::ALN_CTRS * sizeof(uint32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
-    if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->st)) return rc;
+    if (aln_two_streams() && !b->st2) {
+        int least = 0, greatest = 0;  // the light reads' stream at the lowest priority
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&b->st2, hipStreamNonBlocking, least));
+        HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    }
+    if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->st,
+                         aln_two_streams() ? b->st2 : nullptr, b->ev_join))
+        return rc;
     tmp = b->d_sa_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_aln_nregs.p, b->d_aln_regoff.p, n, b->d_sa_tmp.p, &tmp, b->st));
     HIP_TRY(hipMemcpyAsync(b->h_tot.p + 5, b->d_aln_regoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));

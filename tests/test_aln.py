@@ -90,7 +90,12 @@ def test_aln_gpu_vs_reference(gpu_device, fix, heavy, monkeypatch):
 def _heavy_env(monkeypatch, heavy):
     """heavy = "min[:seeds]": SMEM_ALN_HEAVY_MIN / SMEM_ALN_HEAVY_SEEDS, the
     chain / seed counts from which a read takes the heavy-read path; its walk
-    then always uses the region bin hash (SMEM_ALN_HASH_MIN = 1)."""
+    then always uses the region bin hash (SMEM_ALN_HASH_MIN = 1).  A "/1"
+    suffix: the light and heavy reads' kernels one after the other on the
+    batch's stream (SMEM_ALN_STREAMS=1) instead of side by side."""
+    if heavy and "/" in heavy:
+        heavy, _, streams = heavy.partition("/")
+        monkeypatch.setenv("SMEM_ALN_STREAMS", streams)
     if heavy:
         m, _, sd = heavy.partition(":")
         monkeypatch.setenv("SMEM_ALN_HEAVY_MIN", m)
@@ -125,7 +130,7 @@ def test_pack_matches_reference_pac():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,a,heavy", [(100, 1, None), (20, 1, None), (100, 2, None), (100, 1, "1"), (100, 2, "1"),
-                                       (20, 1, "3"), (100, 1, "0"), (100, 1, "1000:3")])
+                                       (20, 1, "3"), (100, 1, "0"), (100, 1, "1000:3"), (100, 1, "3/1")])
 def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a, heavy, monkeypatch):
     """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
     kernel instantiations) with substitutions and Ns; chains from the GPU

@@ -19,6 +19,8 @@ def main():
     p.add_argument("--launches", type=int, default=2)
     p.add_argument("--cycles", default=None, help="write per-read shader cycles of the last launch here (u64)")
     p.add_argument("--lib", default=None, help="another libsmemgpu build (diagnostics)")
+    p.add_argument("--env-sweep", default="", help="';'-separated settings, each ','-separated VAR=value: "
+                   "--launches launches under each, in turn (the library reads them per call)")
     own, rest = p.parse_known_args()
     import torch
     torch.cuda.device_count()  # as bench.py's Dist does, before libsmemgpu touches the device
@@ -39,14 +41,24 @@ def main():
     b.run(opt)
     b.sa(opt.min_seed_len, 10000)
     b.chain(idx.seq_len // 2)
-    for k in range(own.launches):
-        if own.cycles and k == own.launches - 1:
-            os.environ["SMEM_ALN_CYCLES"] = own.cycles
-        t = time.time()
-        b.chain2aln(oracle.aln_opt(min_seed_len=opt.min_seed_len))
-        st = b.stats()
-        print(f"chain2aln: {st['aln_ms']:.3f} ms, {st['n_regs']} regions, {st['n_chains']} chains, "
-              f"wall {1e3 * (time.time() - t):.1f} ms", flush=True)
+    settings = [s for s in own.env_sweep.split(";") if s] or [""]
+    for setting in settings:
+        kv = dict(x.split("=", 1) for x in setting.split(",") if x)
+        saved = {k: os.environ.get(k) for k in kv}
+        os.environ.update(kv)
+        for k in range(own.launches):
+            if own.cycles and k == own.launches - 1:
+                os.environ["SMEM_ALN_CYCLES"] = own.cycles
+            t = time.time()
+            b.chain2aln(oracle.aln_opt(min_seed_len=opt.min_seed_len))
+            st = b.stats()
+            print(f"chain2aln{' [' + setting + ']' if setting else ''}: {st['aln_ms']:.3f} ms, {st['n_regs']} regions, "
+                  f"{st['n_chains']} chains, wall {1e3 * (time.time() - t):.1f} ms", flush=True)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     if own.cycles:  # per-read chain / seed counts beside the cycles
         import numpy as np
         res = b.fetch()
