@@ -30,6 +30,19 @@ __device__ __forceinline__ int scan_max(int v) {
     return v;
 }
 
+// The same scan for inputs that are >= 0 or NEG, whose scan is only read
+// where it is >= 0 or where 0 and NEG give the same result: lanes with no
+// source read 0 (bound_ctrl), so each row step is one v_max_i32_dpp.
+__device__ __forceinline__ int scan_max_nn(int v) {
+    v = imax(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));  // row_shr:1
+    v = imax(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));  // row_shr:2
+    v = imax(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));  // row_shr:4
+    v = imax(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));  // row_shr:8
+    v = imax(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = imax(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+
 __device__ __forceinline__ int wave_shr1(int v, int first) {
     return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
@@ -117,7 +130,10 @@ __device__ __forceinline__ KswResult extend_wave(const ExtIn& T, QF qsym, TF tsy
             const bool valid = j >= beg && j < end;
             const int s = tc < 4 ? (int)(int8_t)(sc[c] >> (8 * tc)) : sc4[c];
             const int d = imax(hp[c] + s, ee[c]);
-            const int incl = scan_max(valid ? d + j * e_ins : NEG);
+            // d >= 0 (E >= 0), e_ins >= 1: a lane with no valid column before
+            // it reads 0 instead of NEG, and f = max(0, 0 - oe_ins - ...) = 0
+            // there as before
+            const int incl = scan_max_nn(valid ? d + j * e_ins : NEG);
             const int excl = imax(wave_shr1(incl, NEG), carry);
             carry = imax(carry, rl(incl, 63));
             const int f = imax(0, excl - oe_ins - (j - 1) * e_ins);
@@ -131,7 +147,7 @@ __device__ __forceinline__ KswResult extend_wave(const ExtIn& T, QF qsym, TF tsy
         const bool nonempty = beg < end;
         int m = 0, mj = -1;
         if (nonempty) {
-            const int kmax = wave_max(key);
+            const int kmax = rl(scan_max_nn(key), 63);  // some key >= 0
             m = kmax >> JB;
             mj = kmax & ((1 << JB) - 1);
         }

@@ -1,13 +1,12 @@
 """Chaining-stage timing on the bench workload: smem_batch_chain with and
 without the filter, and the reads that carry the most seeds / chains.
 
-    python tools/chain_prof.py [--genome-mbp 2000 --reads 1000000]
+    SMEM_CHAIN_DBG=1 python tools/chain_prof.py [--reps 2] [bench args]
 """
 import argparse
 import json
 import os
 import sys
-import tempfile
 
 import numpy as np
 
@@ -17,31 +16,25 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--genome-mbp", type=float, default=3101.804739)
-    p.add_argument("--seed", type=int, default=1)
-    p.add_argument("--reads", type=int, default=1_000_000)
+    """the bench's index, reads and options (bench args pass through, e.g.
+    --genome-profile human)"""
+    p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--reps", type=int, default=2)
-    p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
-    a = p.parse_args()
+    own, rest = p.parse_known_args()
+    import torch
+    torch.cuda.device_count()  # as bench.py's Dist does, before libsmemgpu touches the device
+    import bench
     import smemgpu
-    from smemgpu import synth
-    os.makedirs(a.cache, exist_ok=True)
-    n_bp = int(a.genome_mbp * 1e6)
-    g = synth.make_genome(n_bp, seed=a.seed, n_chrom=24)
-    key = os.path.join(a.cache, f"genome_{n_bp}_{a.seed}")
-    if not os.path.exists(key + ".bwt"):
-        idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32, gpu=True)
-        idx.write(key + ".bwt")
-        sa.write(key + ".sa")
-    idx, sa = smemgpu.Index.read(key + ".bwt"), smemgpu.SA.read(key + ".sa")
-    reads = synth.make_reads(g.codes, a.reads, 150, seed=1000 + a.seed * 7919, sub_rate=0.02, n_rate=0.001)
-    gpu = smemgpu.Gpu(idx)
+    a = bench.parse(rest)
+    a.reps = own.reps
+    idx, _, sa, codes = bench.get_index(a, 0, lambda: None, 0)
+    reads = bench.make_reads(a, 0, codes, 1)
+    gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu)
     gpu.load_sa(sa)
-    b = gpu.batch(reads.n, reads.codes.size, 150)
+    b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
     b.set_reads(reads.codes, reads.offs)
-    b.run()
-    b.sa(19, 10000)
+    b.run(smemgpu.Options(min_seed_len=a.min_seed_len))
+    b.sa(a.min_seed_len, 10000)
     out = {}
     for filt in (False, True):
         ms = []
