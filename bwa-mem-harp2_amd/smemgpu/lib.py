@@ -38,14 +38,14 @@ EXPORTED = [
 
 def source_hash() -> str:
     """The content hash bwa-mem-harp2_amd/Makefile compiles into the library
-    (SRC_HASH): sha256 of csrc/*.{hip,cpp,c,h} and include/*.h, concatenated in
-    path order, first 16 hex digits."""
+    (SRC_HASH): sha256 of csrc/*.{hip,cpp,c,h}, include/*.h and the Makefile
+    (its compiler flags), concatenated in path order, first 16 hex digits."""
     import glob
     import hashlib
     inc = os.path.join(os.path.dirname(PKG_DIR), "include")
     files = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.hip")) + glob.glob(os.path.join(PKG_DIR, "csrc", "*.cpp"))
                    + glob.glob(os.path.join(PKG_DIR, "csrc", "*.c")) + glob.glob(os.path.join(PKG_DIR, "csrc", "*.h"))
-                   + glob.glob(os.path.join(inc, "*.h")))
+                   + glob.glob(os.path.join(inc, "*.h")) + [os.path.join(PKG_DIR, "Makefile")])
     h = hashlib.sha256()
     for f in files:
         with open(f, "rb") as fh:
