@@ -91,6 +91,9 @@ struct ChainParams {
     int cluster;               // heavy path: position-cluster decomposition (0: tree path only)
     int wave_sort;             // heavy path: mem_chain_flt's introsort by the wave (0: lane 0 alone)
     uint32_t sort_lane_max;    // wave sort: segments up to this size are cut by one lane
+    int tier;                  // chain_heavy_kernel's items: 0 giants, 1 the rest, -1 both (one launch)
+    uint32_t lds_rest;         // dynamic LDS of the tier-1 launch
+    int drop_blocked;          // heavy path: drop loop's kept list first, then p2 in blocks (0: flt_drop_pruned)
     uint64_t* dbg;             // optional phase clocks of the heavy path (16 words per item)
     // output (write kernel)
     const uint64_t* chain_off; // [n_reads + 1]
@@ -102,6 +105,9 @@ struct ChainParams {
 }  // namespace smem
 
 extern "C" {
-hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_cu, hipStream_t st);
+// st2 (may be null: one launch on st): the heavy reads' second tier runs
+// there beside the giants, between ev_fork and ev_join
+hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_cu, hipStream_t st, hipStream_t st2,
+                                   hipEvent_t ev_fork, hipEvent_t ev_join);
 hipError_t smem_launch_chain_write(const smem::ChainParams* P, int n_cu, hipStream_t st);
 }

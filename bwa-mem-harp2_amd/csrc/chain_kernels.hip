@@ -481,6 +481,138 @@ __device__ __forceinline__ int flt_drop_pruned(FltRec* a, uint32_t* U, int n, fl
     return m;
 }
 
+// The same loop once more, in two passes (drop_ratio > 0).  Which chains are
+// kept does not depend on p2: chain i is dropped by the first kept j (in
+// kept order) that overlaps it significantly and may drop it, and only the
+// prefix of the kept list heavy enough to drop i is searched (as in
+// flt_drop_pruned).  Every i that the heaviest chain a[0] cannot drop is kept
+// outright (no lighter j can drop it either): that prefix [0, I0) is settled
+// in parallel, and only i >= I0 walk the kept list, one at a time, leaving
+// jst[i] (the dropping kept index, -1 if kept) and the kept list's original
+// positions in kidx.  Then p2: kept chain j gets the first later i whose
+// scan reached it (i kept, or kpos(j) <= jst[i]) with a significant overlap
+// -- the reference's first write.  Those are found 64 i at a time against
+// the list U of kept chains still without one: each lane holds a kept chain
+// and tests the block's 64 chains, broadcast by readlane, so the loop's
+// round trips are per block, not per chain.  Last, a[0 .. m) is compacted
+// from kidx (a[k] <- a[kidx[k]], kidx[k] >= k, chunk by chunk).  Same kept
+// list and p2 as flt_drop_serial.
+__device__ __forceinline__ bool flt_can_drop(const FltRec& ai, const FltRec& aj, float drop_ratio, int msl) {
+    return (float)ai.w < (float)aj.w * drop_ratio && aj.w - ai.w >= msl << 1;
+}
+
+__device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_t* U, int n, float mask_level,
+                                float drop_ratio, int msl, int lane) {
+    // I0: the first i >= 1 that a[0] can drop
+    const FltRec a0 = a[0];
+    int I0 = n;
+    for (int base = 1; base < n; base += 64) {
+        const int i = base + lane;
+        const uint64_t bc = __ballot(i < n && flt_can_drop(a[i], a0, drop_ratio, msl));
+        if (bc) {
+            I0 = base + (int)__builtin_ctzll(bc);
+            break;
+        }
+    }
+    I0 = __builtin_amdgcn_readfirstlane(I0);
+    for (int k = lane; k < I0; k += 64) kidx[k] = (uint32_t)k;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    int m = I0;
+    for (int i = I0; i < n; ++i) {
+        const FltRec ai = a[i];
+        int jstar = -1;
+        for (int base = 0; base < m; base += 64) {
+            const int j = base + lane;
+            bool can = false, hit = false;
+            if (j < m) {
+                const FltRec aj = a[kidx[j]];
+                can = flt_can_drop(ai, aj, drop_ratio, msl);
+                hit = can && flt_sig(ai, aj, mask_level);
+            }
+            const uint64_t bh = __ballot(hit);
+            if (bh) {
+                jstar = base + (int)__builtin_ctzll(bh);
+                break;
+            }
+            if (__ballot(can) != __ballot(j < m)) break;  // the prefix ends in this chunk
+        }
+        jstar = __builtin_amdgcn_readfirstlane(jstar);
+        if (lane == 0) {
+            jst[i] = jstar;
+            if (jstar < 0) kidx[m] = (uint32_t)i;
+        }
+        if (jstar < 0) ++m;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    // p2, 64 chains i at a time
+    int nu = 0, m_run = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        int32_t bi = 0, ei = 0, ji = 0;
+        bool kept = false;
+        if (i < n) {
+            const FltRec r = a[i];
+            bi = r.beg;
+            ei = r.end;
+            ji = i < I0 ? -1 : jst[i];
+            kept = ji < 0;
+        }
+        // the block's kept chains join U (they can be marked by later i of the block)
+        const uint64_t bk = __ballot(kept);
+        const uint32_t below = (uint32_t)__builtin_popcountll(bk & ((1ull << lane) - 1));
+        if (kept) U[nu + below] = (uint32_t)(m_run + below);
+        nu += __builtin_popcountll(bk);
+        m_run += __builtin_popcountll(bk);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const int nb = n - b < 64 ? n - b : 64;
+        int out = 0;
+        for (int c = 0; c < nu; c += 64) {
+            const int u = c + lane;
+            const bool act = u < nu;
+            uint32_t kp = 0, oj = 0;
+            FltRec rj{0, 0, 0, 0, -1};
+            if (act) {
+                kp = U[u];
+                oj = kidx[kp];
+                rj = a[oj];
+            }
+            int hit = -1;
+            for (int t = 0; t < nb; ++t) {
+                const int32_t bt = __builtin_amdgcn_readlane(bi, t), et = __builtin_amdgcn_readlane(ei, t);
+                const int32_t jt = __builtin_amdgcn_readlane(ji, t);
+                if (act && hit < 0 && (uint32_t)(b + t) > oj && (jt < 0 || (int32_t)kp <= jt) &&
+                    flt_sig(FltRec{bt, et, 0, 0, 0}, rj, mask_level))
+                    hit = b + t;
+            }
+            if (hit >= 0) a[oj].p2 = hit;
+            const bool keep = act && hit < 0;
+            const uint64_t bq = __ballot(keep);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            if (keep) U[out + __builtin_popcountll(bq & ((1ull << lane) - 1))] = kp;
+            out += __builtin_popcountll(bq);
+        }
+        nu = out;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    // compact the kept records (with their p2) to a[0 .. m)
+    for (int base = 0; base < m; base += 64) {
+        const int k = base + lane;
+        FltRec r{};
+        if (k < m) r = a[kidx[k]];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        if (k < m) a[k] = r;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    return m;
+}
+
 // weights + sort + reorder of mem_chain_flt (software/bwamem.c:636-651) by
 // one lane; ord holds the tree order, ord2 receives the sorted order
 __device__ __forceinline__ void flt_prepare_serial(const ChainParams& P, uint64_t S, FltRec* a, const uint32_t* ord,
@@ -848,8 +980,13 @@ __device__ __forceinline__ bool insert_read_wave(const ChainParams& P, uint64_t 
 // pos; a cluster that creates an equal pos (kbtree's answer then depends on
 // the node layout) sends the read back to the tree path.  With distinct keys
 // the in-order traversal is pos order: clusters in order, pos order inside.
-// One lane runs one cluster (64 per round), its sorted chain list (pos << 20
-// | local id) kept in the LDS slots of the cluster's already-read seeds.
+// One lane runs one cluster (64 per round).  Its chains are marks on the
+// ranks of their first seeds in rbeg order (a bitmap + summary in LDS after
+// the keys): the lower chain of a seed is the highest mark below the seed's
+// own rank -- among equal rbeg, ranks follow seed order, so that is the
+// chain with the largest pos <= rb, the latest one on a tie -- found in one
+// or two LDS reads, and a new chain is one mark, where a sorted chain list
+// took a binary search and a shift per seed (quadratic in giant clusters).
 // ---------------------------------------------------------------------------
 constexpr int CL_OBITS = 20;  // seed index bits in the sort keys
 constexpr uint64_t CL_OMASK = (1ull << CL_OBITS) - 1;
@@ -906,6 +1043,45 @@ __device__ __forceinline__ void chain_append(ChainRec& c, uint32_t o, int64_t rb
     c.last_qbeg = qb;
     c.last_len = ln;
     c.n += 1;
+}
+
+// The chains of a cluster as marks on the ranks of their first seeds (the
+// read's seeds sorted by rbeg): bm holds one bit per rank, sm one bit per
+// non-empty bm word.  Lanes mark disjoint rank ranges whose end words may be
+// shared, hence the LDS atomics.
+__device__ __forceinline__ uint32_t cluster_bm_words(uint32_t npad) { return (npad + 31) / 32; }
+__device__ __host__ __forceinline__ uint64_t cluster_lds_need(uint64_t npad) {
+    const uint64_t nbw = (npad + 31) / 32;
+    return npad * 8 + 4 * (nbw + (nbw + 31) / 32);
+}
+
+__device__ __forceinline__ void mark_set(uint32_t* bm, uint32_t* sm, uint32_t q) {
+    atomicOr(bm + (q >> 5), 1u << (q & 31));
+    atomicOr(sm + (q >> 10), 1u << ((q >> 5) & 31));
+}
+
+// the highest marked rank in [cs, r), -1 if none
+__device__ __forceinline__ int mark_pred(const uint32_t* bm, const uint32_t* sm, uint32_t cs, uint32_t r) {
+    if (r <= cs) return -1;
+    const uint32_t wlo = cs >> 5;
+    uint32_t w = (r - 1) >> 5;
+    uint32_t bits = bm[w] & (0xffffffffu >> (31 - ((r - 1) & 31)));
+    for (;;) {
+        if (w == wlo) bits &= ~0u << (cs & 31);
+        if (bits) return (int)(w * 32 + 31 - __builtin_clz(bits));
+        if (w == wlo) return -1;
+        --w;  // the next lower non-empty word, from the summary
+        uint32_t sw = w >> 5;
+        uint32_t sb = sm[sw] & (0xffffffffu >> (31 - (w & 31)));
+        while (!sb) {
+            if ((sw << 5) <= wlo) return -1;
+            --sw;
+            sb = sm[sw];
+        }
+        w = sw * 32 + 31 - __builtin_clz(sb);
+        if (w < wlo) return -1;
+        bits = bm[w];
+    }
 }
 
 // true: chains built, tree order in ord[0, n_out); false: a cluster made an
@@ -967,7 +1143,7 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
         const uint32_t cid = n_cl + (uint32_t)__builtin_popcountll(hm & ((2ull << lane) - 1)) - 1;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
-        if (valid) key[p] = ((uint64_t)cid << CL_OBITS) | (k & CL_OMASK);
+        if (valid) key[p] = ((uint64_t)cid << (2 * CL_OBITS)) | ((k & CL_OMASK) << CL_OBITS) | p;
         if (head) cstart[cid] = p;
         n_cl += (uint32_t)__builtin_popcountll(hm);
         n_valid += (uint32_t)__builtin_popcountll(__ballot(valid));
@@ -975,6 +1151,22 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
     wave_bitonic(key, npad, lane);  // cluster order kept, seed order inside
+    // key[p] = o << 20 | rank (seed order inside each cluster), and bits 40+
+    // of key[rank] = the seed at that rank; the marks cleared
+    const uint32_t nbw = cluster_bm_words(npad), nsw = (nbw + 31) / 32;
+    uint32_t* bm = reinterpret_cast<uint32_t*>(key + npad);
+    uint32_t* sm = bm + nbw;
+    for (uint32_t p = lane; p < n_valid; p += 64) key[p] &= (1ull << (2 * CL_OBITS)) - 1;
+    for (uint32_t w = lane; w < nbw + nsw; w += 64) bm[w] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t p = lane; p < n_valid; p += 64) {
+        const uint64_t e = key[p];
+        atomicOr(reinterpret_cast<unsigned long long*>(key + (e & CL_OMASK)),
+                 (unsigned long long)((e >> CL_OBITS) & CL_OMASK) << (2 * CL_OBITS));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     bool dup = false;
     uint32_t n_tot = 0, n_mine = 0;
     for (uint32_t r0 = 0; r0 < n_cl; r0 += 64) {
@@ -986,58 +1178,115 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
         }
         uint32_t n_ch = 0;
         bool cdup = false;
+        // seed p + 1's record and its lower chain's record are loaded while
+        // seed p is decided (against the marks before p); p's own mark or
+        // append then corrects them from registers
+        uint64_t e_n = 0;
+        SeedRec sd_n{0, 0, 0};
+        int L_n = -1;
+        ChainRec c_n{};
+        if (cs < ce) {
+            e_n = key[cs];
+            sd_n = seed[(uint32_t)(e_n >> CL_OBITS) & (uint32_t)CL_OMASK];
+        }
         for (uint32_t p = cs; p < ce; ++p) {
-            const uint32_t o = (uint32_t)(key[p] & CL_OMASK);
+            const uint64_t e = e_n;
+            const uint32_t o = (uint32_t)(e >> CL_OBITS) & (uint32_t)CL_OMASK, rk = (uint32_t)e & (uint32_t)CL_OMASK;
+            const SeedRec sd = sd_n;
+            const int Lp = L_n;
+            ChainRec cp = c_n;
+            uint32_t rk_n = 0;
+            if (!cdup && p + 1 < ce) {
+                e_n = key[p + 1];
+                const uint32_t o_n = (uint32_t)(e_n >> CL_OBITS) & (uint32_t)CL_OMASK;
+                rk_n = (uint32_t)e_n & (uint32_t)CL_OMASK;
+                sd_n = seed[o_n];
+                L_n = mark_pred(bm, sm, cs, rk_n);
+                if (L_n >= 0) c_n = chn[(uint32_t)(key[L_n] >> (2 * CL_OBITS))];
+            } else if (p + 1 < ce) {
+                e_n = key[p + 1];
+            }
             if (cdup) {  // past an equal chain key: the tree replay decides
                 code[o] = CODE_REPLAY;
                 ++n_mine;
                 continue;
             }
-            const SeedRec sd = seed[o];
             const int64_t rb = sd.rbeg;
-            // lower chain: the last list entry with pos <= rb
-            int lo = 0, hi = (int)n_ch;  // first entry with pos > rb
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if ((int64_t)(key[cs + mid] >> CL_OBITS) <= rb) lo = mid + 1;
-                else hi = mid;
-            }
-            const int L = lo - 1;
+            // lower chain: the highest mark below the seed's rank (the first
+            // seed of the cluster has none)
+            const int L = p == cs ? -1 : Lp;
             bool make = true;
+            uint32_t id = 0;
+            ChainRec c = cp;
             if (L >= 0) {
-                const uint32_t id = (uint32_t)(key[cs + L] & CL_OMASK);
-                ChainRec c = chn[id];
+                id = (uint32_t)(key[L] >> (2 * CL_OBITS));
                 const int mg = merge_test(P, c, rb, sd.qbeg, sd.len);
                 if (mg == MERGE_APPEND) {
                     P.next[S + c.last] = o;
                     chain_append(c, o, rb, sd.qbeg, sd.len);
                     chn[id] = c;
+                    if (L_n == L) c_n = c;  // the prefetched record is this chain's
                 }
                 make = mg == MERGE_NEW;
                 if (make && c.pos == rb) cdup = true;
             }
             code[o] = make ? CODE_NEW : CODE_SKIP;
             if (make) {
-                chn[o] = ChainRec{rb, rb, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
+                const ChainRec nc{rb, rb, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
+                chn[o] = nc;
                 ++n_mine;
                 if (!cdup) {
-                    // insert after L; the slots up to cs + n_ch are already read
-                    for (int q = (int)n_ch; q > L + 1; --q) key[cs + q] = key[cs + q - 1];
-                    key[cs + L + 1] = ((uint64_t)rb << CL_OBITS) | o;
+                    mark_set(bm, sm, rk);
                     ++n_ch;
+                    // the new mark is seed p + 1's lower chain when it lies between
+                    if (p + 1 < ce && rk < rk_n && (L_n < 0 || (uint32_t)L_n < rk)) {
+                        L_n = (int)rk;
+                        c_n = nc;
+                    }
                 }
             }
         }
         dup = dup || cdup;
         uint32_t tot;
         const uint32_t base = wave_excl_scan(n_ch, lane, tot);
-        for (uint32_t j = 0; j < n_ch; ++j) ord[n_tot + base + j] = (uint32_t)(key[cs + j] & CL_OMASK);
+        // the cluster's chains in pos order: its marks in rank order
+        uint32_t q = n_tot + base;
+        if (n_ch) {
+            const uint32_t w0 = cs >> 5, w1 = (ce - 1) >> 5;
+            for (uint32_t w = w0; w <= w1; ++w) {
+                uint32_t bits = bm[w];
+                if (w == w0) bits &= ~0u << (cs & 31);
+                if (w == w1) bits &= 0xffffffffu >> (31 - ((ce - 1) & 31));
+                while (bits) {
+                    const uint32_t b = (uint32_t)__builtin_ctz(bits);
+                    bits &= bits - 1;
+                    ord[q++] = (uint32_t)(key[w * 32 + b] >> (2 * CL_OBITS));
+                }
+            }
+        }
         n_tot += tot;
     }
     n_out = (int)n_tot;
     for (int off = 32; off > 0; off >>= 1) n_mine += __shfl_xor(n_mine, off);
     n_cand = n_mine;
     return __ballot(dup) == 0;
+}
+
+// kb_intervalp's `lower` by a whole wave (as tree_lower): one LDS round per
+// node; every value the descent branches on is wave-uniform
+template <class N>
+__device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int64_t k, int lane) {
+    uint32_t x = root;
+    int lower = -1;
+    for (;;) {
+        const N* nd = pool + x;
+        bool eq;
+        const int i = __builtin_amdgcn_readfirstlane(node_find_wave(nd, k, lane, eq));
+        if (i >= 0) lower = __builtin_amdgcn_readfirstlane((int)nd->id[i]);
+        if (i >= 0 && eq) return lower;
+        if (__builtin_amdgcn_readfirstlane((int)nd->leaf)) return lower;
+        x = (uint32_t)__builtin_amdgcn_readfirstlane((int)nd->child[i + 1]);
+    }
 }
 
 // The kbtree pass of a read whose clusters made an equal chain key: which of
@@ -1047,8 +1296,11 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
 // Chains of clean clusters, and the seeds of a dup cluster up to its first
 // equal key, are as the cluster pass decided them (exact: no equal keys
 // there yet); the later seeds of a dup cluster (CODE_REPLAY) are decided
-// here against the tree, as mem_insert_seed does.  Lane 0 walks the tree;
-// the wave loads codes and seeds 64 at a time.
+// here against the tree, as mem_insert_seed does.  The seeds go one at a
+// time in seed order, each tree search and kb_putp by the whole wave (one
+// LDS round per node, shifts and splits in parallel: the serial lane-0 walk
+// spent most of its time in the leaf shifts); lane 0 alone reads and writes
+// the chain records.  The wave loads codes and seeds 64 at a time.
 template <class N>
 __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane) {
     const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
@@ -1056,6 +1308,8 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
     ChainRec* chn = P.chn + S;
     uint32_t root = 0, n_nodes = 1, n_ch = 0;
     if (lane == 0) node_init(pool, 1);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     for (uint32_t base = 0; base < ns; base += 64) {
         const uint32_t o = base + (uint32_t)lane;
         const uint32_t cd = o < ns ? code[o] : CODE_SKIP;
@@ -1069,26 +1323,28 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
             const int64_t rb = rl64(sd.rbeg, t);
             const int32_t qb = rl32(sd.qbeg, t), ln = rl32(sd.len, t);
             const uint32_t ot = base + (uint32_t)t;
-            if (lane == 0) {
-                bool make = true;
-                if (ct == CODE_REPLAY && n_ch) {
-                    const int lw = tree_lower(pool, root, rb);
-                    if (lw >= 0) {
-                        ChainRec c = chn[lw];
-                        const int mg = merge_test(P, c, rb, qb, ln);
-                        if (mg == MERGE_APPEND) {
-                            P.next[S + c.last] = ot;
-                            chain_append(c, ot, rb, qb, ln);
-                            chn[lw] = c;
-                        }
-                        make = mg == MERGE_NEW;
+            int lw = -1;
+            if (ct == CODE_REPLAY && n_ch) lw = tree_lower_wave(pool, root, rb, lane);
+            int make = 1;
+            if (lw >= 0) {
+                if (lane == 0) {
+                    ChainRec c = chn[lw];
+                    const int mg = merge_test(P, c, rb, qb, ln);
+                    if (mg == MERGE_APPEND) {
+                        P.next[S + c.last] = ot;
+                        chain_append(c, ot, rb, qb, ln);
+                        chn[lw] = c;
                     }
+                    make = mg == MERGE_NEW;
                 }
-                if (make) {
-                    if (ct == CODE_REPLAY) chn[ot] = ChainRec{rb, rb, qb, qb, ln, 1, ot, ot};
-                    tree_insert(pool, root, n_nodes, ot, rb);
-                    ++n_ch;
-                }
+                make = __builtin_amdgcn_readfirstlane(make);
+            }
+            if (make) {
+                if (lane == 0 && ct == CODE_REPLAY) chn[ot] = ChainRec{rb, rb, qb, qb, ln, 1, ot, ot};
+                tree_insert_wave(pool, root, n_nodes, ot, rb, lane);
+                root = (uint32_t)__builtin_amdgcn_readfirstlane((int)root);
+                n_nodes = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_nodes);
+                ++n_ch;
             }
         }
     }
@@ -1362,12 +1618,13 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
     __shared__ uint32_t s_stk[3 * 64];
     const int lane = threadIdx.x;
     const uint32_t n_giant = P.heavy_ctr[0], n_all = n_giant + P.heavy_ctr[1];
+    const uint32_t it_lo = P.tier == 1 ? n_giant : 0, it_hi = P.tier == 0 ? n_giant : n_all;
     for (;;) {
-        if (lane == 0) s_item = atomicAdd(P.heavy_ctr + 2, 1u);
+        if (lane == 0) s_item = it_lo + atomicAdd(P.heavy_ctr + 2 + (P.tier == 1 ? 1 : 0), 1u);
         __syncthreads();
         const uint32_t item = s_item;
         __syncthreads();
-        if (item >= n_all) break;
+        if (item >= it_hi) break;
         const uint32_t r = item < n_giant ? P.heavy[item] : P.heavy[(uint64_t)P.n_reads + (item - n_giant)];
         const uint64_t i0 = P.intv_off[r], i1 = P.intv_off[r + 1];
         const uint64_t S = P.occ_off[i0];
@@ -1396,7 +1653,7 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             const uint64_t E = P.occ_off[i1];
             uint32_t npad = 2;
             while (npad < E - S) npad <<= 1;
-            if (E - S < (1ull << CL_OBITS) && (uint64_t)npad * 8 <= P.lds_bytes) {
+            if (E - S < (1ull << CL_OBITS) && cluster_lds_need(npad) <= P.lds_bytes) {
                 int n = 0;
                 uint32_t n_cand = 0;
                 const bool clean =
@@ -1524,7 +1781,25 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             }
             __syncthreads();
             int m;
-            if (P.drop_ratio > 0.f) {
+            if (P.drop_ratio > 0.f && P.drop_blocked) {
+                // kidx / jst / U: LDS after the records while all fit, else
+                // kidx in the read's ord rows (free until the marks below),
+                // jst and U in its kbtree node pool (free after the sort)
+                const bool x_lds = in_lds && (uint64_t)n * (sizeof(FltRec) + 12) <= (uint64_t)P.lds_bytes;
+                uint32_t* kidx;
+                int32_t* jst;
+                uint32_t* U;
+                if (x_lds) {
+                    kidx = reinterpret_cast<uint32_t*>(la + n);
+                } else {
+                    kidx = ord;
+                }
+                uint32_t* xs = x_lds ? kidx + n : reinterpret_cast<uint32_t*>(P.node + (S / 7 + 3ull * (uint64_t)r));
+                jst = reinterpret_cast<int32_t*>(xs);
+                U = xs + n;
+                m = in_lds ? flt_drop_blocked(la, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane)
+                           : flt_drop_blocked(ga, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane);
+            } else if (P.drop_ratio > 0.f) {
                 // U: LDS after the records while both fit, else the read's ord
                 // rows (free until the marks below)
                 const bool u_lds = in_lds && (uint64_t)n * (sizeof(FltRec) + 4) <= (uint64_t)P.lds_bytes;
@@ -1624,7 +1899,14 @@ __global__ __launch_bounds__(64) void chain_write_heavy_kernel(ChainParams P) {
 
 }  // namespace smem
 
-extern "C" hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_cu, hipStream_t st) {
+// The heavy reads in two tiers: the giants (> giant_min seeds) with the big
+// LDS allotment, one wave per CU, and the rest with lds_rest (several waves
+// per CU; their trees, clusters and filter records fit it) on st2 beside
+// them, picking up the CUs as giant waves retire.  One launch of both with
+// the big allotment left 3 of 4 SIMDs idle while the bulk of the heavy reads
+// went through it.
+extern "C" hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_cu, hipStream_t st, hipStream_t st2,
+                                              hipEvent_t ev_fork, hipEvent_t ev_join) {
     if (P->n_reads <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(P->heavy_ctr, 0, 4 * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
@@ -1634,8 +1916,26 @@ extern "C" hipError_t smem_launch_chain_build(const smem::ChainParams* P, int n_
     // more than the default 64 KB of dynamic LDS per workgroup (gfx950 has 160 KB per CU)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(smem::chain_heavy_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)P->lds_bytes);
-    hipLaunchKernelGGL(smem::chain_heavy_kernel, dim3(n_cu), dim3(64), P->lds_bytes, st, *P);
-    return hipGetLastError();
+    if (!st2) {
+        smem::ChainParams Q = *P;
+        Q.tier = -1;
+        hipLaunchKernelGGL(smem::chain_heavy_kernel, dim3(n_cu), dim3(64), Q.lds_bytes, st, Q);
+        return hipGetLastError();
+    }
+    if ((e = hipEventRecord(ev_fork, st)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st2, ev_fork, 0)) != hipSuccess) return e;
+    smem::ChainParams G = *P, R = *P;
+    G.tier = 0;
+    R.tier = 1;
+    R.lds_bytes = P->lds_rest < P->lds_bytes ? P->lds_rest : P->lds_bytes;
+    hipLaunchKernelGGL(smem::chain_heavy_kernel, dim3(n_cu), dim3(64), G.lds_bytes, st, G);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t per_cu = 160u * 1024u / (R.lds_bytes + 4096u);
+    hipLaunchKernelGGL(smem::chain_heavy_kernel, dim3(n_cu * (per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu))), dim3(64),
+                       R.lds_bytes, st2, R);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev_join, st2)) != hipSuccess) return e;
+    return hipStreamWaitEvent(st, ev_join, 0);
 }
 
 extern "C" hipError_t smem_launch_chain_write(const smem::ChainParams* P, int n_cu, hipStream_t st) {

@@ -102,7 +102,8 @@ constexpr uint32_t SA_DENSE_SHIFT = 2;
 // chaining: reads with more seed occurrences than this get a wave each
 // (chain_heavy_kernel), giants first; its chain tree / filter records live
 // in CHAIN_HEAVY_LDS bytes of LDS (one such workgroup per CU)
-constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 1024, CHAIN_HEAVY_LDS = 150 * 1024;
+constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 1024, CHAIN_HEAVY_LDS = 150 * 1024,
+                   CHAIN_REST_LDS = 36 * 1024;
 
 struct smem_gpu {
     int device = 0;
@@ -150,8 +151,9 @@ struct smem_batch {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // chains -> regions: the light reads' kernel runs on st2 beside the heavy
     // reads' kernels on st, joined by ev_join (created on first use)
+    // (chaining: the heavy reads' second tier on st2, forked by ev_fork)
     hipStream_t st2 = nullptr;
-    hipEvent_t ev_join = nullptr;
+    hipEvent_t ev_join = nullptr, ev_fork = nullptr;
     int max_reads = 0, max_len = 0;
     uint64_t max_bases = 0;
     uint32_t cap_intv = 0, cap_calls = 0, cap_list = 0;
@@ -389,6 +391,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
+    if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
     if (b->st2) (void)hipStreamDestroy(b->st2);
     if (b->st) (void)hipStreamDestroy(b->st);
     delete b;
@@ -923,14 +926,27 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.cluster = getenv("SMEM_CHAIN_TREE_ONLY") ? 0 : 1;
     P.wave_sort = getenv("SMEM_CHAIN_SERIAL_SORT") ? 0 : 1;
     P.sort_lane_max = 256;
+    P.drop_blocked = getenv("SMEM_CHAIN_DROP_PRUNED") ? 0 : 1;
     if (const char* v = getenv("SMEM_CHAIN_SORT_LANE_MAX")) P.sort_lane_max = (uint32_t)std::max(17, atoi(v));
     if (getenv("SMEM_CHAIN_DBG")) {
         HIP_TRY(b->d_dbg.ensure(256 * 16));
         HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 256 * 16 * sizeof(uint64_t), b->st));
         P.dbg = b->d_dbg.p;
     }
+    // the heavy reads' second tier beside the giants (SMEM_CHAIN_STREAMS=1:
+    // one launch of both on the batch's stream; SMEM_CHAIN_LDS_REST: its LDS)
+    P.lds_rest = CHAIN_REST_LDS;
+    if (const char* v = getenv("SMEM_CHAIN_LDS_REST")) P.lds_rest = (uint32_t)std::max(1024, atoi(v));
+    const bool two = !(getenv("SMEM_CHAIN_STREAMS") && atoi(getenv("SMEM_CHAIN_STREAMS")) == 1);
+    if (two && !b->st2) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&b->st2, hipStreamNonBlocking, least));
+    }
+    if (two && !b->ev_fork) HIP_TRY(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    if (two && !b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
-    HIP_TRY(smem_launch_chain_build(&P, b->g->n_cu, b->st));
+    HIP_TRY(smem_launch_chain_build(&P, b->g->n_cu, b->st, two ? b->st2 : nullptr, b->ev_fork, b->ev_join));
     tmp = b->d_sa_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_n_out.p, b->d_chain_off.p, n, b->d_sa_tmp.p, &tmp, b->st));
     tmp = b->d_sa_tmp.n;

@@ -153,14 +153,20 @@ def test_chain_strand_bridging_and_empty(gpu_device):
                                  dict(SMEM_CHAIN_TREE_ONLY="1", SMEM_CHAIN_HEAVY_MIN="0"),
                                  dict(SMEM_CHAIN_SERIAL_SORT="1"),
                                  dict(SMEM_CHAIN_SORT_LANE_MAX="17", SMEM_CHAIN_HEAVY_MIN="0"),
-                                 dict(SMEM_CHAIN_SORT_LANE_MAX="17", SMEM_CHAIN_LDS="4096")],
+                                 dict(SMEM_CHAIN_SORT_LANE_MAX="17", SMEM_CHAIN_LDS="4096"),
+                                 dict(SMEM_CHAIN_DROP_PRUNED="1", SMEM_CHAIN_HEAVY_MIN="0"),
+                                 dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_LDS="3072"),
+                                 dict(SMEM_CHAIN_STREAMS="1", SMEM_CHAIN_HEAVY_MIN="0"),
+                                 dict(SMEM_CHAIN_LDS_REST="2048", SMEM_CHAIN_HEAVY_MIN="0")],
                          ids=["all-wave", "all-lane", "lds-overflow", "tree-only", "tree-only-all-wave",
-                              "serial-sort", "wave-cut-sort", "wave-cut-sort-hbm"])
+                              "serial-sort", "wave-cut-sort", "wave-cut-sort-hbm", "drop-pruned", "drop-hbm",
+                              "one-launch", "rest-tier-hbm"])
 def test_chain_paths_agree(gpu_device, monkeypatch, env):
     """The lane-per-read path, the wave-per-read paths (position clusters,
-    and the chain tree they fall back to on equal chain keys) and the wave
-    path's HBM fallbacks (chain tree / filter records beyond its LDS) give
-    the restatement's chains."""
+    and the chain tree they fall back to on equal chain keys), the wave
+    path's HBM fallbacks (chain tree / filter records / drop-loop scratch
+    beyond its LDS) and both drop loops (blocked, pruned) give the
+    restatement's chains."""
     import smemgpu
     from smemgpu import synth
     for k, v in env.items():
