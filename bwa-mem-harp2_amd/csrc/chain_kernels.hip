@@ -14,6 +14,14 @@
 namespace smem {
 namespace {
 
+// Every wave-cooperative routine below runs in a one-wave workgroup
+// (chain_heavy_kernel), where lanes hand data to each other through LDS or
+// HBM: a wavefront-scope fence orders those accesses for the compiler and
+// costs no wait (a wave's memory operations are performed in order), where a
+// workgroup-scope fence waited for every outstanding store -- the chain
+// records' HBM stores -- at each tree insertion.
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
 // The chain tree in two node formats with one code path: BNode (u32 ids and
 // children, HBM pools) and LNode (u16, the LDS pool of the heavy path).
 
@@ -424,7 +432,7 @@ __device__ __forceinline__ int flt_drop_pruned(FltRec* a, uint32_t* U, int n, fl
                                                int msl, int lane) {
     int m = 1, nu = 1;
     if (lane == 0) U[0] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     for (int i = 1; i < n; ++i) {
         const FltRec ai = a[i];
@@ -461,7 +469,7 @@ __device__ __forceinline__ int flt_drop_pruned(FltRec* a, uint32_t* U, int n, fl
                 }
             }
             const uint64_t bk = __ballot(keep);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            wave_fence();
             __builtin_amdgcn_wave_barrier();
             if (keep) U[out + __builtin_popcountll(bk & ((1ull << lane) - 1))] = j;
             out += __builtin_popcountll(bk);
@@ -475,7 +483,7 @@ __device__ __forceinline__ int flt_drop_pruned(FltRec* a, uint32_t* U, int n, fl
             ++m;
             ++nu;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
     }
     return m;
@@ -516,7 +524,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
     }
     I0 = __builtin_amdgcn_readfirstlane(I0);
     for (int k = lane; k < I0; k += 64) kidx[k] = (uint32_t)k;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     int m = I0;
     for (int i = I0; i < n; ++i) {
@@ -544,7 +552,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
         }
         if (jstar < 0) ++m;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     // p2, 64 chains i at a time
     int nu = 0, m_run = 0;
@@ -565,7 +573,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
         if (kept) U[nu + below] = (uint32_t)(m_run + below);
         nu += __builtin_popcountll(bk);
         m_run += __builtin_popcountll(bk);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
         const int nb = n - b < 64 ? n - b : 64;
         int out = 0;
@@ -590,13 +598,13 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
             if (hit >= 0) a[oj].p2 = hit;
             const bool keep = act && hit < 0;
             const uint64_t bq = __ballot(keep);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            wave_fence();
             __builtin_amdgcn_wave_barrier();
             if (keep) U[out + __builtin_popcountll(bq & ((1ull << lane) - 1))] = kp;
             out += __builtin_popcountll(bq);
         }
         nu = out;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
     }
     // compact the kept records (with their p2) to a[0 .. m)
@@ -604,10 +612,10 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
         const int k = base + lane;
         FltRec r{};
         if (k < m) r = a[kidx[k]];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
         if (k < m) a[k] = r;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
     }
     return m;
@@ -713,10 +721,32 @@ __device__ __forceinline__ void node_split_wave(N* pool, uint32_t xi, int i, uin
         x->id[i] = mid;
         x->n = n + 1;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // other lanes read these next (HBM pool too)
+    wave_fence();  // other lanes read these next (HBM pool too)
     __builtin_amdgcn_wave_barrier();
 }
 
+// one node into the wave, one LDS round: lane l holds key / id slot l and
+// child slot l; n and leaf wave-uniform
+template <class N>
+__device__ __forceinline__ void node_load_wave(const N* nd, int lane, int& n, int& leaf, int64_t& kv, uint32_t& idv,
+                                               uint32_t& chv) {
+    const int n0 = nd->n, l0 = nd->leaf;
+    kv = lane < BT_MAX ? nd->key[lane] : INT64_MAX;
+    idv = lane < BT_MAX ? (uint32_t)nd->id[lane] : 0u;
+    chv = lane <= BT_MAX ? (uint32_t)nd->child[lane] : 0u;
+    n = __builtin_amdgcn_readfirstlane(n0);
+    leaf = __builtin_amdgcn_readfirstlane(l0);
+}
+
+// __kb_getp_aux on a loaded node: the slot index (eq: the leftmost equal key)
+__device__ __forceinline__ int node_find_regs(int n, int64_t kv, int64_t k, int lane, bool& eq) {
+    const int below = __builtin_popcountll(__ballot(lane < n && kv < k));
+    eq = __ballot(lane == below && lane < n && kv == k) != 0;
+    return eq ? below : below - 1;
+}
+
+// kb_putp by the wave: a node per LDS round on the way down (plus its
+// child's fill, for the pre-emptive split), the leaf's shift from registers
 template <class N>
 __device__ __forceinline__ void tree_insert_wave(N* pool, uint32_t& root, uint32_t& n_nodes, uint32_t id, int64_t k,
                                                  int lane) {
@@ -728,42 +758,41 @@ __device__ __forceinline__ void tree_insert_wave(N* pool, uint32_t& root, uint32
             node_init(pool + s, 0);
             pool[s].child[0] = x;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
         node_split_wave(pool, s, 0, x, n_nodes, lane);
         root = x = s;
     }
-    while (!pool[x].leaf) {
-        int i = node_find_wave(pool + x, k, lane, eq) + 1;
-        const uint32_t c = pool[x].child[i];
-        if (pool[c].n == BT_MAX) {
+    for (;;) {
+        int n, leaf;
+        int64_t kv;
+        uint32_t idv, chv;
+        node_load_wave(pool + x, lane, n, leaf, kv, idv, chv);
+        if (leaf) {
+            N* nd = pool + x;
+            const int i = node_find_regs(n, kv, k, lane, eq);
+            if (lane >= i + 1 && lane < n) {
+                nd->key[lane + 1] = kv;
+                nd->id[lane + 1] = idv;
+            }
+            if (lane == 0) {
+                nd->key[i + 1] = k;
+                nd->id[i + 1] = id;
+                nd->n = n + 1;
+            }
+            wave_fence();
+            __builtin_amdgcn_wave_barrier();
+            return;
+        }
+        int i = node_find_regs(n, kv, k, lane, eq) + 1;
+        uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)chv, i);
+        if (__builtin_amdgcn_readfirstlane((int)pool[c].n) == BT_MAX) {
             node_split_wave(pool, x, i, c, n_nodes, lane);
             if (k > pool[x].key[i]) ++i;
+            c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[x].child[i]);
         }
-        x = pool[x].child[i];
+        x = c;
     }
-    N* nd = pool + x;
-    const int i = node_find_wave(nd, k, lane, eq);
-    const int n = nd->n;
-    int64_t kv = 0;
-    uint32_t iv = 0;
-    const bool mv = lane >= i + 1 && lane < n;
-    if (mv) {
-        kv = nd->key[lane];
-        iv = nd->id[lane];
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (mv) {
-        nd->key[lane + 1] = kv;
-        nd->id[lane + 1] = iv;
-    }
-    if (lane == 0) {
-        nd->key[i + 1] = k;
-        nd->id[i + 1] = id;
-        nd->n = n + 1;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
 }
 
 // Wave form of the same loop for one read, exact by construction: a window
@@ -1004,7 +1033,7 @@ __device__ __forceinline__ void wave_bitonic(uint64_t* key, uint32_t npad, int l
                     key[l] = a;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            wave_fence();
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -1119,7 +1148,7 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
         const int32_t t = __shfl_xor(lmax, off);
         lmax = t > lmax ? t : lmax;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     wave_bitonic(key, npad, lane);
     const int64_t G = (int64_t)(P.max_chain_gap > 1 ? P.max_chain_gap : 1) + lmax;
@@ -1141,14 +1170,14 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
         const bool head = valid && (p == 0 || (int64_t)(k >> CL_OBITS) - (int64_t)(kp >> CL_OBITS) >= G);
         const uint64_t hm = __ballot(head);
         const uint32_t cid = n_cl + (uint32_t)__builtin_popcountll(hm & ((2ull << lane) - 1)) - 1;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         __builtin_amdgcn_wave_barrier();
         if (valid) key[p] = ((uint64_t)cid << (2 * CL_OBITS)) | ((k & CL_OMASK) << CL_OBITS) | p;
         if (head) cstart[cid] = p;
         n_cl += (uint32_t)__builtin_popcountll(hm);
         n_valid += (uint32_t)__builtin_popcountll(__ballot(valid));
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     wave_bitonic(key, npad, lane);  // cluster order kept, seed order inside
     // key[p] = o << 20 | rank (seed order inside each cluster), and bits 40+
@@ -1158,14 +1187,14 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
     uint32_t* sm = bm + nbw;
     for (uint32_t p = lane; p < n_valid; p += 64) key[p] &= (1ull << (2 * CL_OBITS)) - 1;
     for (uint32_t w = lane; w < nbw + nsw; w += 64) bm[w] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     for (uint32_t p = lane; p < n_valid; p += 64) {
         const uint64_t e = key[p];
         atomicOr(reinterpret_cast<unsigned long long*>(key + (e & CL_OMASK)),
                  (unsigned long long)((e >> CL_OBITS) & CL_OMASK) << (2 * CL_OBITS));
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     bool dup = false;
     uint32_t n_tot = 0, n_mine = 0;
@@ -1279,13 +1308,16 @@ __device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int
     uint32_t x = root;
     int lower = -1;
     for (;;) {
-        const N* nd = pool + x;
+        int n, leaf;
+        int64_t kv;
+        uint32_t idv, chv;
+        node_load_wave(pool + x, lane, n, leaf, kv, idv, chv);
         bool eq;
-        const int i = __builtin_amdgcn_readfirstlane(node_find_wave(nd, k, lane, eq));
-        if (i >= 0) lower = __builtin_amdgcn_readfirstlane((int)nd->id[i]);
+        const int i = node_find_regs(n, kv, k, lane, eq);
+        if (i >= 0) lower = __builtin_amdgcn_readlane((int)idv, i);
         if (i >= 0 && eq) return lower;
-        if (__builtin_amdgcn_readfirstlane((int)nd->leaf)) return lower;
-        x = (uint32_t)__builtin_amdgcn_readfirstlane((int)nd->child[i + 1]);
+        if (leaf) return lower;
+        x = (uint32_t)__builtin_amdgcn_readlane((int)chv, i + 1);
     }
 }
 
@@ -1298,9 +1330,12 @@ __device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int
 // there yet); the later seeds of a dup cluster (CODE_REPLAY) are decided
 // here against the tree, as mem_insert_seed does.  The seeds go one at a
 // time in seed order, each tree search and kb_putp by the whole wave (one
-// LDS round per node, shifts and splits in parallel: the serial lane-0 walk
-// spent most of its time in the leaf shifts); lane 0 alone reads and writes
-// the chain records.  The wave loads codes and seeds 64 at a time.
+// LDS round per node, shifts and splits in parallel: 35 -> 20 M cycles on
+// the bench's worst read against lane 0 walking the tree alone); lane 0
+// alone reads and writes the chain records.  The wave loads codes and seeds
+// 64 at a time.  (Prefetching the chain records a window of 64 seeds at a
+// time was measured too: no change, so the walk is bound by the single
+// wave's instruction latency, not by the record loads.)
 template <class N>
 __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane) {
     const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
@@ -1308,7 +1343,7 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
     ChainRec* chn = P.chn + S;
     uint32_t root = 0, n_nodes = 1, n_ch = 0;
     if (lane == 0) node_init(pool, 1);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
     for (uint32_t base = 0; base < ns; base += 64) {
         const uint32_t o = base + (uint32_t)lane;
@@ -1427,7 +1462,7 @@ __device__ void flt_sort_seg_serial(FltRec* a, size_t s, size_t t, int d) {
 }
 
 __device__ __forceinline__ void wave_sync_mem() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
     __builtin_amdgcn_wave_barrier();
 }
 

@@ -102,7 +102,7 @@ constexpr uint32_t SA_DENSE_SHIFT = 2;
 // chaining: reads with more seed occurrences than this get a wave each
 // (chain_heavy_kernel), giants first; its chain tree / filter records live
 // in CHAIN_HEAVY_LDS bytes of LDS (one such workgroup per CU)
-constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 1024, CHAIN_HEAVY_LDS = 150 * 1024,
+constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 2048, CHAIN_HEAVY_LDS = 150 * 1024,
                    CHAIN_REST_LDS = 36 * 1024;
 
 struct smem_gpu {
@@ -923,6 +923,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     // HBM fallbacks), SMEM_CHAIN_HEAVY_MIN moves the lane/wave split
     if (const char* v = getenv("SMEM_CHAIN_LDS")) P.lds_bytes = (uint32_t)std::max(1024, atoi(v));
     if (const char* v = getenv("SMEM_CHAIN_HEAVY_MIN")) P.heavy_min = (uint32_t)std::max(0, atoi(v));
+    if (const char* v = getenv("SMEM_CHAIN_GIANT_MIN")) P.giant_min = (uint32_t)std::max(0, atoi(v));
     P.cluster = getenv("SMEM_CHAIN_TREE_ONLY") ? 0 : 1;
     P.wave_sort = getenv("SMEM_CHAIN_SERIAL_SORT") ? 0 : 1;
     P.sort_lane_max = 256;

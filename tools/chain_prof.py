@@ -20,6 +20,7 @@ def main():
     --genome-profile human)"""
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--sweep", default="", help="giant_min:lds_rest_kb,... timed with the filter")
     own, rest = p.parse_known_args()
     import torch
     torch.cuda.device_count()  # as bench.py's Dist does, before libsmemgpu touches the device
@@ -42,6 +43,20 @@ def main():
             b.chain(idx.seq_len // 2, filter=filt)
             ms.append(b.stats()["chain_ms"])
         out[f"filter{int(filt)}_ms"] = ms
+    for item in [x for x in own.sweep.split(",") if x]:
+        gm, lr = item.split(":")
+        os.environ["SMEM_CHAIN_GIANT_MIN"] = gm
+        os.environ["SMEM_CHAIN_LDS_REST"] = str(int(lr) * 1024)
+        ms = []
+        for _ in range(a.reps):
+            b.chain(idx.seq_len // 2, filter=True)
+            ms.append(b.stats()["chain_ms"])
+        out[f"sweep_{gm}_{lr}k_ms"] = ms
+        print(item, ms, file=sys.stderr, flush=True)
+    os.environ.pop("SMEM_CHAIN_GIANT_MIN", None)
+    os.environ.pop("SMEM_CHAIN_LDS_REST", None)
+    if own.sweep:
+        b.chain(idx.seq_len // 2, filter=True)
     if os.environ.get("SMEM_CHAIN_DBG"):
         d = b.debug_words(256 * 16).reshape(256, 16).astype(np.int64)
         d = d[np.argsort(-(d[:, 9] - d[:, 2]))]
