@@ -526,31 +526,52 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
     for (int k = lane; k < I0; k += 64) kidx[k] = (uint32_t)k;
     wave_fence();
     __builtin_amdgcn_wave_barrier();
+    // the kept list's first 64 records live in registers (lane j: kept j),
+    // the chains i in registers a block of 64 at a time: a chain whose
+    // droppers' prefix ends inside the first 64 is decided without a load
     int m = I0;
-    for (int i = I0; i < n; ++i) {
-        const FltRec ai = a[i];
-        int jstar = -1;
-        for (int base = 0; base < m; base += 64) {
-            const int j = base + lane;
-            bool can = false, hit = false;
-            if (j < m) {
-                const FltRec aj = a[kidx[j]];
-                can = flt_can_drop(ai, aj, drop_ratio, msl);
-                hit = can && flt_sig(ai, aj, mask_level);
+    FltRec kr{0, 0, 0, 0, -1};
+    if (lane < I0) kr = a[lane];
+    for (int blk = I0; blk < n; blk += 64) {
+        FltRec rb{0, 0, 0, 0, -1};
+        if (blk + lane < n) rb = a[blk + lane];
+        const int nb = n - blk < 64 ? n - blk : 64;
+        for (int t = 0; t < nb; ++t) {
+            const int i = blk + t;
+            const FltRec ai{__builtin_amdgcn_readlane(rb.beg, t), __builtin_amdgcn_readlane(rb.end, t),
+                            __builtin_amdgcn_readlane(rb.w, t), i, -1};
+            const int mr = m < 64 ? m : 64;
+            const bool can_r = lane < mr && flt_can_drop(ai, kr, drop_ratio, msl);
+            const uint64_t bh_r = __ballot(can_r && flt_sig(ai, kr, mask_level));
+            int jstar = bh_r ? (int)__builtin_ctzll(bh_r) : -1;
+            if (!bh_r && m > 64 && __ballot(can_r) == __ballot(lane < mr)) {
+                // the prefix goes on past the registers
+                for (int base = 64; base < m; base += 64) {
+                    const int j = base + lane;
+                    bool can = false, hit = false;
+                    if (j < m) {
+                        const FltRec aj = a[kidx[j]];
+                        can = flt_can_drop(ai, aj, drop_ratio, msl);
+                        hit = can && flt_sig(ai, aj, mask_level);
+                    }
+                    const uint64_t bh = __ballot(hit);
+                    if (bh) {
+                        jstar = base + (int)__builtin_ctzll(bh);
+                        break;
+                    }
+                    if (__ballot(can) != __ballot(j < m)) break;  // the prefix ends in this chunk
+                }
             }
-            const uint64_t bh = __ballot(hit);
-            if (bh) {
-                jstar = base + (int)__builtin_ctzll(bh);
-                break;
+            jstar = __builtin_amdgcn_readfirstlane(jstar);
+            if (lane == 0) {
+                jst[i] = jstar;
+                if (jstar < 0) kidx[m] = (uint32_t)i;
             }
-            if (__ballot(can) != __ballot(j < m)) break;  // the prefix ends in this chunk
+            if (jstar < 0) {
+                if (lane == m) kr = ai;
+                ++m;
+            }
         }
-        jstar = __builtin_amdgcn_readfirstlane(jstar);
-        if (lane == 0) {
-            jst[i] = jstar;
-            if (jstar < 0) kidx[m] = (uint32_t)i;
-        }
-        if (jstar < 0) ++m;
     }
     wave_fence();
     __builtin_amdgcn_wave_barrier();
