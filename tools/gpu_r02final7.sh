@@ -1,7 +1,7 @@
 # round-2 measurements after the chaining changes: every GPU test, traffic
 # for this build, bench c2 (uniform and human-like), the rocprof summary, smoke
 set -o pipefail
-O=gpurun_out/final7
+O=gpurun_out/${FINAL_OUT:-final7}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
