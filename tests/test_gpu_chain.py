@@ -235,3 +235,40 @@ def test_chain_equal_keys_replay(gpu_device, monkeypatch, env):
         b.close()
     finally:
         gpu.close()
+
+
+@pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_STREAMS="1"), dict(SMEM_CHAIN_GIANT_MIN="256")],
+                         ids=["tiers", "one-launch", "more-giants"])
+def test_chain_human_like_giants(gpu_device, monkeypatch, env):
+    """A 4 Mbp genome with the human-like repeat profile and 8 % satellite /
+    simple-sequence arrays: reads from the arrays carry thousands of seed
+    occurrences (the giant LDS tier, > 2048), thousands of chains per read
+    (rank-bitmap clusters, the kbtree replay, the two-pass drop loop with its
+    kept list past the 64 register slots).  Chains == the restatement's, with
+    and without the filter, in both heavy-read launch layouts."""
+    import smemgpu
+    from smemgpu import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.make_genome_human_like(4_000_000, seed=5, n_chrom=2, satellite_frac=0.08)
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    reads = synth.make_reads(g.codes, 4000, 150, seed=6, sub_rate=0.01)
+    gpu = smemgpu.Gpu(idx, device=gpu_device)
+    try:
+        gpu.load_sa(sa)
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        b.sa(19, 10000)
+        l_pac = idx.seq_len // 2
+        for filt in (0, 1):
+            b.chain(l_pac, filter=bool(filt))
+            res = b.fetch()
+            n_occ = np.array([res.read_sa(i).size for i in range(reads.n)])
+            n_chain = np.diff(res.chain_off)
+            assert n_occ.max() > 2048 and (n_occ > 256).sum() >= 16
+            assert n_chain.max() > (1000 if not filt else 64)
+            assert res.to_smch() == _oracle_chains(res, reads.n, l_pac, 19, 10000, filter=filt)
+        b.close()
+    finally:
+        gpu.close()
