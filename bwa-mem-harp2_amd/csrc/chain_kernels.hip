@@ -1840,7 +1840,9 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             if (P.drop_ratio > 0.f && P.drop_blocked) {
                 // kidx / jst / U: LDS after the records while all fit, else
                 // kidx in the read's ord rows (free until the marks below),
-                // jst and U in its kbtree node pool (free after the sort)
+                // jst and U in its kbtree node pool (free after the sort; the
+                // pool holds >= (E - S) / 7 + 2 nodes of 256 B, > 8 n bytes
+                // as n <= E - S)
                 const bool x_lds = in_lds && (uint64_t)n * (sizeof(FltRec) + 12) <= (uint64_t)P.lds_bytes;
                 uint32_t* kidx;
                 int32_t* jst;
