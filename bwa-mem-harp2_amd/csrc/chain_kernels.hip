@@ -151,6 +151,25 @@ __device__ __forceinline__ int tree_inorder(const N* pool, uint32_t root, uint32
     return n_out;
 }
 
+// the same traversal for a tree of at most two levels (fewer than 127 keys:
+// a third level needs 2 t^2 - 1 = 127), without the stack the general walk
+// keeps in scratch
+template <class N>
+__device__ __forceinline__ int tree_inorder2(const N* pool, uint32_t root, uint32_t* out) {
+    const N* r = pool + root;
+    int n_out = 0;
+    if (r->leaf) {
+        for (int j = 0; j < r->n; ++j) out[n_out++] = r->id[j];
+        return n_out;
+    }
+    for (int i = 0; i <= r->n; ++i) {
+        const N* c = pool + r->child[i];
+        for (int j = 0; j < c->n; ++j) out[n_out++] = c->id[j];
+        if (i < r->n) out[n_out++] = r->id[i];
+    }
+    return n_out;
+}
+
 // mem_chain_weight (software/bwamem.c:501-521), the second loop's `end`
 // advanced by query coordinates as the reference writes it
 __device__ __forceinline__ int chain_weight(const ChainRec& c, const SeedRec* seed, const uint32_t* next) {
@@ -1324,22 +1343,105 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
 
 // kb_intervalp's `lower` by a whole wave (as tree_lower): one LDS round per
 // node; every value the descent branches on is wave-uniform
+// What a search leaves for a kb_putp of the same key: the leaf it reached
+// and that leaf's slots, valid (ok) when no node on the path was full (so
+// kb_putp would split nothing and descend the same way) and the search did
+// not stop at an equal key above the leaf.
+struct LeafHand {
+    bool ok;
+    uint32_t x;
+    int n;
+    int64_t kv;
+    uint32_t idv;
+};
+
 template <class N>
-__device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int64_t k, int lane) {
+__device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int64_t k, int lane,
+                                               LeafHand* hand = nullptr) {
     uint32_t x = root;
     int lower = -1;
+    bool full = false;
+    if (hand) hand->ok = false;
     for (;;) {
         int n, leaf;
         int64_t kv;
         uint32_t idv, chv;
         node_load_wave(pool + x, lane, n, leaf, kv, idv, chv);
+        full = full || n == BT_MAX;
         bool eq;
         const int i = node_find_regs(n, kv, k, lane, eq);
         if (i >= 0) lower = __builtin_amdgcn_readlane((int)idv, i);
-        if (i >= 0 && eq) return lower;
-        if (leaf) return lower;
+        if (i >= 0 && eq && !leaf) return lower;
+        if (leaf) {
+            if (hand) *hand = LeafHand{!full, x, n, kv, idv};
+            return lower;
+        }
         x = (uint32_t)__builtin_amdgcn_readlane((int)chv, i + 1);
     }
+}
+
+// kb_putp of key k into the leaf a search handed over (LeafHand::ok): the
+// leaf's shift and the new slot from registers, no descent
+template <class N>
+__device__ __forceinline__ void leaf_insert_hand(N* pool, const LeafHand& h, uint32_t id, int64_t k, int lane) {
+    N* nd = pool + h.x;
+    bool eq;
+    const int i = node_find_regs(h.n, h.kv, k, lane, eq);
+    if (lane >= i + 1 && lane < h.n) {
+        nd->key[lane + 1] = h.kv;
+        nd->id[lane + 1] = h.idv;
+    }
+    if (lane == 0) {
+        nd->key[i + 1] = k;
+        nd->id[i + 1] = id;
+        nd->n = h.n + 1;
+    }
+    wave_fence();
+    __builtin_amdgcn_wave_barrier();
+}
+
+// __kb_traverse (as tree_inorder) by the wave, for the heavy path: the
+// stack of (node, next child) lives in the lanes (lane d: depth d, read by
+// readlane, written by a lane select), a node is one LDS round, and a leaf's
+// ids go out in one store.  tree_inorder keeps its stack in scratch: a
+// lane-serial walk of a several-thousand-chain tree waited on a scratch
+// round trip per step, most of the kbtree replay's time.
+template <class N>
+__device__ int tree_inorder_wave(const N* pool, uint32_t root, uint32_t* out, int lane) {
+    int sxv = lane == 0 ? (int)root : 0, siv = 0;
+    int top = 0, n_out = 0;
+    while (top >= 0) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane(sxv, top);
+        const int i = __builtin_amdgcn_readlane(siv, top);
+        int n, leaf;
+        int64_t kv;
+        uint32_t idv, chv;
+        node_load_wave(pool + x, lane, n, leaf, kv, idv, chv);
+        (void)kv;
+        if (leaf) {
+            if (lane < n) out[n_out + lane] = idv;
+            n_out += n;
+            --top;
+            continue;
+        }
+        // back from child i - 1: its key; then child i, or up
+        if (i > 0 && i - 1 < n) {
+            if (lane == 0) out[n_out] = (uint32_t)__builtin_amdgcn_readlane((int)idv, i - 1);
+            ++n_out;
+        }
+        if (i <= n) {
+            if (lane == top) siv = i + 1;
+            ++top;
+            const int c = __builtin_amdgcn_readlane((int)chv, i);
+            if (lane == top) {
+                sxv = c;
+                siv = 0;
+            }
+        } else {
+            --top;
+        }
+    }
+    return n_out;
 }
 
 // The kbtree pass of a read whose clusters made an equal chain key: which of
@@ -1380,7 +1482,8 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
             const int32_t qb = rl32(sd.qbeg, t), ln = rl32(sd.len, t);
             const uint32_t ot = base + (uint32_t)t;
             int lw = -1;
-            if (ct == CODE_REPLAY && n_ch) lw = tree_lower_wave(pool, root, rb, lane);
+            LeafHand hand{false, 0, 0, 0, 0};
+            if (ct == CODE_REPLAY && n_ch) lw = tree_lower_wave(pool, root, rb, lane, &hand);
             int make = 1;
             if (lw >= 0) {
                 if (lane == 0) {
@@ -1397,16 +1500,18 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
             }
             if (make) {
                 if (lane == 0 && ct == CODE_REPLAY) chn[ot] = ChainRec{rb, rb, qb, qb, ln, 1, ot, ot};
-                tree_insert_wave(pool, root, n_nodes, ot, rb, lane);
-                root = (uint32_t)__builtin_amdgcn_readfirstlane((int)root);
-                n_nodes = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_nodes);
+                if (hand.ok) {  // no split on the search's path: insert into its leaf
+                    leaf_insert_hand(pool, hand, ot, rb, lane);
+                } else {
+                    tree_insert_wave(pool, root, n_nodes, ot, rb, lane);
+                    root = (uint32_t)__builtin_amdgcn_readfirstlane((int)root);
+                    n_nodes = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_nodes);
+                }
                 ++n_ch;
             }
         }
     }
-    int n = 0;
-    if (lane == 0 && n_ch) n = tree_inorder(pool, root, P.ord + S);
-    return __shfl(n, 0, 64);
+    return n_ch ? tree_inorder_wave(pool, root, P.ord + S, lane) : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1648,7 +1753,7 @@ __global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
     insert_read(P, i1, S, pool, 0xffffffffu, st);
     uint32_t* ord = P.ord + S;
     uint32_t* ord2 = P.ord2 + S;
-    const int n = st.n_ch ? tree_inorder(pool, st.root, ord) : 0;
+    const int n = !st.n_ch ? 0 : (st.n_ch < 127 ? tree_inorder2(pool, st.root, ord) : tree_inorder(pool, st.root, ord));
     int n_keep = n;
     if (!P.filter || n <= 1) {
         for (int i = 0; i < n; ++i) ord2[i] = ord[i];
@@ -1766,10 +1871,10 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 __syncthreads();
                 insert_read_wave(P, S, E, gpool, 0xffffffffu, o, n_ch, root, n_nodes, lane, s_dups, n_dup, dbg);
             }
+            int n_io = 0;
+            if (n_ch) n_io = in_lds ? tree_inorder_wave(lpool, root, ord, lane) : tree_inorder_wave(gpool, root, ord, lane);
             if (lane == 0) {
-                int n;
-                if (in_lds) n = n_ch ? tree_inorder(lpool, root, ord) : 0;
-                else n = n_ch ? tree_inorder(gpool, root, ord) : 0;
+                const int n = n_io;
                 s_n = n;
                 if (dbg) {
                     dbg[3] = __builtin_readcyclecounter();

@@ -103,7 +103,7 @@ constexpr uint32_t SA_DENSE_SHIFT = 2;
 // (chain_heavy_kernel), giants first; its chain tree / filter records live
 // in CHAIN_HEAVY_LDS bytes of LDS (one such workgroup per CU)
 constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 2048, CHAIN_HEAVY_LDS = 150 * 1024,
-                   CHAIN_REST_LDS = 36 * 1024;
+                   CHAIN_REST_LDS = 28 * 1024;
 
 struct smem_gpu {
     int device = 0;
