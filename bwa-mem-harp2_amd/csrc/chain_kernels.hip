@@ -1456,9 +1456,12 @@ __device__ int tree_inorder_wave(const N* pool, uint32_t root, uint32_t* out, in
 // LDS round per node, shifts and splits in parallel: 35 -> 20 M cycles on
 // the bench's worst read against lane 0 walking the tree alone); lane 0
 // alone reads and writes the chain records.  The wave loads codes and seeds
-// 64 at a time.  (Prefetching the chain records a window of 64 seeds at a
-// time was measured too: no change, so the walk is bound by the single
-// wave's instruction latency, not by the record loads.)
+// 64 at a time.  A search whose path holds no full node hands its leaf to
+// the insert (no second descent).  Measured without effect on the walk's
+// time: that hand-off, one LDS round per node instead of three, wavefront-
+// instead of workgroup-scope fences, and the chain records prefetched a
+// window of 64 seeds at a time; the in-order listing's scratch stack was
+// what it waited on (tree_inorder_wave).
 template <class N>
 __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane) {
     const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
