@@ -114,6 +114,11 @@ def parse(argv=None):
     p.add_argument("--parity", type=int, default=1,
                    help="1: seed the stats sample on the GPU too and compare (0: every seed_kernel launch is a "
                         "full resident batch, for rocprofv3 summaries)")
+    p.add_argument("--e2e-reads", type=int, default=200_000,
+                   help="reads of the end-to-end leg (bwa-gpu mem vs the reference pipeline; 0: skip; N=1 only)")
+    p.add_argument("--e2e-batch", type=int, default=0, help="-b of bwa-gpu mem (0: reads / threads)")
+    p.add_argument("--human-like", type=int, default=1,
+                   help="1: also measure the seeding step on the human-like genome profile (N=1 only)")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch TCC_EA0_RDREQ / FETCH_SIZE recorded by tools/traffic.py for this build + workload")
@@ -537,6 +542,107 @@ def sw_cpu(kb) -> dict:
             "sample": f"{kb.tasks.size} problems, {secs:.2f} s incl. file I/O"}
 
 
+BWA_GPU = os.path.join(ROOT, "oracle", "_ref", "bwa-gpu")       # the reference's `bwa`, integration/ patch
+REF_HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")  # the unpatched reference pipeline
+
+
+def _mem_times(stderr: str) -> tuple:
+    """(reads, summed real seconds) of the reference's per-chunk
+    "[M::mem_process_seqs] Processed N reads in C CPU sec, R real sec" lines
+    (software/bwamem.c:1637-1638)."""
+    import re
+    n, real = 0, 0.0
+    for m in re.finditer(r"\[M::mem_process_seqs\] Processed (\d+) reads in ([\d.]+) CPU sec, ([\d.]+) real sec",
+                         stderr):
+        n += int(m.group(1))
+        real += float(m.group(3))
+    return n, real
+
+
+def _sam_body(path: str):
+    """sha256 and line count of a SAM file without its @PG line."""
+    import hashlib
+    h = hashlib.sha256()
+    n = 0
+    with open(path, "rb") as fh:
+        for line in fh:
+            if line.startswith(b"@PG"):
+                continue
+            h.update(line)
+            n += 1
+    return h.hexdigest(), n
+
+
+def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> dict | None:
+    """The product path end to end (north_star: the `bwa mem` CLI unchanged):
+    the reference's own `bwa mem` built with the integration/ patch against
+    libsmemgpu.so (oracle/_ref/bwa-gpu: every kt_for_batch worker batch's
+    seeding -> bwt_sa -> mem_chain + mem_chain_flt -> mem_chain2aln on the
+    GPU, sort / pairing / SAM on the CPU) beside the unpatched reference
+    pipeline on the same reads, index and threads (oracle/_ref/ref_harness
+    mem: main_mem's body over mem_process_seqs with -b 1, every batch on the
+    CPU path -- the only way the reference runs without its FPGA).  The index
+    prefix is the bench's own .bwt / .sa plus .pac / .ann / .amb in `bwa
+    index` format (synth.write_bwa_bns; byte-identical to bwa index,
+    tests/test_bwa_integration.py).  Timed: each process's wall clock
+    (index load + upload included) and the reference's own per-chunk
+    mem_process_seqs real time.  SAM identity is checked on every read."""
+    import subprocess
+    from smemgpu import synth
+    if not (os.path.exists(BWA_GPU) and os.path.exists(REF_HARNESS)) or args.e2e_reads <= 0:
+        return None
+    if not all(os.path.exists(base + e) for e in (".pac", ".ann", ".amb")):
+        t = time.time()
+        synth.write_bwa_bns(base + ".tmp", genome_codes)
+        for e in (".pac", ".ann", ".amb"):
+            os.replace(base + ".tmp" + e, base + e)
+        log(f"bwa .pac/.ann/.amb written in {time.time() - t:.1f} s")
+    m = min(args.e2e_reads, reads.n)
+    sub = reads.subset(np.arange(m))
+    batch = args.e2e_batch or max(1024, -(-m // threads))
+    out = {"reads": m, "read_len": args.read_len, "threads": threads, "batch": batch,
+           "what": "bwa-gpu mem (the reference's bwa mem with integration/patches, libsmemgpu.so: seeding -> "
+                   "bwt_sa -> mem_chain + mem_chain_flt -> mem_chain2aln on the GPU, the regions copied back, "
+                   "mem_sort_and_dedup / mem_mark_primary_se / mem_reg2sam_se on the CPU) vs the unpatched "
+                   "reference pipeline (ref_harness mem = main_mem over mem_process_seqs, -b 1) on the same reads, "
+                   "index, threads; seconds include loading the index"}
+    with tempfile.TemporaryDirectory(dir=args.cache) as d:
+        fq = os.path.join(d, "r.fq")
+        synth.write_fastq(fq, sub)
+        runs = {}
+        env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu))
+        legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq], {}),
+                ("gpu_chains_only", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq],
+                 {"SMEM_GPU_STAGES": "1"}),
+                ("reference", [REF_HARNESS, "mem", base, fq, str(threads), "1", "0"], {})]
+        for name, cmd, env in legs:
+            sam = os.path.join(d, name + ".sam")
+            t = time.perf_counter()
+            with open(sam, "wb") as fh:
+                p = subprocess.run(cmd, stdout=fh, stderr=subprocess.PIPE, env=dict(env_base, **env), timeout=900)
+            wall = time.perf_counter() - t
+            err = p.stderr.decode(errors="replace")
+            if p.returncode != 0:
+                log(f"e2e {name} failed ({p.returncode}): {err[-800:]}")
+                return dict(out, error=f"{name} exit {p.returncode}")
+            n_proc, real = _mem_times(err)
+            digest, n_lines = _sam_body(sam)
+            runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
+                          "reads_per_s_wall": round(m / wall, 1),
+                          "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
+                          "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
+                          "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
+            log(f"e2e {name}: {wall:.1f} s wall, mem_process_seqs {real:.1f} s")
+        out.update(runs)
+        out["sam_identical"] = runs["gpu"]["sam_sha256"] == runs["reference"]["sam_sha256"] == \
+            runs["gpu_chains_only"]["sam_sha256"]
+        g, r = runs["gpu"], runs["reference"]
+        out["speedup_wall"] = round(r["wall_s"] / g["wall_s"], 2)
+        if g["mem_process_seqs_real_s"] > 0:
+            out["speedup_mem_process_seqs"] = round(r["mem_process_seqs_real_s"] / g["mem_process_seqs_real_s"], 2)
+    return out
+
+
 def span_union(spans) -> float:
     """Total time covered by the [start, end) intervals (chip-clock ticks)."""
     tot, cur = 0, None
@@ -600,19 +706,12 @@ def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id,
     return out
 
 
-def main():
-    args = parse()
+def time_seeding(args, d, gpu, reads, opt) -> dict:
+    """The timed region of a seeding step (see the module docstring): W warmup
+    steps (the alone launches give kernel_ms_alone), then K steps between
+    barriers, --streams host workers each running whole steps on its own
+    batch and stream.  Returns the step's numbers; the batches are closed."""
     import torch
-    import smemgpu
-
-    d = Dist()
-    rank, world = d.rank, d.world
-    barrier = d.barrier
-
-    idx, idx_path, sa, genome_codes = get_index(args, rank, barrier, d.gpu)
-    reads = make_reads(args, rank, genome_codes, world)
-    gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu, variant=args.variant, kmer_k=args.kmer_k)
-    gpu.load_sa(sa)
     # one batch object (own HIP stream, own buffers) per host worker, each
     # holding the whole read set: a step is one full pass over the reads
     batches = []
@@ -622,8 +721,6 @@ def main():
         batches.append(b)
     batch = batches[0]
     torch.cuda.synchronize()
-
-    opt = smemgpu.Options(min_seed_len=args.min_seed_len)
     # warmup; launches that run alone on the GPU (no other stream's kernels
     # beside them) give kernel_ms_alone
     alone_ms, alone_span = [], []
@@ -640,7 +737,7 @@ def main():
     kernel_ms, spans = [], []
     for b in batches[1:]:
         b.run(opt)
-    barrier()
+    d.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if len(batches) == 1:
@@ -675,13 +772,77 @@ def main():
         if errs:
             raise errs[0]
     torch.cuda.synchronize()
-    barrier()
+    d.barrier()
     elapsed = time.perf_counter() - t0
     st = batch.stats()
     value, elapsed_max = aggregate(d, elapsed, reads.n, args.steps)
     for b in batches[1:]:
         b.close()
-    batches = [batch]
+    a_ms = float(np.mean(alone_ms))
+    return {"batch": batch, "value": value, "elapsed_max": elapsed_max, "st": st,
+            "k_ms": float(np.mean(kernel_ms)), "a_ms": a_ms,
+            "busy_ms": span_union(spans) / RT_TICKS_PER_MS / max(len(spans), 1),
+            "clock_check": float(np.mean(alone_span)) / a_ms if a_ms > 0 else None,
+            "compact_alone": compact_alone}
+
+
+def human_like_report(args, d, cores) -> dict:
+    """The same step on the human-like repeat profile (--genome-profile human:
+    ~46 % interspersed repeats + satellites, closer to human_g1k_v37 than the
+    uniform profile of the headline), same read seeds and sizes: value, busy
+    time, roofline fraction, request fraction (when tools/traffic.py recorded
+    this build on this workload), extends per read, parity sample and the
+    reference's CPU rate on a sample of these reads.  Its own index (cached
+    like the headline's)."""
+    import copy
+    import smemgpu
+    h = copy.copy(args)
+    h.genome_profile = "human"
+    h.traffic_json = os.path.join(os.path.dirname(args.traffic_json), "traffic_human.json")
+    t = time.time()
+    idx, idx_path, sa, genome_codes = get_index(h, d.rank, d.barrier, d.gpu)
+    t_index = time.time() - t
+    reads = make_reads(h, d.rank, genome_codes, d.world)
+    gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu, variant=args.variant, kmer_k=args.kmer_k)
+    opt = smemgpu.Options(min_seed_len=args.min_seed_len)
+    T = time_seeding(h, d, gpu, reads, opt)
+    h.cpu_seconds = min(args.cpu_seconds, 10.0)
+    bpr, bpr64, ostats, n_counted, parity, cpu, _ = cpu_leg(h, gpu, opt, idx, idx_path, reads, cores)
+    T["batch"].close()
+    gpu.close()
+    rf = roofline(h, bpr, bpr64, ostats, n_counted, reads.n, T["k_ms"], T["a_ms"], smemgpu.build_id(), T["busy_ms"],
+                  T["clock_check"])
+    out = {"value": round(T["value"], 1), "unit": "reads/s", "ms_per_step": round(T["elapsed_max"] / args.steps * 1e3, 3),
+           "steps": args.steps, "genome_profile": "human", "reads": reads.n, "read_len": args.read_len,
+           "kernel_busy_ms": rf["kernel_busy_ms"], "kernel_ms_alone": rf["kernel_ms_alone"],
+           "frac": rf["frac"], "frac_alone": rf["frac_alone"], "achieved_GBps": rf["achieved"],
+           "bytes_per_read": rf["bytes_per_read"], "extends_per_read": rf["extends_per_read"],
+           "request_frac": (rf.get("request_roofline") or {}).get("frac"),
+           "request_roofline": rf.get("request_roofline"),
+           "parity_sample": parity, "cpu_baseline": cpu,
+           "index_s": round(t_index, 1),
+           "what": "the headline step on the human-like genome profile (~46 % interspersed repeats shaped like "
+                   "RepeatMasker's classes + 3 % satellites), same sizes and read seeds"}
+    del idx, sa, genome_codes
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    import smemgpu
+
+    d = Dist()
+    rank, world = d.rank, d.world
+    barrier = d.barrier
+
+    idx, idx_path, sa, genome_codes = get_index(args, rank, barrier, d.gpu)
+    reads = make_reads(args, rank, genome_codes, world)
+    gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu, variant=args.variant, kmer_k=args.kmer_k)
+    gpu.load_sa(sa)
+    opt = smemgpu.Options(min_seed_len=args.min_seed_len)
+    T = time_seeding(args, d, gpu, reads, opt)
+    batch, st, value, elapsed_max = T["batch"], T["st"], T["value"], T["elapsed_max"]
 
     # streaming (PCIe-inclusive) on every rank, then its aggregate; the
     # config's target read count, or the resident reads (c2)
@@ -704,6 +865,7 @@ def main():
         aln_rep = aln_report(gpu, batch, opt, idx.seq_len // 2)
         sw_rep, sw_tasks = sw_report(gpu, np.asarray(genome_codes))
 
+    out = None
     if rank == 0:
         inv = cpu_inventory()
         cores = inv["use"]
@@ -713,10 +875,6 @@ def main():
             sw_rep["cpu_baseline"] = sw_cpu_rep
         if aln_rep is not None and args.cpu_seconds > 0:
             aln_rep["cpu_baseline"] = aln_cpu(args, idx_path, reads, genome_codes, opt)
-        k_ms = float(np.mean(kernel_ms))
-        a_ms = float(np.mean(alone_ms))
-        busy_ms = span_union(spans) / RT_TICKS_PER_MS / max(len(spans), 1)
-        clock_check = float(np.mean(alone_span)) / a_ms if a_ms > 0 else None
         cfg = CONFIGS[args.config]
         out = {
             "metric": METRIC,
@@ -750,11 +908,11 @@ def main():
                 "grid": st["grid"], "block": st["block"],
                 "kernel_variant": args.variant or 2, "kmer_k": args.kmer_k,
             },
-            "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, k_ms, a_ms, smemgpu.build_id(), busy_ms,
-                                 clock_check),
+            "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, T["k_ms"], T["a_ms"], smemgpu.build_id(),
+                                 T["busy_ms"], T["clock_check"]),
             "cpu_baseline": cpu,
             "parity_sample": parity,
-            "compact_ms": round(compact_alone, 3),
+            "compact_ms": round(T["compact_alone"], 3),
             "streaming": srep,
             "sa_lookup": sa_rep,
             "chaining": chain_rep,
@@ -764,10 +922,18 @@ def main():
             "build_id": smemgpu.build_id(),
             "build_id_matches_sources": smemgpu.build_id() == smemgpu.source_hash(),
         }
-        print(json.dumps(out), flush=True)
-    for b in batches:
-        b.close()
+    batch.close()
     gpu.close()
+    # the product path end to end and the human-like profile: one GPU (the
+    # driver's N=1 line), after the headline's GPU state is released
+    if rank == 0 and world == 1:
+        if args.e2e_reads > 0:
+            out["e2e"] = e2e_report(args, genome_key(args), genome_codes, reads, cores, d.gpu)
+        if args.human_like and args.genome_profile == "uniform":
+            del idx, sa
+            out["human_like"] = human_like_report(args, d, cores)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     d.close()
 
 

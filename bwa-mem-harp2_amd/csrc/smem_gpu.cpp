@@ -68,6 +68,13 @@ struct DevBuf {
         if (e == hipSuccess) n = std::max<size_t>(want, 1);
         return e;
     }
+    // ensure() with 25 % headroom when it must reallocate: for scratch whose
+    // size follows each batch's contents (a reallocation frees, and hipFree
+    // waits for the whole device)
+    hipError_t grow(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        return ensure(want + want / 4);
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -79,6 +86,13 @@ template <class T>
 struct HostBuf {
     T* p = nullptr;
     size_t n = 0;
+    // a pinned result buffer of at least `want` elements, grown with 25 %
+    // headroom: batches of a worker vary in size, and re-pinning on every
+    // slightly larger one costs more than the copy
+    hipError_t grow(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        return ensure(want + want / 4);
+    }
     hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
         if (p) (void)hipHostFree(p);
@@ -111,7 +125,7 @@ struct smem_gpu {
     int lanes_per_cu = 768;  // 3 blocks of 256 per CU: what the default kernel's LDS allows
     int intv_cap = 0;
     int variant = 2;  // see smem_gpu_set_kernel_variant
-    uint32_t* d_bwt = nullptr;      // reference layout (variants 3, 4)
+    uint32_t* d_bwt = nullptr;      // reference layout (A/B variants 3, 4; freed after the Occ64 re-layout otherwise)
     uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
     uint32_t* d_occ192 = nullptr;   // Occ192 layout (variant 10)
     uint4* d_kt = nullptr;          // k-mer bi-interval table (smem_gpu_set_kmer_table; variant 23)
@@ -124,6 +138,11 @@ struct smem_gpu {
     uint64_t bwt_size = 0, primary = 0, L2[5] = {0, 0, 0, 0, 0};
     std::mutex mu;
     std::unordered_map<std::thread::id, smem_batch_t*> per_thread;
+    // smem_gpu_collect_ex's batches by worker slot (the kt_for_batch tid):
+    // kt_for_batch starts new threads for every chunk, so batches keyed by
+    // thread would pile up; a slot's batch is reused by whichever thread holds
+    // the slot next
+    std::vector<smem_batch_t*> slots;
     // smem_gpu_seed_stream's worker batches, kept between calls: creating one
     // pins ~1 GB of host memory and allocates its device buffers
     std::vector<smem_batch_t*> stream_pool;
@@ -302,6 +321,12 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
         delete g;
         return fail(SMEM_E_DEVICE, "smem_gpu_init: Occ64 layout", e);
     }
+#ifndef SMEM_AB_VARIANTS
+    // only the A/B variants 3 / 4 read the reference layout: 3.1 GB of HBM
+    // back at human size once Occ64 is built
+    (void)hipFree(g->d_bwt);
+    g->d_bwt = nullptr;
+#endif
     *out = g;
     return SMEM_OK;
 }
@@ -313,7 +338,10 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 23))) return SMEM_E_ARG;
+    g_err[0] = 0;
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 23))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
+    if (!smem_seed_variant_built(variant))
+        return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: A/B variant not in this build (make AB=1)");
     if ((variant == 10 || variant == 22) && !g->d_occ192) {
         // the Occ192 layout (variant 10 only), built from Occ64 on first use
         std::lock_guard<std::mutex> lk(g->mu);
@@ -402,6 +430,8 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     (void)hipSetDevice(g->device);
     for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
     g->per_thread.clear();
+    for (auto* b : g->slots) smem_batch_destroy(b);
+    g->slots.clear();
     for (auto* b : g->stream_pool) smem_batch_destroy(b);
     g->stream_pool.clear();
     if (g->d_bwt) (void)hipFree(g->d_bwt);
@@ -684,14 +714,16 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     return SMEM_OK;
 }
 
-int smem_batch_fetch(smem_batch_t* b) {
-    g_err[0] = 0;
-    if (!b || !b->ran) return fail(SMEM_E_ARG, "smem_batch_fetch: batch has not run");
+// copy the outputs `mask` names (SMEM_FETCH_*) device -> pinned host memory
+static int fetch_impl(smem_batch_t* b, int mask) {
     HIP_TRY(hipSetDevice(b->g->device));
     const int n = b->n_reads;
+    const bool f_intv = mask & SMEM_FETCH_INTV, f_sa = (mask & SMEM_FETCH_SA) && b->sa_ran;
+    const bool f_chain = (mask & SMEM_FETCH_CHAINS) && b->chain_ran, f_aln = (mask & SMEM_FETCH_REGS) && b->aln_ran;
     // pinned result buffers grow with headroom: a streamed batch whose next
     // chunk holds a few more intervals must not re-pin a gigabyte
-    if (b->packed) {
+    if (!f_intv) {
+    } else if (b->packed) {
         if (b->d_pintv.n < b->tot_intv || !b->d_pintv.p)
             HIP_TRY(b->d_pintv.ensure(std::max<uint64_t>(b->tot_intv + b->tot_intv / 4, 1)));
         if (b->h_pintv.n < b->tot_intv || !b->h_pintv.p)
@@ -699,31 +731,34 @@ int smem_batch_fetch(smem_batch_t* b) {
     } else if (b->h_intv.n < b->tot_intv || !b->h_intv.p) {
         HIP_TRY(b->h_intv.ensure(std::max<uint64_t>(b->tot_intv + b->tot_intv / 4, 1)));
     }
-    if (b->h_calls.n < b->tot_calls || !b->h_calls.p)
+    if (f_intv && (b->h_calls.n < b->tot_calls || !b->h_calls.p))
         HIP_TRY(b->h_calls.ensure(std::max<uint64_t>(b->tot_calls + b->tot_calls / 4, 1)));
-    HIP_TRY(hipMemcpyAsync(b->h_intv_off.p, b->d_intv_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
-    HIP_TRY(hipMemcpyAsync(b->h_call_off.p, b->d_call_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
-    if (b->tot_intv && b->packed) {
+    if (f_intv) {
+        HIP_TRY(hipMemcpyAsync(b->h_intv_off.p, b->d_intv_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
+        HIP_TRY(hipMemcpyAsync(b->h_call_off.p, b->d_call_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, b->st));
+    }
+    if (!f_intv) {
+    } else if (b->tot_intv && b->packed) {
         HIP_TRY(smem_launch_pack_intv(b->d_flat_intv.p, b->tot_intv, b->d_pintv.p, b->st));
         HIP_TRY(hipMemcpyAsync(b->h_pintv.p, b->d_pintv.p, sizeof(uint4) * b->tot_intv, hipMemcpyDeviceToHost, b->st));
     } else if (b->tot_intv) {
         HIP_TRY(hipMemcpyAsync(b->h_intv.p, b->d_flat_intv.p, sizeof(Intv) * b->tot_intv, hipMemcpyDeviceToHost, b->st));
     }
-    if (b->tot_calls)
+    if (f_intv && b->tot_calls)
         HIP_TRY(hipMemcpyAsync(b->h_calls.p, b->d_flat_calls.p, sizeof(uint32_t) * b->tot_calls, hipMemcpyDeviceToHost, b->st));
-    if (b->sa_ran) {
-        HIP_TRY(b->h_occ_off.ensure(b->tot_intv + 1));
-        HIP_TRY(b->h_sa_pos.ensure(std::max<uint64_t>(b->tot_occ, 1)));
+    if (f_sa) {
+        HIP_TRY(b->h_occ_off.grow(b->tot_intv + 1));
+        HIP_TRY(b->h_sa_pos.grow(b->tot_occ));
         HIP_TRY(hipMemcpyAsync(b->h_occ_off.p, b->d_occ_off.p, sizeof(uint64_t) * (b->tot_intv + 1),
                                hipMemcpyDeviceToHost, b->st));
         if (b->tot_occ)
             HIP_TRY(hipMemcpyAsync(b->h_sa_pos.p, b->d_sa_pos.p, sizeof(uint64_t) * b->tot_occ, hipMemcpyDeviceToHost,
                                    b->st));
     }
-    if (b->chain_ran) {
-        HIP_TRY(b->h_chain_off.ensure(n + 1));
-        HIP_TRY(b->h_out_chain.ensure(std::max<uint64_t>(b->tot_chains, 1)));
-        HIP_TRY(b->h_out_seed.ensure(std::max<uint64_t>(b->tot_seeds, 1)));
+    if (f_chain) {
+        HIP_TRY(b->h_chain_off.grow((uint64_t)n + 1));
+        HIP_TRY(b->h_out_chain.grow(b->tot_chains));
+        HIP_TRY(b->h_out_seed.grow(b->tot_seeds));
         HIP_TRY(hipMemcpyAsync(b->h_chain_off.p, b->d_chain_off.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost,
                                b->st));
         if (b->tot_chains)
@@ -733,10 +768,9 @@ int smem_batch_fetch(smem_batch_t* b) {
             HIP_TRY(hipMemcpyAsync(b->h_out_seed.p, b->d_out_seed.p, sizeof(smem::SeedRec) * b->tot_seeds,
                                    hipMemcpyDeviceToHost, b->st));
     }
-    if (b->aln_ran) {
-        if (b->h_aln_regoff.n < (uint64_t)n + 1 || !b->h_aln_regoff.p) HIP_TRY(b->h_aln_regoff.ensure(n + 1));
-        if (b->h_aln_regs.n < b->tot_regs || !b->h_aln_regs.p)
-            HIP_TRY(b->h_aln_regs.ensure(std::max<uint64_t>(b->tot_regs + b->tot_regs / 4, 1)));
+    if (f_aln) {
+        HIP_TRY(b->h_aln_regoff.grow((uint64_t)n + 1));
+        HIP_TRY(b->h_aln_regs.grow(b->tot_regs));
         HIP_TRY(hipMemcpyAsync(b->h_aln_regoff.p, b->d_aln_regoff.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost,
                                b->st));
         if (b->tot_regs)
@@ -744,12 +778,29 @@ int smem_batch_fetch(smem_batch_t* b) {
                                    hipMemcpyDeviceToHost, b->st));
     }
     HIP_TRY(hipStreamSynchronize(b->st));
-    b->fetched = true;
-    b->sa_fetched = b->sa_ran;
-    b->chain_fetched = b->chain_ran;
-    b->aln_fetched = b->aln_ran;
+    b->fetched = f_intv;
+    b->sa_fetched = f_sa;
+    b->chain_fetched = f_chain;
+    b->aln_fetched = f_aln;
     return SMEM_OK;
 }
+
+int smem_batch_fetch(smem_batch_t* b) {
+    g_err[0] = 0;
+    if (!b || !b->ran) return fail(SMEM_E_ARG, "smem_batch_fetch: batch has not run");
+    return fetch_impl(b, SMEM_FETCH_ALL);
+}
+
+int smem_batch_fetch_mask(smem_batch_t* b, int mask) {
+    g_err[0] = 0;
+    if (!b || !b->ran) return fail(SMEM_E_ARG, "smem_batch_fetch_mask: batch has not run");
+    if (mask & ~SMEM_FETCH_ALL) return fail(SMEM_E_ARG, "smem_batch_fetch_mask: unknown bits");
+    if (((mask & SMEM_FETCH_SA) && !b->sa_ran) || ((mask & SMEM_FETCH_CHAINS) && !b->chain_ran) ||
+        ((mask & SMEM_FETCH_REGS) && !b->aln_ran))
+        return fail(SMEM_E_ARG, "smem_batch_fetch_mask: a requested stage has not run on this batch");
+    return fetch_impl(b, mask);
+}
+
 
 int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
     g_err[0] = 0;
@@ -811,11 +862,11 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     HIP_TRY(hipSetDevice(g->device));
     const uint64_t ni = b->tot_intv;
     if (ni >= (1ull << 31)) return fail(SMEM_E_CAPACITY, "smem_batch_sa: too many intervals");
-    HIP_TRY(b->d_occ_n.ensure(ni));
-    HIP_TRY(b->d_occ_off.ensure(ni + 1));
+    HIP_TRY(b->d_occ_n.grow(ni));
+    HIP_TRY(b->d_occ_off.grow(ni + 1));
     size_t tmp = 0;
     HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)std::max<uint64_t>(ni, 1), nullptr, &tmp, b->st));
-    HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
+    HIP_TRY(b->d_sa_tmp.grow(tmp + 256));
     smem::SaParams S;
     std::memset(&S, 0, sizeof(S));
     S.occ64 = g->d_occ64;
@@ -836,8 +887,8 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     HIP_TRY(hipMemcpyAsync(b->h_tot.p + 2, b->d_occ_off.p + ni, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
     HIP_TRY(hipStreamSynchronize(b->st));
     b->tot_occ = b->h_tot.p[2];
-    HIP_TRY(b->d_sa_pos.ensure(std::max<uint64_t>(b->tot_occ, 1)));
-    HIP_TRY(b->d_kstart.ensure(b->tot_occ + 2));  // +2: the walk's aligned 16-B loads
+    HIP_TRY(b->d_sa_pos.grow(std::max<uint64_t>(b->tot_occ, 1)));
+    HIP_TRY(b->d_kstart.grow(b->tot_occ + 2));  // +2: the walk's aligned 16-B loads
     S.n_occ = b->tot_occ;
     S.pos = b->d_sa_pos.p;
     S.kstart = b->d_kstart.p;
@@ -874,21 +925,21 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     HIP_TRY(hipSetDevice(b->g->device));
     const int n = b->n_reads;
     const uint64_t no = std::max<uint64_t>(b->tot_occ, 1);
-    HIP_TRY(b->d_seed.ensure(no));
-    HIP_TRY(b->d_next.ensure(no));
-    HIP_TRY(b->d_chn.ensure(no));
-    HIP_TRY(b->d_node.ensure(b->tot_occ / 7 + 3ull * (uint64_t)n + 8));
-    HIP_TRY(b->d_ord.ensure(no));
-    HIP_TRY(b->d_ord2.ensure(no));
-    HIP_TRY(b->d_flt.ensure(no));  // also the heavy path's per-seed codes
-    HIP_TRY(b->d_n_out.ensure(std::max(n, 1)));
-    HIP_TRY(b->d_ns_out.ensure(std::max(n, 1)));
-    HIP_TRY(b->d_chain_off.ensure(n + 1));
-    HIP_TRY(b->d_seed_off.ensure(n + 1));
-    HIP_TRY(b->d_heavy.ensure(2ull * (uint64_t)n + 4));
+    HIP_TRY(b->d_seed.grow(no));
+    HIP_TRY(b->d_next.grow(no));
+    HIP_TRY(b->d_chn.grow(no));
+    HIP_TRY(b->d_node.grow(b->tot_occ / 7 + 3ull * (uint64_t)n + 8));
+    HIP_TRY(b->d_ord.grow(no));
+    HIP_TRY(b->d_ord2.grow(no));
+    HIP_TRY(b->d_flt.grow(no));  // also the heavy path's per-seed codes
+    HIP_TRY(b->d_n_out.grow(std::max(n, 1)));
+    HIP_TRY(b->d_ns_out.grow(std::max(n, 1)));
+    HIP_TRY(b->d_chain_off.grow(n + 1));
+    HIP_TRY(b->d_seed_off.grow(n + 1));
+    HIP_TRY(b->d_heavy.grow(2ull * (uint64_t)n + 4));
     size_t tmp = 0;
     HIP_TRY(smem_launch_offsets(nullptr, nullptr, std::max(n, 1), nullptr, &tmp, b->st));
-    HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
+    HIP_TRY(b->d_sa_tmp.grow(tmp + 256));
     smem::ChainParams P;
     std::memset(&P, 0, sizeof(P));
     P.intv = reinterpret_cast<const uint64_t*>(b->d_flat_intv.p);
@@ -957,8 +1008,8 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     HIP_TRY(hipStreamSynchronize(b->st));
     b->tot_chains = b->h_tot.p[3];
     b->tot_seeds = b->h_tot.p[4];
-    HIP_TRY(b->d_out_chain.ensure(std::max<uint64_t>(b->tot_chains, 1)));
-    HIP_TRY(b->d_out_seed.ensure(std::max<uint64_t>(b->tot_seeds, 1)));
+    HIP_TRY(b->d_out_chain.grow(std::max<uint64_t>(b->tot_chains, 1)));
+    HIP_TRY(b->d_out_seed.grow(std::max<uint64_t>(b->tot_seeds, 1)));
     P.out_chain = b->d_out_chain.p;
     P.out_seed = b->d_out_seed.p;
     HIP_TRY(smem_launch_chain_write(&P, b->g->n_cu, b->st));
@@ -1220,17 +1271,27 @@ int smem_gpu_load_pac(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
     g_err[0] = 0;
     if (!g || !pac || l_pac <= 0 || 2 * (uint64_t)l_pac != g->L2[4])
         return fail(SMEM_E_ARG, "smem_gpu_load_pac: pac does not belong to this index (2 l_pac != seq_len)");
+    // under the device lock and after every queued kernel: no batch may be
+    // reading the old copy, and a failed upload leaves no half-written one
+    std::lock_guard<std::mutex> lk(g->mu);
     HIP_TRY(hipSetDevice(g->device));
+    HIP_TRY(hipDeviceSynchronize());
     if (g->d_pac) {
         (void)hipFree(g->d_pac);
         g->d_pac = nullptr;
     }
+    g->l_pac = 0;
     const uint64_t bytes = (uint64_t)(l_pac + 3) / 4;
-    hipError_t e = hipMalloc(&g->d_pac, bytes + 64);
+    uint8_t* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes + 64);
     if (e != hipSuccess) return fail(SMEM_E_NOMEM, "smem_gpu_load_pac: hipMalloc", e);
-    e = hipMemcpy(g->d_pac, pac, bytes, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(g->d_pac + bytes, 0, 64);
-    if (e != hipSuccess) return fail(SMEM_E_DEVICE, "smem_gpu_load_pac: upload", e);
+    e = hipMemcpy(p, pac, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(p + bytes, 0, 64);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return fail(SMEM_E_DEVICE, "smem_gpu_load_pac: upload", e);
+    }
+    g->d_pac = p;
     g->l_pac = l_pac;
     return SMEM_OK;
 }
@@ -1285,29 +1346,29 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
     }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
-        HIP_TRY(H.heavy.ensure(n));
-        HIP_TRY(H.hcnt.ensure(n));
-        HIP_TRY(H.hscnt.ensure(n));
+        HIP_TRY(H.heavy.grow(n));
+        HIP_TRY(H.hcnt.grow(n));
+        HIP_TRY(H.hscnt.grow(n));
         P.heavy = H.heavy.p, P.hcnt = H.hcnt.p, P.hscnt = H.hscnt.p;
         HIP_TRY(smem_launch_aln_classify(&P, st));
         HIP_TRY(hipMemcpyAsync(&n_heavy, P.ctr + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
     if (n_heavy) {
-        HIP_TRY(H.hoff.ensure(n_heavy + 1));
+        HIP_TRY(H.hoff.grow(n_heavy + 1));
         size_t tb = 0;
         HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)n_heavy, nullptr, &tb, st));
-        HIP_TRY(H.tmp.ensure(tb + 256));
+        HIP_TRY(H.tmp.grow(tb + 256));
         tb = H.tmp.n;
         HIP_TRY(smem_launch_offsets(H.hcnt.p, H.hoff.p, (int)n_heavy, H.tmp.p, &tb, st));
-        HIP_TRY(H.pre.ensure(std::max<uint64_t>(n_seeds, 1)));
-        HIP_TRY(H.loc.ensure(std::max<uint64_t>(n_seeds, 1)));
-        HIP_TRY(H.pre_ok.ensure(std::max<uint64_t>(n_seeds, 1)));
-        HIP_TRY(H.pre_short.ensure(std::max<uint64_t>(n_chains, 1)));
-        HIP_TRY(H.short_ok.ensure(std::max<uint64_t>(n_chains, 1)));
-        HIP_TRY(H.span.ensure(2 * std::max<uint64_t>(n_chains, 1)));
-        HIP_TRY(H.ht.ensure((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
-        HIP_TRY(H.rnext.ensure(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.pre.grow(std::max<uint64_t>(n_seeds, 1)));
+        if (P.spec_local) HIP_TRY(H.loc.grow(std::max<uint64_t>(n_seeds, 1)));  // only SMEM_ALN_SPEC_LOCAL reads it
+        HIP_TRY(H.pre_ok.grow(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.pre_short.grow(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.short_ok.grow(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.span.grow(2 * std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+        HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.hoff = H.hoff.p, P.pre = H.pre.p, P.loc = H.loc.p, P.pre_ok = H.pre_ok.p, P.pre_short = H.pre_short.p;
         P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
         if (st2 && ev_join) {
@@ -1339,14 +1400,14 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     HIP_TRY(hipSetDevice(g->device));
     const int n = b->n_reads;
     const uint64_t ns = std::max<uint64_t>(b->tot_seeds, 1);
-    HIP_TRY(b->d_aln_srt.ensure(ns + 1));
-    HIP_TRY(b->d_aln_raw.ensure(ns + 1));
-    HIP_TRY(b->d_aln_nregs.ensure(std::max(n, 1)));
-    HIP_TRY(b->d_aln_regoff.ensure(n + 1));
-    HIP_TRY(b->d_aln_ctr.ensure(smem::ALN_CTRS));
+    HIP_TRY(b->d_aln_srt.grow(ns + 1));
+    HIP_TRY(b->d_aln_raw.grow(ns + 1));
+    HIP_TRY(b->d_aln_nregs.grow(std::max(n, 1)));
+    HIP_TRY(b->d_aln_regoff.grow(n + 1));
+    HIP_TRY(b->d_aln_ctr.grow(smem::ALN_CTRS));
     size_t tmp = 0;
     HIP_TRY(smem_launch_offsets(nullptr, nullptr, std::max(n, 1), nullptr, &tmp, b->st));
-    HIP_TRY(b->d_sa_tmp.ensure(tmp + 256));
+    HIP_TRY(b->d_sa_tmp.grow(tmp + 256));
     smem::AlnParams P;
     std::memset(&P, 0, sizeof(P));
     P.codes = b->d_codes.p, P.offs = b->d_offs.p, P.chains = b->d_out_chain.p, P.chain_off = b->d_chain_off.p;
@@ -1383,7 +1444,7 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     HIP_TRY(hipStreamSynchronize(b->st));
     b->tot_regs = n > 0 ? b->h_tot.p[5] : 0;
     if (b->tot_regs > b->tot_seeds) return fail(SMEM_E_INTERNAL, "smem_batch_chain2aln: more regions than seeds");
-    HIP_TRY(b->d_aln_out.ensure(std::max<uint64_t>(b->tot_regs, 1)));
+    HIP_TRY(b->d_aln_out.grow(std::max<uint64_t>(b->tot_regs, 1)));
     P.reg_off = b->d_aln_regoff.p, P.out = b->d_aln_out.p;
     HIP_TRY(smem_launch_aln_write(&P, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
@@ -1677,7 +1738,9 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
         for (auto* b : bs)
             if (b) {
                 b->packed = false;
-                if (rc == SMEM_OK && g->stream_pool.size() < 16) g->stream_pool.push_back(b);
+                // kept for the next call, at most this call's worker count (each
+                // pins its staging and result buffers: ~1 GB per 1M-read chunk)
+                if (rc == SMEM_OK && g->stream_pool.size() < (size_t)nw) g->stream_pool.push_back(b);
                 else smem_batch_destroy(b);
             }
     }
@@ -1700,24 +1763,19 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
     return SMEM_OK;
 }
 
-int smem_gpu_collect(smem_gpu_t* g, int n_reads, const uint8_t* const* seq, const int* len, const smem_opt_t* opt,
-                     smem_batch_t** batch_out) {
-    g_err[0] = 0;
-    if (!g || !opt || !batch_out || n_reads < 0 || (n_reads > 0 && (!seq || !len)))
-        return fail(SMEM_E_ARG, "smem_gpu_collect");
-    *batch_out = nullptr;
-    int max_len = 1;
-    uint64_t bases = 0;
-    for (int i = 0; i < n_reads; ++i) {
-        if (len[i] < 0) return fail(SMEM_E_ARG, "smem_gpu_collect: negative length");
-        max_len = std::max(max_len, len[i]);
-        bases += (uint64_t)len[i];
-    }
+// the batch a collect call seeds into: the calling thread's (slot < 0) or the
+// worker slot's, (re)created when too small for this batch of reads
+static int collect_batch(smem_gpu_t* g, int slot, int n_reads, int max_len, uint64_t bases, smem_batch_t** out) {
     smem_batch_t* b = nullptr;
     {
         std::lock_guard<std::mutex> lk(g->mu);
-        auto it = g->per_thread.find(std::this_thread::get_id());
-        if (it != g->per_thread.end()) b = it->second;
+        if (slot >= 0) {
+            if ((size_t)slot >= g->slots.size()) g->slots.resize((size_t)slot + 1, nullptr);
+            b = g->slots[(size_t)slot];
+        } else {
+            auto it = g->per_thread.find(std::this_thread::get_id());
+            if (it != g->per_thread.end()) b = it->second;
+        }
     }
     if (!b || b->max_reads < n_reads || b->max_len < max_len || b->max_bases < bases) {
         const int mr = std::max(n_reads, b ? b->max_reads : 1);
@@ -1728,14 +1786,105 @@ int smem_gpu_collect(smem_gpu_t* g, int n_reads, const uint8_t* const* seq, cons
         if (rc) return rc;
         std::lock_guard<std::mutex> lk(g->mu);
         if (b) smem_batch_destroy(b);
-        g->per_thread[std::this_thread::get_id()] = nb;
+        if (slot >= 0) g->slots[(size_t)slot] = nb;
+        else g->per_thread[std::this_thread::get_id()] = nb;
         b = nb;
     }
-    int rc = smem_batch_set_reads(b, n_reads, seq, len);
+    *out = b;
+    return SMEM_OK;
+}
+
+int smem_gpu_collect_ex(smem_gpu_t* g, int slot, int n_reads, const uint8_t* const* seq, const int* len,
+                        const smem_opt_t* opt, int flags, smem_batch_t** batch_out) {
+    g_err[0] = 0;
+    if (!g || !opt || !batch_out || n_reads < 0 || (n_reads > 0 && (!seq || !len)) || slot > 4096 ||
+        (flags & ~SMEM_COLLECT_NO_FETCH))
+        return fail(SMEM_E_ARG, "smem_gpu_collect");
+    *batch_out = nullptr;
+    int max_len = 1;
+    uint64_t bases = 0;
+    for (int i = 0; i < n_reads; ++i) {
+        if (len[i] < 0) return fail(SMEM_E_ARG, "smem_gpu_collect: negative length");
+        max_len = std::max(max_len, len[i]);
+        bases += (uint64_t)len[i];
+    }
+    smem_batch_t* b = nullptr;
+    int rc = collect_batch(g, slot, n_reads, max_len, bases, &b);
+    if (!rc) rc = smem_batch_set_reads(b, n_reads, seq, len);
     if (!rc) rc = smem_batch_run(b, opt);
-    if (!rc) rc = smem_batch_fetch(b);
+    if (!rc && !(flags & SMEM_COLLECT_NO_FETCH)) rc = smem_batch_fetch(b);
     if (!rc) *batch_out = b;
     return rc;
+}
+
+int smem_gpu_collect(smem_gpu_t* g, int n_reads, const uint8_t* const* seq, const int* len, const smem_opt_t* opt,
+                     smem_batch_t** batch_out) {
+    return smem_gpu_collect_ex(g, -1, n_reads, seq, len, opt, 0, batch_out);
+}
+
+int smem_gpu_parse_devices(const char* spec, int* devices, int max_devices) {
+    g_err[0] = 0;
+    if (!devices || max_devices <= 0) return fail(SMEM_E_ARG, "smem_gpu_parse_devices");
+    const int n_vis = smem_gpu_device_count();
+    if (!spec || !*spec) {  // every visible device
+        if (n_vis <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_parse_devices: no HIP device");
+        const int n = std::min(n_vis, max_devices);
+        for (int i = 0; i < n; ++i) devices[i] = i;
+        return n;
+    }
+    int n = 0;
+    const char* p = spec;
+    while (*p) {
+        char* e = nullptr;
+        const long v = strtol(p, &e, 10);
+        if (e == p || v < 0 || v > 1 << 20) return fail(SMEM_E_ARG, "smem_gpu_parse_devices: bad device list");
+        if (n == max_devices) return fail(SMEM_E_ARG, "smem_gpu_parse_devices: too many devices");
+        devices[n++] = (int)v;
+        p = e;
+        if (*p == ',' && p[1]) ++p;
+        else if (*p) return fail(SMEM_E_ARG, "smem_gpu_parse_devices: bad device list");
+    }
+    if (n == 0) return fail(SMEM_E_ARG, "smem_gpu_parse_devices: empty device list");
+    return n;
+}
+
+int smem_gpu_init_devices(smem_gpu_t** gpus, int n, const int* devices, const uint32_t* bwt, uint64_t bwt_size,
+                          uint64_t primary, const uint64_t L2[5], const smem_sa_t* sa, const uint8_t* pac,
+                          int64_t l_pac) {
+    g_err[0] = 0;
+    if (!gpus || n <= 0 || n > 1024) return fail(SMEM_E_ARG, "smem_gpu_init_devices");
+    for (int i = 0; i < n; ++i) gpus[i] = nullptr;
+    std::vector<int> rc(n, SMEM_OK);
+    std::vector<std::string> msg(n);
+    // one host thread per device: the uploads (and each device's Occ64 /
+    // .sa densification kernels) run side by side
+    auto open1 = [&](int i) {
+        smem_gpu_t* g = nullptr;
+        int r = smem_gpu_init(&g, devices ? devices[i] : i, bwt, bwt_size, primary, L2);
+        if (!r && sa) r = smem_gpu_load_sa(g, sa);
+        if (!r && pac) r = smem_gpu_load_pac(g, pac, l_pac);
+        if (r) {
+            msg[i] = g_err;
+            smem_gpu_shutdown(g);
+            g = nullptr;
+        }
+        rc[i] = r;
+        gpus[i] = g;
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < n; ++i) th.emplace_back(open1, i);
+    open1(0);
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n; ++i) {
+        if (rc[i] == SMEM_OK) continue;
+        for (int k = 0; k < n; ++k) {
+            smem_gpu_shutdown(gpus[k]);
+            gpus[k] = nullptr;
+        }
+        snprintf(g_err, sizeof(g_err), "smem_gpu_init_devices: device %d: %s", devices ? devices[i] : i, msg[i].c_str());
+        return rc[i];
+    }
+    return SMEM_OK;
 }
 
 }  // extern "C"

@@ -96,6 +96,8 @@ struct FinalizeParams {
 
 extern "C" {
 hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st);
+// 1 when this build instantiates seeding-kernel variant `variant` (A/B variants need SMEM_AB_VARIANTS)
+int smem_seed_variant_built(int variant);
 // reference interleaved words (n_ref_buckets x 64 B) -> 2 * n_ref_buckets 32-B buckets
 hipError_t smem_launch_occ64(const uint32_t* bwt, uint64_t n_ref_buckets, uint32_t* out, hipStream_t st);
 hipError_t smem_launch_occ192(const uint32_t* occ64, uint64_t n_blocks, uint32_t* out, hipStream_t st);

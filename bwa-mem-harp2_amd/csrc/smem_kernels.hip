@@ -114,7 +114,7 @@ constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
 // keep the wave at 13 KB of LDS, so 3 blocks of 4 waves fit a CU, which
 // measured faster than 12 entries at 2 blocks (39.5 vs 42.1 ms per 1M reads).
 // The forward list itself stays in global memory.
-constexpr int LIST_LDS = 7;
+[[maybe_unused]] constexpr int LIST_LDS = 7;
 
 // Wave-private LDS.  img: the Occ bucket image (FETCH_OCC64: 4 planes
 // [slot*2 + chunk][lane]; FETCH_LANE: 8 planes [k0..k3, l0..l3][lane];
@@ -1252,37 +1252,52 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 }  // namespace smem
 
 // ------------------------------------------------------------ host launchers
+// The product build instantiates the default kernel (2; 0 and 20 name it too),
+// its stamped diagnostic twin (9) and the k-mer table variant (23).  The other
+// A/B variants measured in rounds 1-2 are compiled only with
+// SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
+// in every library for numbers already recorded.
+extern "C" int smem_seed_variant_built(int variant) {
+#ifdef SMEM_AB_VARIANTS
+    return variant == 0 || (variant >= 2 && variant <= 23);
+#else
+    return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23;
+#endif
+}
+
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
     switch (variant) {
+        // 9: the default with cycle stamps
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 23: the default with the k-mer table (P->kt)
+        case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+#ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
         // LDS at 2 blocks per CU; 6: Occ64, lists in global memory; 7: the
         // default with the bucket fetch of BWD_RES lanes issued inside the
         // advance (no gain measured: the fetch is throughput-bound); 8: 4 blocks per CU
-        // with 4 list entries in LDS; 9: the default with cycle stamps
+        // with 4 list entries in LDS
         case 3: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_COOP, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 4: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_LANE, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 5: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12>), dim3(grid), dim3(block), 0, st, *P); break;
         case 6: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 0>), dim3(grid), dim3(block), 0, st, *P); break;
         case 7: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 8: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 10: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         // 11: the first round-2 layout (LDS bucket slots, 7 list entries, forward ring)
         case 11: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 12: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 13: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 14: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 15: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 3, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 16: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 17: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 12, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 18: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 2, 13, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 19: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 20: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 21: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 7, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 22: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, true, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        // 23: the default with the k-mer table (P->kt)
-        case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 16: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS, true, false, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 14: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 4, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 15: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 3, true, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        case 13: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, smem::LIST_LDS>), dim3(grid), dim3(block), 0, st, *P); break;
+#endif
         // default (2): Occ64, the two bucket slots per lane in registers, 11 list
         // entries per lane in LDS (the forward list as a ring of its last 11 pushes)
         default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;

@@ -33,7 +33,12 @@ EXPORTED = [
     "smem_ksw_opt_default", "smem_ksw_extend", "smem_aln_opt_default", "smem_chain2aln",
     "smem_gpu_seed_stream", "smem_batch_results_packed",
     "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
+    "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
 ]
+
+# smem_batch_fetch_mask bits (include/smem_gpu.h)
+FETCH_INTV, FETCH_SA, FETCH_CHAINS, FETCH_REGS, FETCH_ALL = 1, 2, 4, 8, 15
+COLLECT_NO_FETCH = 1
 
 
 def source_hash() -> str:
@@ -162,6 +167,12 @@ def load() -> C.CDLL:
     lib.smem_gpu_shutdown.argtypes = [C.c_void_p]
     lib.smem_gpu_shutdown.restype = None
     lib.smem_gpu_collect.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, P(OptT), P(C.c_void_p)]
+    lib.smem_gpu_collect_ex.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, P(OptT), C.c_int,
+                                        P(C.c_void_p)]
+    lib.smem_gpu_init_devices.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                          P(C.c_uint64), C.c_void_p, C.c_void_p, C.c_int64]
+    lib.smem_gpu_parse_devices.argtypes = [C.c_char_p, C.c_void_p, C.c_int]
+    lib.smem_batch_fetch_mask.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_seed_stream.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, P(OptT), C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, C.c_void_p, P(StreamStats)]
     lib.smem_ksw_align2.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
@@ -597,12 +608,21 @@ class Batch:
             _check(rc, "smem_batch_debug")
         return out[:rc]
 
-    def fetch(self) -> Results:
+    def fetch(self, mask: int | None = None) -> Results:
+        """Copy the outputs back (smem_batch_fetch: every stage that ran; with
+        `mask`, smem_batch_fetch_mask: only the FETCH_* outputs named) and
+        return copies of them."""
         lib = load()
-        _check(lib.smem_batch_fetch(self._h), "smem_batch_fetch")
+        if mask is None:
+            _check(lib.smem_batch_fetch(self._h), "smem_batch_fetch")
+        else:
+            _check(lib.smem_batch_fetch_mask(self._h, int(mask)), "smem_batch_fetch_mask")
         n = int(self._keep[1].size - 1)
-        res = _results_of(lib, self._h, n)
-        ni = int(res.intv_off[-1])
+        if mask is None or mask & FETCH_INTV:
+            res = _results_of(lib, self._h, n)
+        else:
+            res = Results(None, None, None, None)
+        ni = int(res.intv_off[-1]) if res.intv_off is not None else int(self.stats()["n_intv"])
         pos = C.POINTER(C.c_uint64)()
         oo = C.POINTER(C.c_uint64)()
         no = C.c_uint64()

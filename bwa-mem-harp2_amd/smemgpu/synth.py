@@ -202,6 +202,64 @@ def write_fasta(path: str, genome: Genome, width: int = 60) -> None:
                 fh.write(s[k:k + width] + b"\n")
 
 
+def bns_contigs(n_bp: int, n_contigs: int = 24) -> list:
+    """(name, offset, len) of n_contigs near-equal contigs chr1..chrN covering
+    n_bp bases (each below 2^31: bntann1_t.len is an int32)."""
+    n = max(1, min(n_contigs, n_bp))
+    cuts = [n_bp * k // n for k in range(n + 1)]
+    return [(f"chr{k + 1}", cuts[k], cuts[k + 1] - cuts[k]) for k in range(n)]
+
+
+def write_bwa_bns(prefix: str, codes: np.ndarray, n_contigs: int = 24, chunk: int = 1 << 28) -> None:
+    """The .pac / .ann / .amb `bwa index` writes for a genome of codes 0..3
+    without ambiguous bases cut into bns_contigs (software/bntseq.c:63-93,
+    :275-288): 2-bit forward strand, MSB first, then a 0 byte when l_pac % 4 == 0
+    and l_pac % 4; contigs with gi 0, the "(null)" annotation bwa index gives a
+    FASTA header without a comment, no holes; seed 11.  With
+    the .bwt / .sa of the same codes these are a bwa index prefix (the FM
+    index does not depend on where contigs start).  Streams the codes in
+    chunks (a memory map of a human-size genome is fine)."""
+    n = int(codes.size)
+    with open(prefix + ".pac", "wb") as fh:
+        for a in range(0, n, chunk):   # chunk is a multiple of 4
+            c = np.minimum(np.asarray(codes[a:a + chunk], dtype=np.uint8), 3)
+            pad = (-c.size) % 4
+            if pad:
+                c = np.concatenate([c, np.zeros(pad, np.uint8)])
+            q = c.reshape(-1, 4)
+            fh.write((q[:, 0] << 6 | q[:, 1] << 4 | q[:, 2] << 2 | q[:, 3]).astype(np.uint8).tobytes())
+        if n % 4 == 0:
+            fh.write(b"\0")
+        fh.write(bytes([n % 4]))
+    contigs = bns_contigs(n, n_contigs)
+    with open(prefix + ".ann", "w") as fh:
+        fh.write(f"{n} {len(contigs)} 11\n")
+        for name, off, ln in contigs:
+            fh.write(f"0 {name} (null)\n{off} {ln} 0\n")   # a FASTA line without comment
+    with open(prefix + ".amb", "w") as fh:
+        fh.write(f"{n} {len(contigs)} 0\n")
+
+
+def write_fasta_contigs(path: str, codes: np.ndarray, n_contigs: int = 24, width: int = 60) -> None:
+    """FASTA of codes cut as bns_contigs (what write_bwa_bns describes)."""
+    with open(path, "wb") as fh:
+        for name, off, ln in bns_contigs(int(codes.size), n_contigs):
+            s = ACGT[np.minimum(codes[off:off + ln], 3)].tobytes()
+            fh.write(b">" + name.encode() + b"\n")
+            for k in range(0, len(s), width):
+                fh.write(s[k:k + width] + b"\n")
+
+
+def write_fastq(path: str, reads: "Reads", prefix: str = "r", qual: int = 40) -> None:
+    """Reads (codes 0..4) as FASTQ, named <prefix><index>."""
+    acgtn = np.frombuffer(b"ACGTN", dtype=np.uint8)
+    q = chr(33 + qual)
+    with open(path, "wb") as fh:
+        for i in range(reads.n):
+            s = acgtn[np.minimum(reads.read(i), 4)].tobytes()
+            fh.write(b"@%s%d\n%s\n+\n%s\n" % (prefix.encode(), i, s, (q * len(s)).encode()))
+
+
 def forward_reverse_text(codes: np.ndarray) -> np.ndarray:
     """The text BWA indexes: forward pac followed by its reverse complement
     (software/bntseq.c:303-309, bns_fasta2bntseq with for_only=0)."""

@@ -124,6 +124,21 @@ int  smem_gpu_init(smem_gpu_t **gpu, int device, const uint32_t *bwt, uint64_t b
                    uint64_t primary, const uint64_t L2[5]);
 void smem_gpu_shutdown(smem_gpu_t *gpu);
 
+/* Multi-GPU: the index replicated on `n` devices, one smem_gpu_t each
+ * (reads shard across GPUs, no collective).  devices[i] (NULL:
+ * 0 .. n-1) may repeat a device (two contexts on one GPU).  sa / pac (NULL:
+ * none) are made resident as smem_gpu_load_sa / smem_gpu_load_pac do.  The
+ * uploads run side by side, one host thread per device.  Replaces, for all
+ * devices at once, the single FPGA upload of software/bwa.c:286-307.  On
+ * failure every device opened so far is shut down and gpus[] is zeroed. */
+int  smem_gpu_init_devices(smem_gpu_t **gpus, int n, const int *devices, const uint32_t *bwt, uint64_t bwt_size,
+                           uint64_t primary, const uint64_t L2[5], const smem_sa_t *sa, const uint8_t *pac,
+                           int64_t l_pac);
+/* "0,2,5" -> devices[] = {0, 2, 5}; NULL or "" -> every visible device.
+ * Returns the count, or a negative code (bad list, more than max_devices,
+ * no device for the empty spec). */
+int  smem_gpu_parse_devices(const char *spec, int *devices, int max_devices);
+
 /* ------------------------------------------------------------ one shot */
 /* Thread-safe; may be called concurrently from kt_for_batch workers (each
  * calling thread gets its own stream and buffers, created on first use and
@@ -132,6 +147,18 @@ void smem_gpu_shutdown(smem_gpu_t *gpu);
  * smem_gpu_collect again.  Read them with smem_batch_read(*batch_out, i, ...). */
 int  smem_gpu_collect(smem_gpu_t *gpu, int n_reads, const uint8_t *const *seq, const int *len,
                       const smem_opt_t *opt, smem_batch_t **batch_out);
+/* The same with the batch chosen by worker slot (slot >= 0: the kt_for_batch
+ * tid of software/kthread_batch.c:38, which the reference maps to its
+ * per-worker FPGA buffer through get_thread_id, software/bwt.c:51-58; the slot's
+ * batch is reused by whichever thread holds the slot next, so the short-lived
+ * threads bwa mem starts per chunk do not each leave a batch behind; two
+ * threads must not use one slot at once; slot < 0: the calling thread's batch,
+ * as smem_gpu_collect).  flags: SMEM_COLLECT_NO_FETCH -- results stay in HBM
+ * for smem_batch_sa / _chain / _chain2aln, and smem_batch_fetch_mask copies
+ * only what the caller reads. */
+#define SMEM_COLLECT_NO_FETCH 1
+int  smem_gpu_collect_ex(smem_gpu_t *gpu, int slot, int n_reads, const uint8_t *const *seq, const int *len,
+                         const smem_opt_t *opt, int flags, smem_batch_t **batch_out);
 
 /* ------------------------------------------------------------ streaming */
 /* bwa mem's chunk loop (software/fastmap.c:213-228, mem_process_seqs ->
@@ -176,8 +203,19 @@ int  smem_batch_set_reads(smem_batch_t *b, int n_reads, const uint8_t *const *se
 int  smem_batch_set_reads_packed(smem_batch_t *b, int n_reads, const uint8_t *codes, const uint64_t *offsets);
 /* run the seeding loop on the resident reads; results stay in HBM */
 int  smem_batch_run(smem_batch_t *b, const smem_opt_t *opt);
-/* copy results device -> host (pinned) */
+/* copy results device -> host (pinned): every stage that has run */
 int  smem_batch_fetch(smem_batch_t *b);
+/* copy only the named outputs: the interval lists (smem_batch_read /
+ * _results), the SA positions (smem_batch_sa_results), the chains and seeds
+ * (smem_batch_chain_results), the regions (smem_batch_aln_results).  Naming a
+ * stage that has not run on this batch is SMEM_E_ARG.  A view whose output was
+ * not copied by the last fetch returns SMEM_E_ARG. */
+#define SMEM_FETCH_INTV    1
+#define SMEM_FETCH_SA      2
+#define SMEM_FETCH_CHAINS  4
+#define SMEM_FETCH_REGS    8
+#define SMEM_FETCH_ALL    15
+int  smem_batch_fetch_mask(smem_batch_t *b, int mask);
 /* per-read view of fetched results: the concatenation of all smem_next2
  * lists in order (n_intv intervals) and the size of each list (n_calls) */
 int  smem_batch_read(const smem_batch_t *b, int i, const smem_intv_t **intv, int *n_intv,
@@ -376,7 +414,9 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
 /* per-read output capacity (intervals) of batches created afterwards;
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
-/* seeding-kernel variant, all bit-exact, kept for A/B measurement:
+/* seeding-kernel variant, all bit-exact, kept for A/B measurement (the
+ * product build has 0 = 2 = 20, 9 and 23; the others need a library built with
+ * `make AB=1`, else SMEM_E_ARG):
  * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
  * device at init), per-lane fetch into two register slots with bucket reuse,
  * the first 11 entries of every list in LDS (the forward list as a ring of its

@@ -23,7 +23,8 @@ def _lib_is_current(lib: str) -> bool:
         return False
     import subprocess
     # in a child process: a loaded .so cannot be replaced in this one
-    code = ("import smemgpu,sys; sys.exit(0 if smemgpu.build_id() == smemgpu.source_hash() else 1)")
+    code = ("import smemgpu,sys; h = smemgpu.source_hash(); "
+            "sys.exit(0 if smemgpu.build_id() in (h, h + '-ab') else 1)")
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([PKG, ROOT]))
     return subprocess.run([sys.executable, "-c", code], env=env).returncode == 0
 
@@ -32,13 +33,15 @@ def _lib_is_current(lib: str) -> bool:
 def built():
     """Make sure the native artefacts exist and are built from the current
     sources (build once per session)."""
-    lib = os.path.join(PKG, "lib", "libsmemgpu.so")
+    # SMEMGPU_LIB may name the A/B build (make AB=1: lib_ab/, build id "<hash>-ab")
+    lib = os.environ.get("SMEMGPU_LIB") or os.path.join(PKG, "lib", "libsmemgpu.so")
     orc = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
     if not (_lib_is_current(lib) and os.path.exists(orc)):
         import __graft_entry__
         __graft_entry__.build()
     import smemgpu
-    assert smemgpu.build_id() == smemgpu.source_hash(), "libsmemgpu.so is not the build of these sources"
+    h = smemgpu.source_hash()
+    assert smemgpu.build_id() in (h, h + "-ab"), "libsmemgpu.so is not the build of these sources"
     return True
 
 

@@ -8,11 +8,17 @@ Golden: tests/golden/sam/*.sam.gz, the unpatched reference pipeline's SAM
 SAM apart from the @PG line -- north_star: "the `bwa mem` CLI and downstream
 chaining/SAM path are unchanged".
 
-* CPU (always): without a usable device the patched mem_chain_batched takes the
-  reject -> CPU path (mem_chain); SAM must still be identical.
-* GPU (-m gpu): seeding, bwt_sa and chaining of every kt_for_batch worker batch
-  run on the MI355X (smem_gpu_collect -> smem_batch_sa -> smem_batch_chain),
-  SW extension / pairing / SAM on the CPU, unchanged.
+* CPU (always): without a usable device the patched mem_align1_core_batched
+  takes the reject -> CPU path (mem_chain); SAM must still be identical.
+* GPU (-m gpu): the seeding loop, bwt_sa, mem_chain + mem_chain_flt and
+  mem_chain2aln_short / mem_chain2aln of every kt_for_batch worker batch run on
+  the MI355X (smem_gpu_collect_ex -> smem_batch_sa -> smem_batch_chain(filter)
+  -> smem_batch_chain2aln -> regions only), mem_sort_and_dedup / pairing / SAM
+  on the CPU, unchanged; also SMEM_GPU_STAGES=1 (chains back, filter and
+  extension on the CPU), two device contexts (SMEM_GPU_DEVICES=0,0: worker tid
+  on context tid % 2), and reads > 1024 bp (chains -> regions refused, the
+  GPU-filtered chains extended on the CPU), the last against the compiled
+  reference run on the same reads here.
 """
 import gzip
 import os
@@ -64,20 +70,90 @@ def _run(fa, g, kind, threads, batch, env=None):
 def test_cpu_fallback_sam_identical(indexed, g, kind):
     """No device (or a refused one): the patched build seeds on the CPU and
     the SAM equals the reference's."""
-    got, err = _run(indexed[g], g, kind, 3, 64, env={"SMEM_GPU_DEVICE": "63"})
+    got, err = _run(indexed[g], g, kind, 3, 64, env={"SMEM_GPU_DEVICES": "63"})
     assert "seeding on the CPU" in err
     assert got == _golden(g, kind)
+
+
+def _same(got, want):
+    assert len(got) == len(want)
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert not bad, f"{len(bad)} SAM lines differ, first: {got[bad[0]][:200]} vs {want[bad[0]][:200]}"
+
+
+GPU_MODES = {
+    "regions": {},                             # default: seeding -> regions on the GPU
+    "chains": {"SMEM_GPU_STAGES": "1"},        # seeding -> chains on the GPU (round-2 binding)
+    "two_ctx": {"SMEM_GPU_DEVICES": "0,0"},    # two device contexts, workers dealt tid % 2
+}
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("g,kind", CASES)
 @pytest.mark.parametrize("threads,batch", [(4, 4096), (3, 37)])
-def test_gpu_sam_identical(indexed, gpu_device, g, kind, threads, batch):
-    """Seeding + bwt_sa + mem_chain on the MI355X behind mem_chain_batched:
-    SAM byte-identical to the reference's `bwa mem -t 1 -b 1`."""
-    got, err = _run(indexed[g], g, kind, threads, batch)
-    assert "seeding on the CPU" not in err, err[-2000:]
-    want = _golden(g, kind)
-    assert len(got) == len(want)
-    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
-    assert not bad, f"{len(bad)} SAM lines differ, first: {got[bad[0]][:200]} vs {want[bad[0]][:200]}"
+@pytest.mark.parametrize("mode", sorted(GPU_MODES))
+def test_gpu_sam_identical(indexed, gpu_device, g, kind, threads, batch, mode):
+    """Seeding -> regions (or -> chains) on the MI355X behind
+    mem_align1_core_batched: SAM byte-identical to the reference's
+    `bwa mem -t 1 -b 1`."""
+    got, err = _run(indexed[g], g, kind, threads, batch, env=GPU_MODES[mode])
+    assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
+    if mode == "two_ctx":
+        assert "resident on 2 GPU context(s)" in err, err[-2000:]
+    _same(got, _golden(g, kind))
+
+
+@pytest.mark.gpu
+def test_gpu_long_reads_sam_identical(indexed, gpu_device, tmp_path):
+    """Reads of 30-2000 bp (every batch holds some > 1024 bp, which
+    smem_batch_chain2aln refuses): the GPU-filtered chains are extended on the
+    CPU; SAM equals the compiled reference's `-b 1` run on the same reads
+    (oracle/_ref/ref_harness mem, built from the reference sources)."""
+    import numpy as np
+    from smemgpu import synth
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(ref):
+        pytest.fail("oracle/_ref/ref_harness missing (built by __graft_entry__.build() where /root/reference exists)")
+    fa = indexed["g1"]
+    seq = []
+    with open(fa, "rb") as fh:
+        for line in fh:
+            if not line.startswith(b">"):
+                seq.append(line.strip())
+    codes = synth.NT4[np.frombuffer(b"".join(seq), dtype=np.uint8)]
+    r = synth.make_reads(codes, 600, (30, 2000), seed=31, sub_rate=0.02, n_rate=0.002, random_frac=0.05)
+    fq = tmp_path / "long.fq"
+    acgtn = np.frombuffer(b"ACGTN", dtype=np.uint8)
+    with open(fq, "wb") as fh:
+        for i in range(r.n):
+            s = acgtn[np.minimum(r.read(i), 4)].tobytes()
+            fh.write(b"@l%d\n" % i + s + b"\n+\n" + b"I" * len(s) + b"\n")
+    p = subprocess.run([ref, "mem", fa, str(fq), "4", "1", "0"], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    want = [l for l in p.stdout.split("\n") if l and not l.startswith("@PG")]
+    args = [BWA, "mem", "-t", "3", "-b", "128", fa, str(fq)]
+    q = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    assert q.returncode == 0, q.stderr[-2000:]
+    assert "seeding on the CPU" not in q.stderr, q.stderr[-2000:]
+    _same([l for l in q.stdout.split("\n") if l and not l.startswith("@PG")], want)
+
+
+def test_bwa_prefix_from_smem_index_matches_bwa_index(tmp_path, built):
+    """bench.py's e2e leg builds the human-size bwa index prefix from this
+    repo's own .bwt / .sa plus synth.write_bwa_bns (.pac / .ann / .amb): on a
+    small genome cut the same way, all five files equal the reference's own
+    `bwa index -a is` output byte for byte."""
+    _need_bwa()
+    import smemgpu
+    from smemgpu import synth
+    g = synth.make_genome(250_000, seed=77)
+    fa = tmp_path / "c.fa"
+    synth.write_fasta_contigs(str(fa), g.codes, n_contigs=5)
+    subprocess.run([BWA, "index", "-a", "is", str(fa)], check=True, capture_output=True)
+    mine = str(tmp_path / "m")
+    idx, sa = smemgpu.Index.build_sa(g.codes, sa_intv=32)
+    idx.write(mine + ".bwt")
+    sa.write(mine + ".sa")
+    synth.write_bwa_bns(mine, g.codes, n_contigs=5)
+    for ext in (".bwt", ".sa", ".pac", ".ann", ".amb"):
+        assert open(mine + ext, "rb").read() == open(str(fa) + ext, "rb").read(), ext

@@ -149,8 +149,12 @@ def test_few_lanes_many_reads_per_lane(world, gpu_device):
 @pytest.mark.parametrize("variant", [3, 4, 5, 6, 9, 10, 11, 12, 13, 16, 19, 20, 21, 22])
 def test_kernel_variants(world, gpu_device, variant):
     """The A/B builds (reference-layout fetches, stamped, forward-list LDS
-    ring) are bit-exact too."""
+    ring) are bit-exact too.  The product library instantiates 9 (stamped)
+    and 20 (= the default); the others need a library built with
+    `make -C bwa-mem-harp2_amd AB=1` (lib_ab/, run with SMEMGPU_LIB)."""
     import smemgpu
+    if not smemgpu.load().smem_seed_variant_built(variant):
+        pytest.skip(f"A/B variant {variant} is not in this build (make AB=1)")
     gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant)
     try:
         reads = synth_concat(_reads(world["genome"], "mixed", seed=11), _reads(world["genome"], "250bp5", seed=12))
