@@ -62,6 +62,10 @@ METRIC = "SMEM reads/sec on human_g1k_v37 150bp at 1/2/4/8 MI355X; achieved HBM 
 RT_TICKS_PER_MS = 1e5  # s_memrealtime: 100 MHz (checked against HIP events: chip_clock_check)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 HUMAN_MBP = 3101.804739  # human_g1k_v37 l_pac
+# VALU int32 peak (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs x 32 lanes/clock x 2.4 GHz) and the DP stages' cell
+# ceiling at 8 int32 ops per affine-gap cell (H = max(diag + score, E, F); E', F' = max(. - e, H - o - e); 0 floor)
+VALU_INT32_OPS = 256 * 4 * 32 * 2.4e9
+OPS_PER_CELL = 8
 BLOCK = 1 << 18          # reads per block of the read stream (shards are whole blocks)
 
 # BASELINE.json configs: per-GPU shapes
@@ -462,7 +466,16 @@ def pack_pac(codes) -> np.ndarray:
     return out
 
 
-def aln_report(gpu, batch, opt, l_pac: int, reps: int = 3) -> dict:
+def dp_roofline(cells: float, ms: float) -> dict:
+    achieved = cells / (ms * 1e-3)
+    peak = VALU_INT32_OPS / OPS_PER_CELL
+    return {"bound": "valu", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "cells/s",
+            "frac": round(achieved / peak, 5), "gcups": round(achieved / 1e9, 2),
+            "peak_source": f"VALU int32 {VALU_INT32_OPS / 1e12:.1f} T ops/s (256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz) / "
+                           f"{OPS_PER_CELL} ops per affine-gap cell"}
+
+
+def aln_report(gpu, batch, opt, l_pac: int, pac=None, reads=None, reps: int = 3, cell_sample: int = 50000) -> dict:
     """Chains -> alignment regions (mem_chain2aln_short /
     mem_chain2aln of every filtered chain, software/bwamem.c:1452-1460) on the
     GPU over the chains, seeds, reads and .pac already in HBM
@@ -478,10 +491,28 @@ def aln_report(gpu, batch, opt, l_pac: int, reps: int = 3) -> dict:
         if best is None or st["aln_ms"] < best["aln_ms"]:
             best = st
     n = batch.n_reads
-    return {"ms_per_batch": round(best["aln_ms"], 3), "regions": int(best["n_regs"]), "chains": int(best["n_chains"]),
-            "reads_per_s": round(n / (best["aln_ms"] * 1e-3), 1),
+    cells = None
+    if pac is not None and reads is not None:
+        # the DP cells the stage computes, counted by the restatement on the
+        # first cell_sample reads (same chains), scaled to the batch
+        res = batch.fetch(mask=4)   # FETCH_CHAINS
+        m = min(cell_sample, n)
+        aopt = oracle.aln_opt(min_seed_len=opt.min_seed_len)
+        oracle.dp_cells(True)
+        oracle.aln(pac, l_pac, reads.codes, reads.offs[:m + 1], res.chains, res.chain_off[:m + 1], res.seeds, aopt)
+        ext, sw = oracle.dp_cells(True)
+        cells = {"ksw_extend2_in_band": ext, "ksw_align2": sw, "sample_reads": m,
+                 "per_read": round((ext + sw) / max(m, 1), 1)}
+    out = {"ms_per_batch": round(best["aln_ms"], 3), "regions": int(best["n_regs"]), "chains": int(best["n_chains"]),
+           "reads_per_s": round(n / (best["aln_ms"] * 1e-3), 1)}
+    if cells:
+        out["dp_cells"] = cells
+        out["roofline"] = dp_roofline(cells["per_read"] * n, best["aln_ms"])
+        out["roofline"]["cells_note"] = (f"cells per read counted by the restatement on the first {cells['sample_reads']} "
+                                         "reads x the batch's reads")
+    return dict(out, **{
             "what": "mem_chain2aln_short / mem_chain2aln (ksw_align2, ksw_extend2 both ways, MAX_BAND_TRY) of every "
-                    "chain kept by mem_chain_flt, one wave per read, chains / seeds / reads / .pac resident in HBM"}
+                    "chain kept by mem_chain_flt, one wave per read, chains / seeds / reads / .pac resident in HBM"})
 
 
 def aln_cpu(args, idx_path: str, reads, genome_codes, opt, n: int = 20000) -> dict:
@@ -517,7 +548,12 @@ def sw_report(gpu, genome_codes, n_unique: int = 20000, tile: int = 10, reps: in
         _, ms = gpu.ksw_extend(big)
         best = min(best, ms)
     cells = int(np.sum(kb.tasks["qlen"].astype(np.int64) * kb.tasks["tlen"])) * tile
-    return {"tasks": int(big.tasks.size), "kernel_ms": round(best, 3),
+    from oracle import oracle
+    oracle.dp_cells(True)
+    oracle.ksw(kb)
+    band = oracle.dp_cells(True)[0] * tile   # in-band cells ksw_extend2 computes (restatement's count)
+    return {"tasks": int(big.tasks.size), "kernel_ms": round(best, 3), "dp_cells_in_band": band,
+            "roofline": dp_roofline(band, best),
             "tasks_per_s": round(big.tasks.size / (best * 1e-3), 1),
             "what": "ksw_extend2 (software/ksw.c:379), one wave per problem; synthetic mem_chain2aln-shaped "
                     "left/right extensions of 100-250 bp reads (2-5% subs, 0.4% indels), w 100 (some 200 / narrow), "
@@ -861,8 +897,10 @@ def main():
     if rank == 0 and args.side_stages:
         sa_rep = sa_lookup(batch, opt)
         chain_rep = chain_report(batch, opt, idx.seq_len // 2)
-        gpu.load_pac(pack_pac(genome_codes), idx.seq_len // 2)
-        aln_rep = aln_report(gpu, batch, opt, idx.seq_len // 2)
+        pac = pack_pac(genome_codes)
+        gpu.load_pac(pac, idx.seq_len // 2)
+        aln_rep = aln_report(gpu, batch, opt, idx.seq_len // 2, pac=pac, reads=reads)
+        del pac
         sw_rep, sw_tasks = sw_report(gpu, np.asarray(genome_codes))
 
     out = None

@@ -55,6 +55,8 @@ void orc_sw_shift_top(const int8_t *mat, int *shift, int *top)
 }
 
 /* one ksw_u8 (p = 16) or ksw_i16 (p = 8) run; xtra as there */
+extern __thread uint64_t orc_cells_ext, orc_cells_sw;  /* ksw_oracle.c */
+
 static swr_t sw_pass(int p, int qlen, const uint8_t *query, int tlen, const uint8_t *target, const int8_t *mat,
 		int o_del, int e_del, int o_ins, int e_ins, int xtra)
 {
@@ -76,6 +78,7 @@ static swr_t sw_pass(int p, int qlen, const uint8_t *query, int tlen, const uint
 	for (i = 0; i < tlen; ++i) {
 		const int8_t *s = prof + target[i] * qp;
 		int rmax = 0;
+		orc_cells_sw += (uint64_t)qlen;
 		/* pass 1: F inside each block of slen columns */
 		for (l = 0; l < p; ++l) {
 			int fl = 0;

@@ -22,6 +22,17 @@
 
 typedef struct { int32_t hprev, e; } col_t;
 
+/* DP cells computed (in-band cells of ksw_extend2, the whole qlen x tlen
+ * matrix of every ksw_align2 pass), per thread: the algorithmic work the GPU's
+ * DP kernels are measured against (bench.py: cells/s) */
+__thread uint64_t orc_cells_ext, orc_cells_sw;
+
+void orc_cells(uint64_t out[2], int reset)
+{
+	out[0] = orc_cells_ext, out[1] = orc_cells_sw;
+	if (reset) orc_cells_ext = orc_cells_sw = 0;
+}
+
 static int imax(int a, int b) { return a > b ? a : b; }
 
 int orc_ksw_extend(const orc_ksw_task_t *T, const uint8_t *query, const uint8_t *target, const orc_ksw_opt_t *o,
@@ -65,6 +76,7 @@ int orc_ksw_extend(const orc_ksw_task_t *T, const uint8_t *query, const uint8_t 
 		if (lo < row - w) lo = row - w;
 		if (hi > row + w + 1) hi = row + w + 1;
 		if (hi > qlen) hi = qlen;
+		if (hi > lo) orc_cells_ext += (uint64_t)(hi - lo);
 		for (j = lo; j < hi; ++j) {
 			int h = c[j].hprev + s[j], e = c[j].e, t;
 			c[j].hprev = hleft;                       /* H(row, j-1) for the next row */

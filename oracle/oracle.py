@@ -96,6 +96,8 @@ def load() -> C.CDLL:
         lib.orc_aln_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p]
         lib.orc_aln_batch.restype = C.c_int
+        lib.orc_cells.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+        lib.orc_cells.restype = None
         lib.orc_ksw_align2.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                        C.c_int, C.c_int, C.POINTER(C.c_int32)]
         lib.orc_ksw_align2.restype = None
@@ -397,6 +399,15 @@ def aln_opt(w=100, min_seed_len=19, a=1, b=4, o_del=6, e_del=1, o_ins=6, e_ins=1
     o.o_del, o.e_del, o.o_ins, o.e_ins, o.a, o.w, o.zdrop = o_del, e_del, o_ins, e_ins, a, w, zdrop
     o.pen_clip5, o.pen_clip3, o.min_seed_len = pen_clip5, pen_clip3, min_seed_len
     return o
+
+
+def dp_cells(reset: bool = True) -> tuple:
+    """(ksw_extend2 in-band cells, ksw_align2 query x target cells) the
+    restatement computed on this thread since the last reset: the DP stages'
+    algorithmic work (ksw_oracle.c orc_cells)."""
+    out = (C.c_uint64 * 2)()
+    load().orc_cells(out, 1 if reset else 0)
+    return int(out[0]), int(out[1])
 
 
 def aln(pac, l_pac: int, codes, offs, chains, chain_off, seeds, opt: AlnOptT):

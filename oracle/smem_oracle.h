@@ -139,6 +139,10 @@ typedef struct {
 } orc_ksw_opt_t;
 int orc_ksw_extend(const orc_ksw_task_t *t, const uint8_t *query, const uint8_t *target, const orc_ksw_opt_t *o,
 		orc_ksw_result_t *res);
+/* DP cells this thread computed since the last reset: out[0] in-band cells of
+ * ksw_extend2 (the columns [lo, hi) of every row), out[1] query x target cells
+ * of every ksw_align2 pass */
+void orc_cells(uint64_t out[2], int reset);
 int orc_ksw_batch(int64_t n, const orc_ksw_task_t *tasks, const uint8_t *q, const uint8_t *t, const orc_ksw_opt_t *o,
 		orc_ksw_result_t *out);
 

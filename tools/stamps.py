@@ -18,31 +18,31 @@ PHASES = ["BWD_RES", "BWD_J", "FWD_RES", "FWD", "FWD_DONE", "BWD_STEP", "SMEM_EN
 
 
 def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--genome-mbp", type=float, default=1000)
-    p.add_argument("--reads", type=int, default=1_000_000)
-    p.add_argument("--lanes-per-cu", type=int, default=0)
-    p.add_argument("--variant", type=int, default=2, help="production variant timed beside the stamped one")
-    p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
-    a = p.parse_args()
+    """Any bench.py argument selects the workload (--genome-profile, --config,
+    --reads ...: the bench's own cached index and reads); --compare is the
+    production variant timed beside the stamped one, --out a JSON file."""
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--compare", type=int, default=2, help="production variant timed beside the stamped one")
+    p.add_argument("--out", default=None)
+    own, rest = p.parse_known_args()
+    import bench
     import smemgpu
-    from smemgpu import synth
-    os.makedirs(a.cache, exist_ok=True)
-    n_bp = int(a.genome_mbp * 1e6)
-    key = os.path.join(a.cache, f"genome_{n_bp}_1.bwt")
-    g = synth.make_genome(n_bp, seed=1, n_chrom=24)
-    if not os.path.exists(key):
-        smemgpu.Index.build_gpu(g.codes).write(key)
-    idx = smemgpu.Index.read(key)
-    reads = synth.make_reads(g.codes, a.reads, 150, seed=1000 + 7919, sub_rate=0.02, n_rate=0.001)
+    a = bench.parse(rest)
+    idx, _, _, codes = bench.get_index(a, 0, lambda: None, 0)
+    reads = bench.make_reads(a, 0, codes, 1)
+    a.variant = own.compare
+    results = {"workload": {"genome_profile": a.genome_profile, "genome_mbp": a.genome_mbp, "reads": reads.n,
+                            "read_len": a.read_len, "sub": a.sub}}
     for variant in (a.variant, 9):
         gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu, variant=variant)
+        opt = smemgpu.Options(min_seed_len=a.min_seed_len)
         b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
         b.set_reads(reads.codes, reads.offs)
-        b.run()
-        b.run()
+        b.run(opt)
+        b.run(opt)
         st = b.stats()
         print(f"variant {variant}: kernel {st['kernel_ms']:.2f} ms", flush=True)
+        results[f"kernel_ms_variant_{variant}"] = st["kernel_ms"]
         if variant == 9:
             w = b.debug_words(st["grid"] * 4 * 32).reshape(-1, 32).astype(np.float64)
             adv, fet, comp, it, act, t0, t1 = (w[:, k] for k in range(7))
@@ -64,8 +64,12 @@ def main():
                 "share_adv_fetch_comp": [float(adv.sum() / tot), float(fet.sum() / tot), float(comp.sum() / tot)],
             }
             print(json.dumps(out, indent=1), flush=True)
+            results["stamps"] = out
         b.close()
         gpu.close()
+    if own.out:
+        with open(own.out, "w") as fh:
+            json.dump(results, fh, indent=1)
 
 
 if __name__ == "__main__":
