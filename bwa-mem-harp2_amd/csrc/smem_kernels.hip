@@ -336,6 +336,47 @@ __device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a,
     nb = b + (uint64_t)(a <= P.primary && a + s - 1 >= P.primary) + gt;
 }
 
+// The same bwt_extend (child c only) with 32-bit arithmetic wherever the
+// values allow it and no branch on c.  When every base occurs fewer than 2^32
+// times in the BWT (the host checks L2; a human-size index: at most 1.9 G),
+// every interval size -- and so ns and the other coordinate's cumulative
+// difference -- is below 2^32, so both are exact as differences of the
+// counts' low 32-bit words (mod 2^32).  Only na = L2[c] + 1 + Occ(c, kk)
+// needs the 34-bit checkpoint.  The base selections are cndmask chains on
+// 32-bit words.
+__device__ __forceinline__ void extend_counts64_lean(const SeedParams& P, uint64_t a, uint64_t b, uint64_t s, int c,
+                                                     uint64_t kk, uint64_t ll, const Bucket32& vk, const Bucket32& vl,
+                                                     uint64_t& na, uint64_t& nb, uint64_t& ns) {
+    uint32_t Ck, Gk, Tk, Cl, Gl, Tl;
+    count_cgt4(vk.sym, (uint32_t)(kk & 63), Ck, Gk, Tk);
+    count_cgt4(vl.sym, (uint32_t)(ll & 63), Cl, Gl, Tl);
+    // low words of Occ(C | G | T, .) and Occ(A, .) = pos + 1 - C - G - T
+    const uint32_t kC = vk.cnt.x + Ck, kG = vk.cnt.y + Gk, kT = vk.cnt.z + Tk;
+    const uint32_t lC = vl.cnt.x + Cl, lG = vl.cnt.y + Gl, lT = vl.cnt.z + Tl;
+    const uint32_t kTG = kT + kG, lTG = lT + lG;
+    const uint32_t kA = (uint32_t)kk + 1u - kTG - kC, lA = (uint32_t)ll + 1u - lTG - lC;
+    const bool c0 = (c & 1) != 0, c1 = (c & 2) != 0;
+    const uint32_t ok = c1 ? (c0 ? kT : kG) : (c0 ? kC : kA);
+    const uint32_t ol = c1 ? (c0 ? lT : lG) : (c0 ? lC : lA);
+    // Occ of the bases after c (the other coordinate's cumulative count)
+    const uint32_t gk = c1 ? (c0 ? 0u : kT) : (c0 ? kTG : kTG + kC);
+    const uint32_t gl = c1 ? (c0 ? 0u : lT) : (c0 ? lTG : lTG + lC);
+    ns = (uint64_t)(ol - ok);
+    const uint32_t dollar = (a <= P.primary && a + s - 1 >= P.primary) ? 1u : 0u;
+    nb = b + (uint64_t)(gl - gk + dollar);
+    // na: Occ(c, kk) with its checkpoint's bits 32-33; for A, kk + 1 minus
+    // the 34-bit C + G + T
+    const uint32_t w = vk.cnt.w;
+    const uint64_t cgt = (uint64_t)vk.cnt.x + vk.cnt.y + vk.cnt.z + (Ck + Gk + Tk) +
+                         ((uint64_t)((w & 3u) + ((w >> 2) & 3u) + ((w >> 4) & 3u)) << 32);
+    const uint32_t sel_lo = c1 ? (c0 ? vk.cnt.z : vk.cnt.y) : vk.cnt.x;
+    const uint32_t sel_pf = c1 ? (c0 ? Tk : Gk) : Ck;
+    const uint32_t sel_hi = (w >> (2u * (uint32_t)(c > 0 ? c - 1 : 0))) & 3u;
+    const uint64_t occ = c == 0 ? kk + 1 - cgt : ((uint64_t)sel_hi << 32 | sel_lo) + sel_pf;
+    const uint64_t L2c = c1 ? (c0 ? P.L2[3] : P.L2[2]) : (c0 ? P.L2[1] : P.L2[0]);
+    na = L2c + 1 + occ;
+}
+
 // Fetch the Occ64 buckets of k and l (issue: DMAs, tags; read: after the
 // wave's vmcnt wait).  Each lane keeps the two buckets it
 // fetched last in two LDS slots (planes [2*slot + chunk][lane]) with their
@@ -480,7 +521,7 @@ __device__ __forceinline__ uint64_t stamp() {
 // its forward string (first kt_k bases) and, in the backward phase, of the
 // kt_k bases from the current position (rolled one base per step).
 template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
-          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false>
+          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool LEAN = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -1145,7 +1186,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             nb = fwd ? p_x0(ktv) : p_x1(ktv);
             ns = p_x2(ktv);
         } else if (want) {
-            if constexpr (FETCH == FETCH_OCC64)
+            if constexpr (FETCH == FETCH_OCC64 && LEAN && !L192)
+                extend_counts64_lean(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
+            else if constexpr (FETCH == FETCH_OCC64)
                 extend_counts64<L192>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
             else
                 extend_counts(P, ra, rb, rs, rc, kk, ll, vk, vl, na, nb, ns);
@@ -1259,9 +1302,10 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
 #ifdef SMEM_AB_VARIANTS
-    return variant == 0 || (variant >= 2 && variant <= 23);
+    return variant == 0 || (variant >= 2 && variant <= 25);
 #else
-    return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23;
+    return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23 || variant == 24 ||
+           variant == 25;
 #endif
 }
 
@@ -1271,6 +1315,10 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         // 23: the default with the k-mer table (P->kt)
         case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 24: the default with the 32-bit extend (extend_counts64_lean; base counts < 2^32, checked on the host);
+        // 25: its stamped twin
+        case 24: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 25: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

@@ -147,7 +147,7 @@ def test_collect_ex_no_fetch_then_stages(world):
         gpu.load_pac(pac, g.codes.size)
         rc, bh, keep = _collect(lib, gpu._h, 0, reads, 0, reads.n, flags=smemgpu.lib.COLLECT_NO_FETCH)
         assert rc == 0
-        iv = C.c_void_p()
+        iv = C.POINTER(smemgpu.lib.Intv)()
         off = C.POINTER(C.c_uint64)()
         assert lib.smem_batch_results(bh, C.byref(iv), C.byref(off), None, None) != 0   # nothing fetched
         assert lib.smem_batch_fetch_mask(bh, smemgpu.lib.FETCH_REGS) != 0                # no regions yet

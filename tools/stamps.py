@@ -23,6 +23,7 @@ def main():
     production variant timed beside the stamped one, --out a JSON file."""
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--compare", type=int, default=2, help="production variant timed beside the stamped one")
+    p.add_argument("--stamped", type=int, default=9, help="the stamped variant (9: default kernel, 25: lean extend)")
     p.add_argument("--out", default=None)
     own, rest = p.parse_known_args()
     import bench
@@ -33,7 +34,7 @@ def main():
     a.variant = own.compare
     results = {"workload": {"genome_profile": a.genome_profile, "genome_mbp": a.genome_mbp, "reads": reads.n,
                             "read_len": a.read_len, "sub": a.sub}}
-    for variant in (a.variant, 9):
+    for variant in (a.variant, own.stamped):
         gpu = smemgpu.Gpu(idx, device=0, lanes_per_cu=a.lanes_per_cu, variant=variant)
         opt = smemgpu.Options(min_seed_len=a.min_seed_len)
         b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
@@ -43,7 +44,7 @@ def main():
         st = b.stats()
         print(f"variant {variant}: kernel {st['kernel_ms']:.2f} ms", flush=True)
         results[f"kernel_ms_variant_{variant}"] = st["kernel_ms"]
-        if variant == 9:
+        if variant == own.stamped:
             w = b.debug_words(st["grid"] * 4 * 32).reshape(-1, 32).astype(np.float64)
             adv, fet, comp, it, act, t0, t1 = (w[:, k] for k in range(7))
             tot = adv.sum() + fet.sum() + comp.sum()
