@@ -6,7 +6,7 @@
 #
 # Outputs land in gpurun_out/<out>/.  Steps (ARGS: bench.py / tool arguments
 # with commas for spaces, e.g. bench:--steps,10,--genome-profile,human):
-#   tests[:FILTER]    python -m pytest tests -m gpu [-k FILTER]     -> tests.log
+#   tests[:FILTER]    python -m pytest tests -m gpu [-k FILTER] (commas: spaces, e.g. tests:product,or,variants) -> tests.log
 #   smoke             __graft_entry__.smoke()                         -> smoke.log
 #   traffic[:ARGS]    tools/traffic.py for this build (TCC_EA0_RDREQ per launch) -> traffic.json,
 #                     copied to profiles/traffic.json (or profiles/traffic_human.json with --genome-profile,human)
@@ -33,7 +33,7 @@ for step in "$@"; do
   case "$name" in
     tests)
       sel=()
-      [ -n "$arg" ] && sel=(-k "$arg")
+      [ -n "$arg" ] && sel=(-k "$args")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${sel[@]}" \
         > "$OUT/tests.log" 2>&1 || { echo "tests failed"; exit $k; } ;;
     smoke)
