@@ -52,6 +52,7 @@ struct AlnParams {
     uint32_t hash_min;        // heavy reads with at least this many chains hash their regions by bin
     uint32_t spec_local;      // 1: a heavy chain precomputes only the seeds its own walk extends (0: all)
     uint32_t light_claims;    // aln_kernel: work-queue claims per wave before it exits (0: until the queue is empty)
+    uint32_t walk_guard;      // != 0: the inlined walk, at most this many loop iterations per read (ctr[15] counts trips)
     int32_t* heavy;           // [n_reads] heavy read ids (ctr[2] of them, any order)
     uint64_t* hcnt;           // [n_reads] their chain counts, then
     uint64_t* hoff;           // [n_heavy + 1] prefix: chain task t of the heavy reads

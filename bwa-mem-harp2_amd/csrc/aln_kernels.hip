@@ -498,7 +498,10 @@ __device__ __forceinline__ bool reg_contains(const AlnParams& P, int64_t s_rb, i
 // the read's longest region before the seed, so a containment test visits
 // one or two bins instead of every region made so far.
 constexpr int HT_BIN = 9;
-__device__ __forceinline__ uint32_t ht_home(uint64_t bin) { return ((uint32_t)bin * 2654435761u) >> 18; }
+// Fibonacci hashing onto all ALN_HT slots (the top log2(ALN_HT) bits of the product)
+constexpr uint32_t ALN_HT_BITS = __builtin_ctz((unsigned)ALN_HT);
+static_assert((1u << ALN_HT_BITS) == (uint32_t)ALN_HT, "ALN_HT is a power of 2");
+__device__ __forceinline__ uint32_t ht_home(uint64_t bin) { return ((uint32_t)bin * 2654435761u) >> (32 - ALN_HT_BITS); }
 
 // the slot of bin (found, or the empty slot where it goes): one 64-slot
 // window per round trip, the lanes probing in parallel
@@ -546,12 +549,22 @@ __device__ __forceinline__ int64_t shr64(int64_t v, int64_t first) {  // wave_sh
 //    computed ahead, so the "long overlapping seed disagrees" test
 //    (software/bwamem.c:1098-1109) is one ballot over the lanes above k and a
 //    made region is one store from lane k.
-// Longer chains take chain_full (and empty the ring).  A call, not inlined:
-// inlined into aln_heavy_kernel's persistent loop the walk hung gfx950 waves
-// (ROCm 7.2 compiler; the same code behind a call ran).
-template <int KC>
-__device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, int r) {
+// Longer chains take chain_full (and empty the ring).
+// GUARD (the inlined diagnostic instantiation, SMEM_ALN_WALK_INLINE=1): every
+// loop iteration of the walk counts against P.walk_guard; past it the wave
+// sets ctr[15] and leaves the read, so a walk that would spin ends instead of
+// hanging the GPU (the round-2 hang).
+#define WALK_GUARD()                                                          \
+    if constexpr (GUARD) {                                                    \
+        if (++guard > P.walk_guard) {                                         \
+            if (lane == 0) atomicAdd(&P.ctr[15], 1u);                         \
+            return;                                                           \
+        }                                                                     \
+    }
+template <int KC, bool GUARD>
+__device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) {
     const int lane = threadIdx.x & 63;
+    uint32_t guard = 0;
     const int L = uni((int)(P.offs[r + 1] - P.offs[r]));
     const uint8_t* query = P.codes + P.offs[r];
     const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
@@ -571,6 +584,7 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
         __threadfence_block();
     }
     for (uint64_t c = c0; c < c1; ++c) {
+        WALK_GUARD();
         OutChain ch = P.chains[c];
         const int n = uni(ch.n);
         if (n <= 0) continue;
@@ -598,6 +612,7 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
             if (hashed) {
                 __threadfence_block();
                 for (int i = before; i < nreg; ++i) {
+                    WALK_GUARD();
                     const int64_t rb = (int64_t)uni64((uint64_t)regs[i].rb), re = (int64_t)uni64((uint64_t)regs[i].re);
                     maxlen = re - rb > maxlen ? re - rb : maxlen;
                     ht_insert(ht, rnext, rb, i, lane);
@@ -610,7 +625,10 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
         if (lane < n) my = S[lane];
         const uint64_t key = lane < n ? ((uint64_t)(uint32_t)my.len << 32 | (uint32_t)lane) : ~0ull;
         int rank = 0;
-        for (int t = 0; t < n; ++t) rank += rl64(key, t) < key;
+        for (int t = 0; t < n; ++t) {
+            WALK_GUARD();
+            rank += rl64(key, t) < key;
+        }
         const int dst = (lane < n ? rank : lane) << 2;  // a permutation of the 64 lanes
         const int64_t s_rb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)my.rbeg) |
                                        (uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(my.rbeg >> 32)) << 32);
@@ -625,6 +643,7 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
         }
         bool skipped = false;
         for (int k = n - 1; k >= 0; --k) {
+            WALK_GUARD();
             const int64_t k_rb = (int64_t)rl64((uint64_t)s_rb, k);
             const int k_qb = kswd::rl(s_qb, k), k_len = kswd::rl(s_len, k);
             bool hit = __ballot(lane < rc && reg_contains(P, k_rb, k_qb, k_len, g_rb, g_re, g_qb, g_qe)) != 0;
@@ -634,10 +653,12 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
                 const uint64_t b1 = (uint64_t)k_rb >> HT_BIN;
                 const uint64_t b0 = (uint64_t)(k_rb - maxlen > 0 ? k_rb - maxlen : 0) >> HT_BIN;
                 for (uint64_t b = b0; b <= b1 && !hit; ++b) {
+                    WALK_GUARD();
                     uint64_t e;
                     (void)ht_find(ht, b, lane, e);
                     int i = e ? uni((int)(e & 0xFFFFF) - 1) : -1;
                     while (i >= 0 && !hit) {
+                        WALK_GUARD();
                         const AlnReg* p = regs + i;
                         hit = reg_contains(P, k_rb, k_qb, k_len, (int64_t)uni64((uint64_t)p->rb),
                                            (int64_t)uni64((uint64_t)p->re), uni(p->qb), uni(p->qe));
@@ -647,6 +668,7 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
             } else if (!hit && older > 0) {
                 __threadfence_block();
                 for (int ib = 0; ib < older && !hit; ib += 64) {
+                    WALK_GUARD();
                     const int i = older - 1 - ib - lane;
                     bool ok = false;
                     if (i >= 0) {
@@ -677,8 +699,14 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
                 a_qb = kswd::rl(mine.qb, k), a_qe = kswd::rl(mine.qe, k);
             } else {
                 __threadfence_block();
-                seed_region_call<KC>(P, query, L, S, n, kswd::rl(s_idx, k), P.span[2 * c], P.span[2 * c + 1],
-                                     regs + nreg);
+                if constexpr (GUARD) {  // inlined too
+                    const AlnReg a = seed_region<KC>(P, query, L, S, n, S[kswd::rl(s_idx, k)], P.span[2 * c],
+                                                     P.span[2 * c + 1], lane);
+                    if (lane == 0) regs[nreg] = a;
+                } else {
+                    seed_region_call<KC>(P, query, L, S, n, kswd::rl(s_idx, k), P.span[2 * c], P.span[2 * c + 1],
+                                         regs + nreg);
+                }
                 __threadfence_block();
                 a_rb = (int64_t)uni64((uint64_t)regs[nreg].rb), a_re = (int64_t)uni64((uint64_t)regs[nreg].re);
                 a_qb = uni(regs[nreg].qb), a_qe = uni(regs[nreg].qe);
@@ -695,9 +723,19 @@ __device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, in
     }
     if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
 }
+#undef WALK_GUARD
+
+// The product instantiation: the walk behind a call.  Round 2 saw gfx950
+// waves hang with the walk inlined into aln_heavy_kernel's persistent loop;
+// SMEM_ALN_WALK_INLINE=1 runs the inlined, guarded instantiation to test that
+// (DESIGN.md §5).
+template <int KC>
+__device__ __attribute__((noinline)) void heavy_read_walk(const AlnParams& P, int r) {
+    heavy_read_walk_body<KC, false>(P, r);
+}
 
 // one wave per heavy read at a time
-template <int KC>
+template <int KC, bool INL = false>
 __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
     const uint32_t nh = P.ctr[2];
     for (;;) {
@@ -706,7 +744,10 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
         h = (uint32_t)uni((int)h);
         if (h >= nh) break;
         const int r = uni(P.heavy[h]);
-        if ((uni((int)(P.offs[r + 1] - P.offs[r])) > 256) == (KC > 4)) heavy_read_walk<KC>(P, r);
+        if ((uni((int)(P.offs[r + 1] - P.offs[r])) > 256) == (KC > 4)) {
+            if constexpr (INL) heavy_read_walk_body<KC, true>(P, r);
+            else heavy_read_walk<KC>(P, r);
+        }
     }
 }
 
@@ -772,7 +813,15 @@ extern "C" hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStre
 extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
     hipLaunchKernelGGL(smem::aln_heavy_task_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
     if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_task_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
-    // the walk kernels use the per-wave hash tables in turn (same stream)
+    // the walk kernels use the per-wave hash tables in turn (same stream);
+    // walk_guard != 0: the inlined, guarded walk (diagnostic)
+    if (P->walk_guard) {
+        hipLaunchKernelGGL((smem::aln_heavy_kernel<4, true>), dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
+        if (long_reads)
+            hipLaunchKernelGGL((smem::aln_heavy_kernel<16, true>), dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0,
+                               st, *P);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
     if (long_reads)
         hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);

@@ -1339,6 +1339,19 @@ static uint32_t aln_heavy_seeds() {
 // and claim from different counters, so they can share the GPU: the light
 // kernel fills the CUs the walk's few long reads leave idle.  st2 == nullptr:
 // everything on st.
+// after a run_aln with the guarded walk: fail if any walk tripped its guard
+static int aln_guard_check(const smem::AlnParams& P, hipStream_t st) {
+    if (!P.walk_guard) return SMEM_OK;
+    uint32_t trips = 0;
+    HIP_TRY(hipMemcpyAsync(&trips, P.ctr + 15, sizeof(trips), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (trips) {
+        snprintf(g_err, sizeof(g_err), "chains -> regions: the inlined heavy-read walk tripped its guard %u times", trips);
+        return SMEM_E_INTERNAL;
+    }
+    return SMEM_OK;
+}
+
 static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_t n_seeds, bool long_reads,
                    AlnHeavyBufs& H, hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t ev_join = nullptr) {
     const int n = P.n_reads;
@@ -1349,6 +1362,10 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         P.hash_min = e ? (uint32_t)std::max(1, atoi(e)) : 64u;
         const char* l = getenv("SMEM_ALN_SPEC_LOCAL");
         P.spec_local = l ? (uint32_t)atoi(l) : 0u;
+        // SMEM_ALN_WALK_INLINE=1: the heavy-read walk inlined, every loop
+        // iteration counted against a guard (diagnostic of the round-2 hang)
+        const char* w = getenv("SMEM_ALN_WALK_INLINE");
+        P.walk_guard = (w && atoi(w) > 0) ? (atoi(w) > 1 ? (uint32_t)atoi(w) : (1u << 26)) : 0u;
     }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
@@ -1444,6 +1461,7 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->st,
                          aln_two_streams() ? b->st2 : nullptr, b->ev_join))
         return rc;
+    if (int rc = aln_guard_check(P, b->st)) return rc;
     tmp = b->d_sa_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_aln_nregs.p, b->d_aln_regoff.p, n, b->d_sa_tmp.p, &tmp, b->st));
     HIP_TRY(hipMemcpyAsync(b->h_tot.p + 5, b->d_aln_regoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
@@ -1590,6 +1608,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     P.srt = dsrt.p, P.raw = draw.p, P.n_regs = dnregs.p, P.ctr = dctr.p;
     HIP_TRY(hipEventRecord(ev[0], st));
     if (int rc = run_aln(g, P, n_chains, n_seeds, long_reads, heavy, st)) return rc;
+    if (int rc = aln_guard_check(P, st)) return rc;
     HIP_TRY(hipEventRecord(ev[1], st));
     std::vector<uint64_t> nr(n_reads);
     HIP_TRY(hipMemcpyAsync(nr.data(), dnregs.p, 8 * n_reads, hipMemcpyDeviceToHost, st));
