@@ -12,7 +12,8 @@
 #                     copied to profiles/traffic.json (or profiles/traffic_human.json with --genome-profile,human)
 #   bench[:ARGS]      python bench.py ARGS                           -> bench<k>.json / .err
 #   rocprof[:ARGS]    rocprofv3 --kernel-trace --stats over bench.py's timed seeding steps -> prof<k>/
-#   pmc[:PASSES]      tools/pmc_passes.sh (PMC_PASSES="0 1 ..."; PMC_PROG / PMC_KERNEL) -> pmc<k>/
+#   pmc:PASSES[:ARGS] tools/pmc_passes.sh, passes "1,2" of its list, ARGS for tools/prof_run.py (bench workload
+#                     args, --variant, --launches) -> pmc<k>/
 #   stamps[:ARGS]     tools/stamps.py (variant-9 cycle split)        -> stamps<k>.log
 #   aln[:ARGS] / chain[:ARGS]   tools/aln_prof.py / tools/chain_prof.py under rocprofv3 --kernel-trace --stats
 #   py:SCRIPT[:ARGS]  python SCRIPT ARGS                              -> py<k>.log
@@ -52,7 +53,10 @@ for step in "$@"; do
         python3 -u bench.py --stream-reads -1 --parity 0 --side-stages 0 --cpu-seconds 0 --e2e-reads 0 --human-like 0 \
         $args > "$OUT/prof$k.json" 2> "$OUT/prof$k.err" || { echo "rocprof failed"; exit $k; } ;;
     pmc)
-      PMC_PASSES="${args:-${PMC_PASSES:-}}" timeout -k 10 900 bash tools/pmc_passes.sh "$OUT/pmc$k" \
+      passes=${arg%%:*}
+      rest=""
+      [[ "$arg" == *:* ]] && rest=${arg#*:}
+      PMC_PASSES="${passes//,/ }" timeout -k 10 900 bash tools/pmc_passes.sh "$OUT/pmc$k" ${rest//,/ } \
         > "$OUT/pmc$k.log" 2>&1 || { echo "pmc failed"; exit $k; } ;;
     stamps)
       timeout -k 10 600 python -u tools/stamps.py $args > "$OUT/stamps$k.log" 2>&1 || { echo "stamps failed"; exit $k; } ;;
