@@ -340,12 +340,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
     g_err[0] = 0;
     if (!g || !(variant == 0 || (variant >= 2 && variant <= 25))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
-    if ((variant == 24 || variant == 25)) {
-        // the 32-bit extend needs every base count below 2^32
-        for (int c = 0; c < 4; ++c)
-            if (g->L2[c + 1] - g->L2[c] >= (1ull << 32))
-                return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: variants 24/25 need base counts < 2^32");
-    }
+
     if (!smem_seed_variant_built(variant))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: A/B variant not in this build (make AB=1)");
     if ((variant == 10 || variant == 22) && !g->d_occ192) {

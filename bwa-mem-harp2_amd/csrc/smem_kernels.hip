@@ -336,47 +336,6 @@ __device__ __forceinline__ void extend_counts64(const SeedParams& P, uint64_t a,
     nb = b + (uint64_t)(a <= P.primary && a + s - 1 >= P.primary) + gt;
 }
 
-// The same bwt_extend (child c only) with 32-bit arithmetic wherever the
-// values allow it and no branch on c.  When every base occurs fewer than 2^32
-// times in the BWT (the host checks L2; a human-size index: at most 1.9 G),
-// every interval size -- and so ns and the other coordinate's cumulative
-// difference -- is below 2^32, so both are exact as differences of the
-// counts' low 32-bit words (mod 2^32).  Only na = L2[c] + 1 + Occ(c, kk)
-// needs the 34-bit checkpoint.  The base selections are cndmask chains on
-// 32-bit words.
-__device__ __forceinline__ void extend_counts64_lean(const SeedParams& P, uint64_t a, uint64_t b, uint64_t s, int c,
-                                                     uint64_t kk, uint64_t ll, const Bucket32& vk, const Bucket32& vl,
-                                                     uint64_t& na, uint64_t& nb, uint64_t& ns) {
-    uint32_t Ck, Gk, Tk, Cl, Gl, Tl;
-    count_cgt4(vk.sym, (uint32_t)(kk & 63), Ck, Gk, Tk);
-    count_cgt4(vl.sym, (uint32_t)(ll & 63), Cl, Gl, Tl);
-    // low words of Occ(C | G | T, .) and Occ(A, .) = pos + 1 - C - G - T
-    const uint32_t kC = vk.cnt.x + Ck, kG = vk.cnt.y + Gk, kT = vk.cnt.z + Tk;
-    const uint32_t lC = vl.cnt.x + Cl, lG = vl.cnt.y + Gl, lT = vl.cnt.z + Tl;
-    const uint32_t kTG = kT + kG, lTG = lT + lG;
-    const uint32_t kA = (uint32_t)kk + 1u - kTG - kC, lA = (uint32_t)ll + 1u - lTG - lC;
-    const bool c0 = (c & 1) != 0, c1 = (c & 2) != 0;
-    const uint32_t ok = c1 ? (c0 ? kT : kG) : (c0 ? kC : kA);
-    const uint32_t ol = c1 ? (c0 ? lT : lG) : (c0 ? lC : lA);
-    // Occ of the bases after c (the other coordinate's cumulative count)
-    const uint32_t gk = c1 ? (c0 ? 0u : kT) : (c0 ? kTG : kTG + kC);
-    const uint32_t gl = c1 ? (c0 ? 0u : lT) : (c0 ? lTG : lTG + lC);
-    ns = (uint64_t)(ol - ok);
-    const uint32_t dollar = (a <= P.primary && a + s - 1 >= P.primary) ? 1u : 0u;
-    nb = b + (uint64_t)(gl - gk + dollar);
-    // na: Occ(c, kk) with its checkpoint's bits 32-33; for A, kk + 1 minus
-    // the 34-bit C + G + T
-    const uint32_t w = vk.cnt.w;
-    const uint64_t cgt = (uint64_t)vk.cnt.x + vk.cnt.y + vk.cnt.z + (Ck + Gk + Tk) +
-                         ((uint64_t)((w & 3u) + ((w >> 2) & 3u) + ((w >> 4) & 3u)) << 32);
-    const uint32_t sel_lo = c1 ? (c0 ? vk.cnt.z : vk.cnt.y) : vk.cnt.x;
-    const uint32_t sel_pf = c1 ? (c0 ? Tk : Gk) : Ck;
-    const uint32_t sel_hi = (w >> (2u * (uint32_t)(c > 0 ? c - 1 : 0))) & 3u;
-    const uint64_t occ = c == 0 ? kk + 1 - cgt : ((uint64_t)sel_hi << 32 | sel_lo) + sel_pf;
-    const uint64_t L2c = c1 ? (c0 ? P.L2[3] : P.L2[2]) : (c0 ? P.L2[1] : P.L2[0]);
-    na = L2c + 1 + occ;
-}
-
 // Fetch the Occ64 buckets of k and l (issue: DMAs, tags; read: after the
 // wave's vmcnt wait).  Each lane keeps the two buckets it
 // fetched last in two LDS slots (planes [2*slot + chunk][lane]) with their
@@ -521,7 +480,7 @@ __device__ __forceinline__ uint64_t stamp() {
 // its forward string (first kt_k bases) and, in the backward phase, of the
 // kt_k bases from the current position (rolled one base per step).
 template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
-          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool LEAN = false>
+          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool PFCH = false>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -551,6 +510,19 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     int item = -1, len = 0;
     int nitem = 0, nlen = -2;  // next read: -2 nothing claimed, -1 claimed, >= 0 offsets loaded
     int rid = 0, nrid = 0;     // read index of the item (overflow pass: through read_ids)
+    // PFCH: the next read's claim and loads are issued in the uniform section
+    // beside the bucket loads and consumed at the top of the next iteration,
+    // so no wave ever waits on them (the blocking claim at the top stalled
+    // the whole wave for two memory round trips in ~12 % of iterations,
+    // profiles/r03/stamps): nst walks NST_CLAIM -> NST_CLAIMING -> (overflow
+    // pass: NST_RID -> NST_RIDING) -> NST_OFF -> NST_OFFING -> NST_READY, and
+    // a lane takes its next read the iteration after it finished one.
+    enum { NST_CLAIM = 0, NST_CLAIMING, NST_RID, NST_RIDING, NST_OFF, NST_OFFING, NST_READY };
+    int nst = NST_CLAIM;
+    int natom = 0, nrank = 0;      // the wave's claim (leader lane's atomic return), this lane's rank in it
+    int nridv = 0;                 // overflow pass: read_ids[nitem] in flight
+    uint32_t clead = 0;            // the claim's leader lane (wave-uniform)
+    uint4 noffv = {0, 0, 0, 0};    // offs[rid], offs[rid + 1] in flight
     uint32_t keep_n = 0;       // intervals of the read that smem_next2 returns (matches + kept sub-matches)
     uint32_t o0 = 0, no0 = 0;
     uint32_t qb = ~0u, qwant = ~0u;      // 16-B query window held / wanted (offsets into codes)
@@ -626,7 +598,22 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         if constexpr (STAMP) ta = stamp();
         // claiming the next read and loading its offsets: here, at the top of the
         // iteration, where no bucket DMA is in flight yet for their waits to cover
-        if (phase == P_FETCH) {
+        if constexpr (PFCH) {
+            // what the last iteration's uniform section issued has landed
+            // (its vmcnt(0) wait): consume it, issue nothing here
+            if (nst == NST_CLAIMING) {
+                nitem = __builtin_amdgcn_readlane(natom, clead) + nrank;
+                nst = nitem >= P.n_items ? NST_READY : (P.read_ids ? NST_RID : NST_OFF);
+                nrid = nitem;
+            } else if (nst == NST_RIDING) {
+                nrid = nridv;
+                nst = NST_OFF;
+            } else if (nst == NST_OFFING) {
+                no0 = noffv.x;
+                nlen = (int)(noffv.z - noffv.x);
+                nst = NST_READY;
+            }
+        } else if (phase == P_FETCH) {
             if (nlen == -2) {  // claim the next read
                 nitem = atomicAdd(P.head, 1);
                 nlen = -1;
@@ -698,7 +685,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             if (phase == P_FETCH) {
                 // claiming the next read and loading its offsets happen in the
                 // uniform section; yield until both are done
-                if (nlen < 0) {
+                if (PFCH ? nst != NST_READY : nlen < 0) {
                     out = true;
                 } else if (nitem >= P.n_items) {
                     phase = P_EXIT;
@@ -710,6 +697,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     o0 = no0;
                     len = nlen;
                     nlen = -2;
+                    nst = NST_CLAIM;  // PFCH: the next claim goes out in this iteration's uniform section
                     raw_n = 0;
                     calls_n = 0;
                     start = 0;
@@ -1053,6 +1041,40 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                 }
             }
         }
+        if constexpr (PFCH) {
+            // the next read's claim / loads, waited for by this iteration's
+            // vmcnt(0) below and consumed at the top of the next one
+            if (nst == NST_RID) {
+                nridv = P.read_ids[nitem];
+                nst = NST_RIDING;
+            } else if (nst == NST_OFF) {
+                const uint2* op = reinterpret_cast<const uint2*>(P.offs + nrid);
+                const uint2 a = op[0], b = op[1];   // batches hold < 2^32 bases: the low words
+                noffv = make_uint4(a.x, a.y, b.x, b.y);
+                nst = NST_OFFING;
+            }
+            const uint64_t want_claim = __ballot(nst == NST_CLAIM && phase != P_EXIT);
+            if (want_claim) {
+                const int me = vlane();
+                clead = (uint32_t)(__builtin_ffsll((long long)want_claim) - 1);
+                if (nst == NST_CLAIM && phase != P_EXIT) {
+                    nrank = (int)__popcll(want_claim & ((1ull << me) - 1));
+                    if ((uint32_t)me == clead) {
+                        // the returning atomic by hand: the compiler's form
+                        // (the atomic optimizer's readfirstlane of the result)
+                        // waits for it right here.  The value is read at the top
+                        // of the next iteration, after this iteration's
+                        // s_waitcnt vmcnt(0) below has drained it.
+                        const int cnt = (int)__popcll(want_claim);
+                        asm volatile("global_atomic_add %0, %1, %2, off sc0"
+                                     : "=v"(natom)
+                                     : "v"(P.head), "v"(cnt)
+                                     : "memory");
+                    }
+                    nst = NST_CLAIMING;
+                }
+            }
+        }
         // prev[j+1] (the owner of a helped batch: prev[j+1+bat_m]) and the query
         // window land in LDS slots (no VGPR-destination load the compiler would
         // wait on right away); read back after the wait
@@ -1186,9 +1208,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             nb = fwd ? p_x0(ktv) : p_x1(ktv);
             ns = p_x2(ktv);
         } else if (want) {
-            if constexpr (FETCH == FETCH_OCC64 && LEAN && !L192)
-                extend_counts64_lean(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
-            else if constexpr (FETCH == FETCH_OCC64)
+            if constexpr (FETCH == FETCH_OCC64)
                 extend_counts64<L192>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
             else
                 extend_counts(P, ra, rb, rs, rc, kk, ll, vk, vl, na, nb, ns);
@@ -1315,8 +1335,7 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         // 23: the default with the k-mer table (P->kt)
         case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        // 24: the default with the 32-bit extend (extend_counts64_lean; base counts < 2^32, checked on the host);
-        // 25: its stamped twin
+        // 24: the default with the next read claimed and loaded in the uniform section (PFCH); 25: its stamped twin
         case 24: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 25: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS

@@ -23,7 +23,7 @@ def main():
     production variant timed beside the stamped one, --out a JSON file."""
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--compare", type=int, default=2, help="production variant timed beside the stamped one")
-    p.add_argument("--stamped", type=int, default=9, help="the stamped variant (9: default kernel, 25: lean extend)")
+    p.add_argument("--stamped", type=int, default=9, help="the stamped variant (9: default kernel, 25: the PFCH variant 24)")
     p.add_argument("--out", default=None)
     own, rest = p.parse_known_args()
     import bench
