@@ -118,7 +118,7 @@ def parse(argv=None):
     p.add_argument("--parity", type=int, default=1,
                    help="1: seed the stats sample on the GPU too and compare (0: every seed_kernel launch is a "
                         "full resident batch, for rocprofv3 summaries)")
-    p.add_argument("--e2e-reads", type=int, default=200_000,
+    p.add_argument("--e2e-reads", type=int, default=1_000_000,
                    help="reads of the end-to-end leg (bwa-gpu mem vs the reference pipeline; 0: skip; N=1 only)")
     p.add_argument("--e2e-batch", type=int, default=0, help="-b of bwa-gpu mem (0: reads / threads)")
     p.add_argument("--human-like", type=int, default=1,
@@ -664,6 +664,7 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
             n_proc, real = _mem_times(err)
             digest, n_lines = _sam_body(sam)
             runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
+                          "outside_mem_process_seqs_s": round(wall - real, 3),
                           "reads_per_s_wall": round(m / wall, 1),
                           "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
                           "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,

@@ -254,6 +254,18 @@ def write_fastq(path: str, reads: "Reads", prefix: str = "r", qual: int = 40) ->
     """Reads (codes 0..4) as FASTQ, named <prefix><index>."""
     acgtn = np.frombuffer(b"ACGTN", dtype=np.uint8)
     q = chr(33 + qual)
+    if reads.n and np.all(reads.lens == reads.lens[0]) and reads.lens[0] > 0:
+        # fixed-length reads: the sequence lines in one array operation
+        L = int(reads.lens[0])
+        o = int(reads.offs[0])
+        seqs = acgtn[np.minimum(reads.codes[o:o + reads.n * L], 4)].reshape(reads.n, L)
+        qline = b"\n+\n" + (q * L).encode() + b"\n"
+        with open(path, "wb") as fh:
+            for i0 in range(0, reads.n, 65536):
+                blk = seqs[i0:i0 + 65536]
+                fh.write(b"".join(b"@%s%d\n%s%s" % (prefix.encode(), i0 + k, row.tobytes(), qline)
+                                  for k, row in enumerate(blk)))
+        return
     with open(path, "wb") as fh:
         for i in range(reads.n):
             s = acgtn[np.minimum(reads.read(i), 4)].tobytes()
