@@ -451,6 +451,7 @@ __device__ __forceinline__ void heavy_chain_task(const AlnParams& P, uint32_t nh
             chain_full<KC, CM_RECORD>(P, query, L, S, ch.n, P.srt + ch.seed_off, P.loc + ch.seed_off, nl, lane,
                                       P.pre + ch.seed_off, P.pre_ok + ch.seed_off);
         } else if (!ok) {  // every seed's region: the read's walk decides which of them are made
+            if (lane == 0) atomicAdd(&P.ctr[8], (uint32_t)ch.n);  // regions computed ahead (SMEM_ALN_STATS)
             for (int i = 0; i < ch.n; ++i) {
                 const AlnReg a = seed_region<KC>(P, query, L, S, ch.n, S[i], r0, r1, lane);
                 if (lane == 0) P.pre[ch.seed_off + i] = a;
@@ -579,6 +580,7 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
     uint64_t* ht = P.ht + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * ALN_HT;
     int32_t* rnext = P.rnext + P.seed_off[r];
     int64_t maxlen = 0;  // the longest region so far
+    uint32_t n_used = 0, n_serial = 0;  // regions taken from the chain tasks / computed here (SMEM_ALN_STATS)
     if (hashed) {
         for (int i = lane; i < ALN_HT; i += 64) ht[i] = 0;
         __threadfence_block();
@@ -694,10 +696,12 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             int64_t a_rb, a_re;
             int a_qb, a_qe;
             if (kswd::rl(mine_ok, k)) {
+                ++n_used;
                 if (lane == k) regs[nreg] = mine;
                 a_rb = (int64_t)rl64((uint64_t)mine.rb, k), a_re = (int64_t)rl64((uint64_t)mine.re, k);
                 a_qb = kswd::rl(mine.qb, k), a_qe = kswd::rl(mine.qe, k);
             } else {
+                ++n_serial;
                 __threadfence_block();
                 if constexpr (GUARD) {  // inlined too
                     const AlnReg a = seed_region<KC>(P, query, L, S, n, S[kswd::rl(s_idx, k)], P.span[2 * c],
@@ -721,7 +725,11 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             ++nreg;
         }
     }
-    if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
+    if (lane == 0) {
+        P.n_regs[r] = (uint64_t)nreg;
+        if (n_used) atomicAdd(&P.ctr[9], n_used);
+        if (n_serial) atomicAdd(&P.ctr[10], n_serial);
+    }
 }
 #undef WALK_GUARD
 

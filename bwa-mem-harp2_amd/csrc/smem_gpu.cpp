@@ -1334,8 +1334,17 @@ static uint32_t aln_heavy_seeds() {
 // and claim from different counters, so they can share the GPU: the light
 // kernel fills the CUs the walk's few long reads leave idle.  st2 == nullptr:
 // everything on st.
-// after a run_aln with the guarded walk: fail if any walk tripped its guard
+// after a run_aln with the guarded walk: fail if any walk tripped its guard.
+// SMEM_ALN_STATS: print the heavy path's counters (regions the chain tasks
+// computed ahead, the walk's regions taken from them / computed serially)
 static int aln_guard_check(const smem::AlnParams& P, hipStream_t st) {
+    if (getenv("SMEM_ALN_STATS")) {
+        uint32_t c[3] = {0, 0, 0};
+        HIP_TRY(hipMemcpyAsync(c, P.ctr + 8, sizeof(c), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "[smem aln] heavy path: %u seed regions computed ahead, %u used by the walks, %u computed "
+                        "serially in the walks\n", c[0], c[1], c[2]);
+    }
     if (!P.walk_guard) return SMEM_OK;
     uint32_t trips = 0;
     HIP_TRY(hipMemcpyAsync(&trips, P.ctr + 15, sizeof(trips), hipMemcpyDeviceToHost, st));
