@@ -279,16 +279,32 @@ static int cmp_u64(const void *a, const void *b)
 	return x < y ? -1 : x > y;
 }
 
+/* shape statistics of the extensions chain2aln makes, per thread (test
+ * infrastructure: how the DP work of the alignment stage is distributed):
+ * [b][0] calls, [b][1] in-band cells, by qlen bucket b = 0: <= 16, 1: <= 32,
+ * 2: <= 64, 3: <= 128, 4: <= 256, 5: longer */
+__thread uint64_t orc_ext_shape[6][2];
+
+void orc_ext_shapes(uint64_t out[12], int reset)
+{
+	memcpy(out, orc_ext_shape, sizeof(orc_ext_shape));
+	if (reset) memset(orc_ext_shape, 0, sizeof(orc_ext_shape));
+}
+
 static int extend(const orc_aln_opt_t *o, int qlen, const uint8_t *q, int tlen, const uint8_t *t, int w,
 		int end_bonus, int h0, orc_ksw_result_t *res)
 {
+	int b = qlen <= 16 ? 0 : qlen <= 32 ? 1 : qlen <= 64 ? 2 : qlen <= 128 ? 3 : qlen <= 256 ? 4 : 5, r;
+	uint64_t c0 = orc_cells_ext;
 	orc_ksw_task_t T;
 	orc_ksw_opt_t ko;
 	memset(&T, 0, sizeof(T));
 	T.qlen = qlen, T.tlen = tlen, T.w = w, T.end_bonus = end_bonus, T.zdrop = o->zdrop, T.h0 = h0;
 	memcpy(ko.mat, o->mat, 25);
 	ko.o_del = o->o_del, ko.e_del = o->e_del, ko.o_ins = o->o_ins, ko.e_ins = o->e_ins;
-	return orc_ksw_extend(&T, q, t, &ko, res);
+	r = orc_ksw_extend(&T, q, t, &ko, res);
+	orc_ext_shape[b][0] += 1, orc_ext_shape[b][1] += orc_cells_ext - c0;
+	return r;
 }
 
 /* mem_chain2aln (software/bwamem.c:1040-1188) */

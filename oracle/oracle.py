@@ -98,6 +98,8 @@ def load() -> C.CDLL:
         lib.orc_aln_batch.restype = C.c_int
         lib.orc_cells.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         lib.orc_cells.restype = None
+        lib.orc_ext_shapes.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+        lib.orc_ext_shapes.restype = None
         lib.orc_ksw_align2.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                        C.c_int, C.c_int, C.POINTER(C.c_int32)]
         lib.orc_ksw_align2.restype = None
@@ -408,6 +410,14 @@ def dp_cells(reset: bool = True) -> tuple:
     out = (C.c_uint64 * 2)()
     load().orc_cells(out, 1 if reset else 0)
     return int(out[0]), int(out[1])
+
+
+def ext_shapes(reset: bool = True) -> list:
+    """[(calls, in-band cells)] of the restatement's chain2aln extensions by
+    qlen bucket (<= 16, 32, 64, 128, 256, longer) on this thread."""
+    out = (C.c_uint64 * 12)()
+    load().orc_ext_shapes(out, 1 if reset else 0)
+    return [(int(out[2 * b]), int(out[2 * b + 1])) for b in range(6)]
 
 
 def aln(pac, l_pac: int, codes, offs, chains, chain_off, seeds, opt: AlnOptT):

@@ -143,6 +143,9 @@ int orc_ksw_extend(const orc_ksw_task_t *t, const uint8_t *query, const uint8_t 
  * ksw_extend2 (the columns [lo, hi) of every row), out[1] query x target cells
  * of every ksw_align2 pass */
 void orc_cells(uint64_t out[2], int reset);
+/* chain2aln's extensions by qlen bucket (<= 16, 32, 64, 128, 256, longer):
+ * out[2 b] calls, out[2 b + 1] in-band cells */
+void orc_ext_shapes(uint64_t out[12], int reset);
 int orc_ksw_batch(int64_t n, const orc_ksw_task_t *tasks, const uint8_t *q, const uint8_t *t, const orc_ksw_opt_t *o,
 		orc_ksw_result_t *out);
 
