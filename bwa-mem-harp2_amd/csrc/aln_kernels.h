@@ -18,6 +18,7 @@ struct AlnReg {
 static_assert(sizeof(AlnReg) == 64, "mem_alnreg_t layout");
 
 constexpr int ALN_CTRS = 16;
+constexpr int ALN_SPLITS = 16;     // SMEM_ALN_SPLIT accumulators (aln_kernel's phases and counts)
 constexpr int ALN_HT = 65536;       // hash slots per walk wave
 constexpr int ALN_WALK_WAVES = 4;   // walk waves per CU (aln_heavy_kernel blocks of 256)
 
@@ -45,6 +46,7 @@ struct AlnParams {
     uint64_t* n_regs;  // [n_reads]
     uint32_t* ctr;     // [ALN_CTRS]: work-queue heads (reads <= 256 bp, longer), heavy-read count, heavy-path heads
     uint64_t* cyc;     // diagnostics (SMEM_ALN_CYCLES): [n_reads] shader cycles per read, nullptr: off
+    uint64_t* split;   // diagnostics (SMEM_ALN_SPLIT): [ALN_SPLITS] aln_kernel's cycles by phase and counts, nullptr: off
     // heavy reads (at least heavy_min chains or heavy_seeds seeds; 0 = none):
     // every chain walked ahead on its own, one wave per chain, then the read's
     // walk replays them (aln_heavy_kernel)

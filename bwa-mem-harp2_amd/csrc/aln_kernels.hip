@@ -78,6 +78,28 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32;
 }
 
+// Diagnostics (SMEM_ALN_SPLIT, aln_kernel<KC, true>): shader cycles of each
+// phase of a read summed per wave, and counts.  t[k]:
+//   0 read setup, 1 chain load + mem_chain2aln_short, 2 chain span + seed
+//   order, 3 containment tests, 4 left extensions, 5 right extensions,
+//   6 seed coverage + region store, 7 claims;
+//   8 reads, 9 chains, 10 short regions, 11 seed regions, 12 left / 13 right
+//   extension calls, 14 extension rows walked, 15 waves.
+struct Split {
+    uint64_t last;
+    uint64_t t[ALN_SPLITS];
+};
+__device__ __forceinline__ void stamp(Split* sp, int k) {
+    if (sp) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        sp->t[k] += t - sp->last;
+        sp->last = t;
+    }
+}
+__device__ __forceinline__ void count(Split* sp, int k) {
+    if (sp) ++sp->t[k];
+}
+
 // mem_chain2aln_short (software/bwamem.c:805-852): 0 when it wrote region
 // *out, 1 when it declines (then mem_chain2aln runs).  One exit: the
 // declines are flags, not early returns (an early return out of this wave-
@@ -230,7 +252,7 @@ __device__ __forceinline__ bool seed_wanted(const AlnParams& P, const SeedRec* S
 // the regions made before -- so heavy reads compute it ahead, in parallel.
 template <int KC>
 __device__ __forceinline__ AlnReg seed_region(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n, const SeedRec& s,
-                              int64_t r0, int64_t r1, int lane) {
+                              int64_t r0, int64_t r1, int lane, Split* sp = nullptr) {
     int aw0 = P.w, aw1 = P.w, score = -1, truesc = -1, aqb, aqe;
     int64_t arb, are;
     if (s.qbeg) {  // left: the reversed query against the reversed reference
@@ -239,10 +261,11 @@ __device__ __forceinline__ AlnReg seed_region(const AlnParams& P, const uint8_t*
         for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY
             const int prev = score;
             aw0 = P.w << t;
+            count(sp, 12);
             x = kswd::extend_wave<KC>(
                 kswd::ExtIn{s.qbeg, (int)tmp, aw0, P.pen_clip5, P.zdrop, s.len * P.a},
                 [&](int j) { return (int)query[s.qbeg - 1 - j]; }, [&](int i) { return ref_at(P, s.rbeg - 1 - i); },
-                P.mat, P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
+                P.mat, P.o_del, P.e_del, P.o_ins, P.e_ins, P.top, sp ? &sp->t[14] : nullptr);
             score = x.score;
             if (score == prev || x.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
         }
@@ -257,6 +280,7 @@ __device__ __forceinline__ AlnReg seed_region(const AlnParams& P, const uint8_t*
         score = truesc = s.len * P.a;
         aqb = 0, arb = s.rbeg;
     }
+    stamp(sp, 4);
     if (s.qbeg + s.len != L) {  // right
         const int qe = s.qbeg + s.len, sc0 = score;
         const int64_t rs = s.rbeg + s.len;
@@ -264,10 +288,11 @@ __device__ __forceinline__ AlnReg seed_region(const AlnParams& P, const uint8_t*
         for (int t = 0; t < 2; ++t) {
             const int prev = score;
             aw1 = P.w << t;
+            count(sp, 13);
             x = kswd::extend_wave<KC>(kswd::ExtIn{L - qe, (int)(r1 - rs), aw1, P.pen_clip3, P.zdrop, sc0},
                                       [&](int j) { return (int)query[qe + j]; },
                                       [&](int i) { return ref_at(P, rs + i); }, P.mat, P.o_del, P.e_del, P.o_ins,
-                                      P.e_ins, P.top);
+                                      P.e_ins, P.top, sp ? &sp->t[14] : nullptr);
             score = x.score;
             if (score == prev || x.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
         }
@@ -281,6 +306,7 @@ __device__ __forceinline__ AlnReg seed_region(const AlnParams& P, const uint8_t*
     } else {
         aqe = L, are = s.rbeg + s.len;
     }
+    stamp(sp, 5);
     int cov = 0;  // seeds inside the region (software/bwamem.c:1180-1184)
     for (int i = lane; i < n; i += 64) {
         const SeedRec t = S[i];
@@ -313,14 +339,18 @@ enum ChainMode { CM_PLAIN = 0, CM_RECORD = 1, CM_REPLAY = 2 };
 template <int KC, int MODE = CM_PLAIN>
 __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n,
                                            uint64_t* srt, AlnReg* regs, int& nreg, int lane, AlnReg* pre = nullptr,
-                                           uint8_t* pre_ok = nullptr, int64_t r0 = 0, int64_t r1 = 0) {
+                                           uint8_t* pre_ok = nullptr, int64_t r0 = 0, int64_t r1 = 0,
+                                           Split* sp = nullptr) {
     n = uni(n);
     if constexpr (MODE != CM_REPLAY) chain_span(P, L, S, n, lane, r0, r1);
     chain_order(S, n, srt, lane);
+    stamp(sp, 2);
     for (int k = n - 1; k >= 0; --k) {
         const uint32_t si = (uint32_t)srt[k];
         const SeedRec s = S[si];
-        if (seed_wanted(P, S, n, srt, k, s, regs, nreg, lane)) {
+        const bool want = seed_wanted(P, S, n, srt, k, s, regs, nreg, lane);
+        stamp(sp, 3);
+        if (want) {
             if constexpr (MODE == CM_REPLAY) {
                 if (uni((int)pre_ok[si])) {
                     if (lane == 0) regs[nreg] = pre[si];
@@ -328,7 +358,8 @@ __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* qu
                     seed_region_call<KC>(P, query, L, S, n, (int)si, r0, r1, regs + nreg);
                 }
             } else {
-                const AlnReg a = seed_region<KC>(P, query, L, S, n, s, r0, r1, lane);
+                count(sp, 11);
+                const AlnReg a = seed_region<KC>(P, query, L, S, n, s, r0, r1, lane, sp);
                 if (lane == 0) {
                     regs[nreg] = a;
                     if constexpr (MODE == CM_RECORD) {
@@ -339,15 +370,20 @@ __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* qu
             }
             ++nreg;
             __threadfence_block();
+            stamp(sp, 6);
         }
     }
 }
 
 // KC = 4 at 4 waves per SIMD (128 VGPRs, 2 spilled): 3 waves at its free
-// allocation (136)
-template <int KC>
+// allocation (136).  SPLIT: the diagnostic instantiation (Split).
+template <int KC, bool SPLIT = false>
 __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
     const int lane = threadIdx.x & 63;
+    Split spl{};
+    Split* sp = SPLIT ? &spl : nullptr;
+    if constexpr (SPLIT) spl.last = __builtin_amdgcn_s_memtime();
+    count(sp, 15);
     constexpr uint32_t CLAIM = 4;  // reads per work-queue claim
     // light_claims > 0: the wave leaves after that many claims (the grid then
     // covers every read), so blocks retire while kernels of another stream wait
@@ -356,6 +392,7 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
         uint32_t r0 = 0;
         if (lane == 0) r0 = atomicAdd(&P.ctr[KC > 4 ? 1 : 0], CLAIM);
         r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0);
+        stamp(sp, 7);
         if (r0 >= (uint32_t)P.n_reads) break;
         const uint32_t r1 = r0 + CLAIM < (uint32_t)P.n_reads ? r0 + CLAIM : (uint32_t)P.n_reads;
         for (uint32_t r = r0; r < r1; ++r) {
@@ -369,21 +406,34 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
                 continue;  // aln_heavy_kernel's read
             AlnReg* regs = P.raw + P.seed_off[r];
             int nreg = 0;
+            count(sp, 8);
+            stamp(sp, 0);
             for (uint64_t c = c0; c < c1; ++c) {
                 OutChain ch = P.chains[c];
                 ch.n = uni(ch.n);
                 if (ch.n <= 0) continue;  // mem_chain2aln_short returns -1, nothing is made
+                count(sp, 9);
                 const SeedRec* S = P.seeds + ch.seed_off;
-                if (chain_short(P, query, L, S, ch.n, regs + nreg, lane) == 0) {
+                const int declined = chain_short(P, query, L, S, ch.n, regs + nreg, lane);
+                stamp(sp, 1);
+                if (declined == 0) {
+                    count(sp, 10);
                     ++nreg;
                     __threadfence_block();
                 } else {
-                    chain_full<KC>(P, query, L, S, ch.n, P.srt + ch.seed_off, regs, nreg, lane);
+                    chain_full<KC>(P, query, L, S, ch.n, P.srt + ch.seed_off, regs, nreg, lane, nullptr, nullptr, 0,
+                                   0, sp);
                 }
             }
             if (lane == 0) P.n_regs[r] = (uint64_t)nreg;
+            stamp(sp, 0);
             if (P.cyc && lane == 0) P.cyc[r] = __builtin_amdgcn_s_memtime() - t_read;
         }
+    }
+    if constexpr (SPLIT) {
+        if (lane == 0)
+            for (int k = 0; k < ALN_SPLITS; ++k)
+                atomicAdd(reinterpret_cast<unsigned long long*>(P.split + k), (unsigned long long)spl.t[k]);
     }
 }
 
@@ -805,10 +855,12 @@ extern "C" hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int lo
         const uint64_t per_block = 4ull * 4 * P->light_claims;  // 4 waves x 4 reads per claim
         blocks = blocks16 = (int)std::max<uint64_t>(1, (P->n_reads + per_block - 1) / per_block);
     }
-    hipLaunchKernelGGL(smem::aln_kernel<4>, dim3(blocks), dim3(256), 0, st, *P);
+    if (P->split) hipLaunchKernelGGL((smem::aln_kernel<4, true>), dim3(blocks), dim3(256), 0, st, *P);
+    else hipLaunchKernelGGL(smem::aln_kernel<4>, dim3(blocks), dim3(256), 0, st, *P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !long_reads) return e;
-    hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(blocks16), dim3(256), 0, st, *P);
+    if (P->split) hipLaunchKernelGGL((smem::aln_kernel<16, true>), dim3(blocks16), dim3(256), 0, st, *P);
+    else hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(blocks16), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

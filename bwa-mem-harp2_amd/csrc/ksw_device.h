@@ -73,7 +73,7 @@ struct ExtIn {
 // entry, at least 0 (software/ksw.c:398-400).
 template <int KC, class QF, class TF>
 __device__ __forceinline__ KswResult extend_wave(const ExtIn& T, QF qsym, TF tsym, const int8_t* mat, int o_del,
-                                                 int e_del, int o_ins, int e_ins, int top) {
+                                                 int e_del, int o_ins, int e_ins, int top, uint64_t* nrows = nullptr) {
     constexpr int JB = KC <= 4 ? 8 : 10;  // column bits of the (score, column) keys
     const int lane = threadIdx.x & 63;
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
@@ -112,6 +112,7 @@ __device__ __forceinline__ KswResult extend_wave(const ExtIn& T, QF qsym, TF tsy
     int beg = 0, end = qlen;
     int tcache = 0;
     for (int i = 0; i < tlen; ++i) {
+        if (nrows) ++*nrows;  // diagnostics (rows the wave walked)
         if ((i & 63) == 0) tcache = i + lane < tlen ? (int)tsym(i + lane) : 0;
         const int tc = rl(tcache, i & 63);
         int h1 = h0 - (o_del + e_del * (i + 1));

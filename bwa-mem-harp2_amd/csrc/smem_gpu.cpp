@@ -1454,6 +1454,15 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
         HIP_TRY(d_cyc.ensure(std::max(n, 1)));
         P.cyc = d_cyc.p;
     }
+    // SMEM_ALN_SPLIT=1: aln_kernel's cycles by phase and its counts (smem::Split), on stderr
+    const bool split = getenv("SMEM_ALN_SPLIT") && atoi(getenv("SMEM_ALN_SPLIT"));
+    DevBuf<uint64_t> d_split;
+    Free free_split{d_split};
+    if (split) {
+        HIP_TRY(d_split.ensure(smem::ALN_SPLITS));
+        HIP_TRY(hipMemsetAsync(d_split.p, 0, smem::ALN_SPLITS * sizeof(uint64_t), b->st));
+        P.split = d_split.p;
+    }
     HIP_TRY(hipMemsetAsync(b->d_aln_ctr.p, 0, smem::ALN_CTRS * sizeof(uint32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
     if (aln_two_streams() && !b->st2) {
@@ -1488,6 +1497,13 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
             fwrite(h.data(), sizeof(uint64_t), n, f);
             fclose(f);
         }
+    }
+    if (split) {
+        uint64_t h[smem::ALN_SPLITS];
+        HIP_TRY(hipMemcpy(h, d_split.p, sizeof(h), hipMemcpyDeviceToHost));
+        fprintf(stderr, "aln split:");
+        for (int k = 0; k < smem::ALN_SPLITS; ++k) fprintf(stderr, " %llu", (unsigned long long)h[k]);
+        fprintf(stderr, "\n");
     }
     b->aln_ran = true;
     b->aln_fetched = false;

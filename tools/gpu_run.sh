@@ -17,6 +17,7 @@
 #   stamps[:ARGS]     tools/stamps.py (variant-9 cycle split)        -> stamps<k>.log
 #   aln[:ARGS] / chain[:ARGS]   tools/aln_prof.py / tools/chain_prof.py under rocprofv3 --kernel-trace --stats
 #   py:SCRIPT[:ARGS]  python SCRIPT ARGS                              -> py<k>.log
+#   env:VAR=v[,VAR=v] exported for the steps after it (e.g. env:PMC_PROG=tools/aln_prof.py,PMC_KERNEL=aln_kernel)
 # Replaces round 2's one-off tools/gpu_r02*.sh scripts (their outputs are under profiles/r02/).
 set -o pipefail
 OUT=gpurun_out/${1:?usage: gpu_run.sh <out> <step>...}
@@ -63,6 +64,8 @@ for step in "$@"; do
     aln|chain)
       timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name$k" -o run -- \
         python3 -u tools/${name}_prof.py $args > "$OUT/$name$k.log" 2>&1 || { echo "$name failed"; exit $k; } ;;
+    env)
+      export $args ;;
     py)
       script=${arg%%:*}
       rest=""
