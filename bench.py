@@ -500,13 +500,16 @@ def aln_report(gpu, batch, opt, l_pac: int, pac=None, reads=None, reps: int = 3,
         aopt = oracle.aln_opt(min_seed_len=opt.min_seed_len)
         oracle.dp_cells(True)
         oracle.ext_shapes(True)
+        oracle.seed_uses(True)
         oracle.aln(pac, l_pac, reads.codes, reads.offs[:m + 1], res.chains, res.chain_off[:m + 1], res.seeds, aopt)
         ext, sw = oracle.dp_cells(True)
         shapes = oracle.ext_shapes(True)
+        uses = oracle.seed_uses(True)
         cells = {"ksw_extend2_in_band": ext, "ksw_align2": sw, "sample_reads": m,
                  "per_read": round((ext + sw) / max(m, 1), 1),
                  "extensions_by_qlen": {lab: {"calls": c, "cells": x} for lab, (c, x) in
-                                        zip(("<=16", "<=32", "<=64", "<=128", "<=256", ">256"), shapes)}}
+                                        zip(("<=16", "<=32", "<=64", "<=128", "<=256", ">256"), shapes)},
+                 "seed_regions": uses}
     out = {"ms_per_batch": round(best["aln_ms"], 3), "regions": int(best["n_regs"]), "chains": int(best["n_chains"]),
            "reads_per_s": round(n / (best["aln_ms"] * 1e-3), 1)}
     if cells:

@@ -291,6 +291,19 @@ void orc_ext_shapes(uint64_t out[12], int reset)
 	if (reset) memset(orc_ext_shape, 0, sizeof(orc_ext_shape));
 }
 
+/* which seeds chain2aln extends, per thread (test infrastructure: how much
+ * work a region computed ahead per chain would save): [0] seeds extended that
+ * are their chain's first in the order (the longest), [1] other seeds
+ * extended, [2] first seeds not extended (contained in an earlier chain's
+ * region), [3] seeds of the chains chain2aln runs on */
+__thread uint64_t orc_seed_use[4];
+
+void orc_seed_uses(uint64_t out[4], int reset)
+{
+	memcpy(out, orc_seed_use, sizeof(orc_seed_use));
+	if (reset) memset(orc_seed_use, 0, sizeof(orc_seed_use));
+}
+
 static int extend(const orc_aln_opt_t *o, int qlen, const uint8_t *q, int tlen, const uint8_t *t, int w,
 		int end_bonus, int h0, orc_ksw_result_t *res)
 {
@@ -335,6 +348,7 @@ static void chain2aln(const orc_aln_opt_t *o, int64_t l_pac, const uint8_t *pac,
 	for (i = 0; i < n; ++i) srt[i] = (uint64_t)sd[i].len << 32 | i;
 	qsort(srt, n, 8, cmp_u64);  /* keys are distinct: any sort gives ks_introsort_64's order */
 	qs = malloc(l_query + 1);
+	orc_seed_use[3] += n;
 	rs = malloc(rlen + 1);
 	for (k = n - 1; k >= 0; --k) {
 		const orc_seed_t *s = &sd[(uint32_t)srt[k]];
@@ -367,9 +381,11 @@ static void chain2aln(const orc_aln_opt_t *o, int64_t l_pac, const uint8_t *pac,
 			}
 			if (i == n) {
 				srt[k] = 0;
+				orc_seed_use[2] += k == n - 1;
 				continue;
 			}
 		}
+		orc_seed_use[k == n - 1 ? 0 : 1] += 1;
 		a = reg_push(av);
 		a->w = aw[0] = aw[1] = o->w;
 		a->score = a->truesc = -1;

@@ -100,6 +100,8 @@ def load() -> C.CDLL:
         lib.orc_cells.restype = None
         lib.orc_ext_shapes.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         lib.orc_ext_shapes.restype = None
+        lib.orc_seed_uses.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+        lib.orc_seed_uses.restype = None
         lib.orc_ksw_align2.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                        C.c_int, C.c_int, C.POINTER(C.c_int32)]
         lib.orc_ksw_align2.restype = None
@@ -418,6 +420,16 @@ def ext_shapes(reset: bool = True) -> list:
     out = (C.c_uint64 * 12)()
     load().orc_ext_shapes(out, 1 if reset else 0)
     return [(int(out[2 * b]), int(out[2 * b + 1])) for b in range(6)]
+
+
+def seed_uses(reset: bool = True) -> dict:
+    """Which seeds the restatement's chain2aln extended on this thread: the
+    chain's first seed in the order (longest) or another, first seeds skipped
+    as contained, and the seeds of the chains it ran on."""
+    out = (C.c_uint64 * 4)()
+    load().orc_seed_uses(out, 1 if reset else 0)
+    return dict(first_extended=int(out[0]), other_extended=int(out[1]), first_skipped=int(out[2]),
+                seeds=int(out[3]))
 
 
 def aln(pac, l_pac: int, codes, offs, chains, chain_off, seeds, opt: AlnOptT):

@@ -146,6 +146,7 @@ void orc_cells(uint64_t out[2], int reset);
 /* chain2aln's extensions by qlen bucket (<= 16, 32, 64, 128, 256, longer):
  * out[2 b] calls, out[2 b + 1] in-band cells */
 void orc_ext_shapes(uint64_t out[12], int reset);
+void orc_seed_uses(uint64_t out[4], int reset);
 int orc_ksw_batch(int64_t n, const orc_ksw_task_t *tasks, const uint8_t *q, const uint8_t *t, const orc_ksw_opt_t *o,
 		orc_ksw_result_t *out);
 
