@@ -22,6 +22,21 @@ constexpr int ALN_SPLITS = 16;     // SMEM_ALN_SPLIT accumulators (aln_kernel's 
 constexpr int ALN_HT = 65536;       // hash slots per walk wave
 constexpr int ALN_WALK_WAVES = 4;   // walk waves per CU (aln_heavy_kernel blocks of 256)
 
+// a seed whose region is computed ahead by the lane engine (ksw_lane.h):
+// chain c (absolute), read r, seed si of the chain
+struct RegTask {
+    uint64_t c;
+    uint32_t r, si;
+};
+
+// the lane path's queue words (AlnParams::lq)
+constexpr int LQ_NTASK = 0;     // tasks listed
+constexpr int LQ_BOUNDS = 8;    // [10] queue q = order[bounds[q] .. bounds[q + 1]): pass lengths 16q + 1 .. 16q + 16
+constexpr int LQ_HEADS = 24;    // [8] claim counters
+constexpr int LQ_HIST = 32;     // [130] tasks per pass length (0..128, longer), then cursors
+constexpr int LQ_WORDS = 192;
+constexpr int LQ_BUCKETS = 130;
+
 struct AlnParams {
     // reads (nt4 codes, 4 = N) and the chains smem_batch_chain wrote
     const uint8_t* codes;
@@ -67,6 +82,15 @@ struct AlnParams {
     AlnReg* loc;              // [n_seeds] the regions of each chain's own walk (scratch at the chain's seeds)
     AlnReg* pre_short;        // [n_chains] mem_chain2aln_short's region, heavy reads only
     uint8_t* short_ok;        // [n_chains] 1: that region was made (0: mem_chain2aln runs)
+    // regions computed ahead one seed per lane (lane_on; SMEM_ALN_LANE=0 turns
+    // it off): the light reads' chains' first seeds, the heavy reads' chains'
+    // every seed; the walks take them from pre / pre_ok
+    uint32_t lane_on;
+    RegTask* tasks;           // [n_seeds + n_chains]
+    uint32_t* torder;         // [n_seeds + n_chains] the tasks in pass order (by the pass's query length)
+    uint8_t* tfail;           // [n_seeds + n_chains] 1: left to the walk (query past 128 columns, or scores past 16 bits)
+    uint8_t* sdec;            // [n_chains] light chains: 1 when mem_chain2aln_short declines before its SW
+    uint32_t* lq;             // [LQ_WORDS] the lane path's counters, queue bounds and histogram
     // compaction
     const uint64_t* reg_off;  // [n_reads + 1]
     AlnReg* out;
@@ -101,5 +125,9 @@ hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st);
 // heavy reads: list them (ctr[2]), then, after the host scanned hcnt into
 // hoff, compute their chains' regions ahead and walk them
 hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st);
-hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st);
+// parts: 1 the chain tasks, 2 the walk, 3 both
+hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, int parts, hipStream_t st);
+// lane_on: the regions computed ahead one seed per lane (after the heavy chain
+// tasks, before the walks; lq zeroed)
+hipError_t smem_launch_aln_lane(const smem::AlnParams* P, int n_cu, hipStream_t st);
 }

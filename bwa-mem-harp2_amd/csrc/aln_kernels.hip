@@ -22,6 +22,7 @@
 
 #include "aln_kernels.h"
 #include "ksw_device.h"
+#include "ksw_lane.h"
 
 namespace smem {
 namespace {
@@ -329,20 +330,22 @@ __device__ __attribute__((noinline)) void seed_region_call(const AlnParams& P, c
     if ((threadIdx.x & 63) == 0) *out = a;
 }
 
-enum ChainMode { CM_PLAIN = 0, CM_RECORD = 1, CM_REPLAY = 2 };
+enum ChainMode { CM_PLAIN = 0, CM_RECORD = 1, CM_REPLAY = 2, CM_REPLAY_INL = 3 };
 
 // mem_chain2aln (software/bwamem.c:1040-1188); regs[0 .. nreg) are the read's
 // regions so far, srt the chain's n-word scratch.
 //  CM_RECORD: also leave each extended seed's region at pre[i] (pre_ok[i] = 1);
 //  CM_REPLAY: take a seed's region from pre[i] when pre_ok[i], else compute it
-//    (the heavy-read walk over the chain walks recorded ahead, r0 / r1 given).
+//    (the heavy-read walk over the chain walks recorded ahead, r0 / r1 given);
+//  CM_REPLAY_INL: the same with the computation inlined (the light reads'
+//    walk: a call would cost it half its waves, the callee's registers).
 template <int KC, int MODE = CM_PLAIN>
 __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n,
                                            uint64_t* srt, AlnReg* regs, int& nreg, int lane, AlnReg* pre = nullptr,
                                            uint8_t* pre_ok = nullptr, int64_t r0 = 0, int64_t r1 = 0,
                                            Split* sp = nullptr) {
     n = uni(n);
-    if constexpr (MODE != CM_REPLAY) chain_span(P, L, S, n, lane, r0, r1);
+    if constexpr (MODE != CM_REPLAY && MODE != CM_REPLAY_INL) chain_span(P, L, S, n, lane, r0, r1);
     chain_order(S, n, srt, lane);
     stamp(sp, 2);
     for (int k = n - 1; k >= 0; --k) {
@@ -351,9 +354,13 @@ __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* qu
         const bool want = seed_wanted(P, S, n, srt, k, s, regs, nreg, lane);
         stamp(sp, 3);
         if (want) {
-            if constexpr (MODE == CM_REPLAY) {
+            if constexpr (MODE == CM_REPLAY || MODE == CM_REPLAY_INL) {
                 if (uni((int)pre_ok[si])) {
                     if (lane == 0) regs[nreg] = pre[si];
+                } else if constexpr (MODE == CM_REPLAY_INL) {
+                    count(sp, 11);
+                    const AlnReg a = seed_region<KC>(P, query, L, S, n, s, r0, r1, lane, sp);
+                    if (lane == 0) regs[nreg] = a;
                 } else {
                     seed_region_call<KC>(P, query, L, S, n, (int)si, r0, r1, regs + nreg);
                 }
@@ -376,8 +383,10 @@ __device__ __forceinline__ void chain_full(const AlnParams& P, const uint8_t* qu
 }
 
 // KC = 4 at 4 waves per SIMD (128 VGPRs, 2 spilled): 3 waves at its free
-// allocation (136).  SPLIT: the diagnostic instantiation (Split).
-template <int KC, bool SPLIT = false>
+// allocation (136).  SPLIT: the diagnostic instantiation (Split).  LANE: the
+// walk over regions computed ahead (lane_on): the extensions left to it are
+// behind a call (seed_region_call), so the walk keeps 4 waves a SIMD.
+template <int KC, bool SPLIT = false, bool LANE = false>
 __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
     const int lane = threadIdx.x & 63;
     Split spl{};
@@ -414,12 +423,18 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
                 if (ch.n <= 0) continue;  // mem_chain2aln_short returns -1, nothing is made
                 count(sp, 9);
                 const SeedRec* S = P.seeds + ch.seed_off;
-                const int declined = chain_short(P, query, L, S, ch.n, regs + nreg, lane);
+                // lane_on: the chains aln_light_prep_kernel saw declined skip the
+                // SW, and their seeds' regions come from pre where computed
+                const int declined = LANE && uni((int)P.sdec[c]) ? 1 : chain_short(P, query, L, S, ch.n, regs + nreg, lane);
                 stamp(sp, 1);
                 if (declined == 0) {
                     count(sp, 10);
                     ++nreg;
                     __threadfence_block();
+                } else if constexpr (LANE) {
+                    chain_full<KC, CM_REPLAY_INL>(P, query, L, S, ch.n, P.srt + ch.seed_off, regs, nreg, lane,
+                                              P.pre + ch.seed_off, P.pre_ok + ch.seed_off, P.span[2 * c],
+                                              P.span[2 * c + 1], sp);
                 } else {
                     chain_full<KC>(P, query, L, S, ch.n, P.srt + ch.seed_off, regs, nreg, lane, nullptr, nullptr, 0,
                                    0, sp);
@@ -494,12 +509,20 @@ __device__ __forceinline__ void heavy_chain_task(const AlnParams& P, uint32_t nh
             P.span[2 * c + 1] = r1;
         }
         const bool local = P.spec_local != 0;
-        for (int i = lane; i < ch.n; i += 64) P.pre_ok[ch.seed_off + i] = (uint8_t)(!ok && !local);
+        for (int i = lane; i < ch.n; i += 64) P.pre_ok[ch.seed_off + i] = (uint8_t)(!ok && !local && !P.lane_on);
         __threadfence_block();
         if (!ok && local) {  // the seeds the chain's own walk extends (the read's walk computes any other)
             int nl = 0;
             chain_full<KC, CM_RECORD>(P, query, L, S, ch.n, P.srt + ch.seed_off, P.loc + ch.seed_off, nl, lane,
                                       P.pre + ch.seed_off, P.pre_ok + ch.seed_off);
+        } else if (!ok && P.lane_on) {  // every seed's region, by the lane engine (aln_region_lane_kernel)
+            uint32_t base = 0;
+            if (lane == 0) {
+                atomicAdd(&P.ctr[8], (uint32_t)ch.n);  // regions computed ahead (SMEM_ALN_STATS)
+                base = atomicAdd(&P.lq[LQ_NTASK], (uint32_t)ch.n);
+            }
+            base = (uint32_t)uni((int)base);
+            for (int i = lane; i < ch.n; i += 64) P.tasks[base + i] = RegTask{c, (uint32_t)r, (uint32_t)i};
         } else if (!ok) {  // every seed's region: the read's walk decides which of them are made
             if (lane == 0) atomicAdd(&P.ctr[8], (uint32_t)ch.n);  // regions computed ahead (SMEM_ALN_STATS)
             for (int i = 0; i < ch.n; ++i) {
@@ -809,6 +832,288 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
     }
 }
 
+
+// ---- regions computed ahead, one seed per lane (lane_on) ----
+// The light reads' walk (aln_kernel) extends a seed of a chain only where no
+// region made before contains it; the chain's first seed in the order (its
+// longest) is extended unless an earlier chain's region covers it, and on
+// mem_chain2aln's inputs that is 94 % of the extensions (oracle seed_uses,
+// profiles/r03).  So those seeds' regions -- and every seed of the heavy
+// reads' chains, as before -- are tasks: the left extensions of all tasks run
+// as one pass of the lane engine (kswl::lane_engine, one problem per lane,
+// tasks sorted by query length), then the right ones (each needs its left
+// score), then a pass adds the seed coverage.  The walks take the regions
+// from pre / pre_ok and extend what is left one wave per problem, as before.
+
+// light reads, one lane each: every chain's reference span (chain_span),
+// whether mem_chain2aln_short declines it without its SW (chain_short's tests
+// on the seeds alone, software/bwamem.c:815-828), and, when it does, its first
+// seed in the order as a task; pre_ok cleared for the chain's seeds
+__global__ __launch_bounds__(256) void aln_light_prep_kernel(AlnParams P) {
+    const int64_t l2 = P.l_pac << 1;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < P.n_reads; r += gridDim.x * blockDim.x) {
+        const uint64_t c0 = P.chain_off[r], c1 = P.chain_off[r + 1];
+        if (P.heavy_min && (c1 - c0 >= P.heavy_min || P.seed_off[r + 1] - P.seed_off[r] >= P.heavy_seeds)) continue;
+        const int L = (int)(P.offs[r + 1] - P.offs[r]);
+        for (uint64_t c = c0; c < c1; ++c) {
+            const OutChain ch = P.chains[c];
+            P.sdec[c] = 0;
+            if (ch.n <= 0) continue;
+            const SeedRec* S = P.seeds + ch.seed_off;
+            int64_t qb = L, qe = 0, rb = l2, re = 0, r0 = l2, r1 = 0;
+            uint64_t best = 0;
+            int top = 0;
+            for (int i = 0; i < ch.n; ++i) {
+                const SeedRec s = S[i];
+                qb = s.qbeg < qb ? s.qbeg : qb;
+                qe = s.qbeg + s.len > qe ? s.qbeg + s.len : qe;
+                rb = s.rbeg < rb ? s.rbeg : rb;
+                re = s.rbeg + s.len > re ? s.rbeg + s.len : re;
+                const int64_t b = s.rbeg - (s.qbeg + max_gap(P, s.qbeg));
+                const int64_t e = s.rbeg + s.len + ((L - s.qbeg - s.len) + max_gap(P, L - s.qbeg - s.len));
+                r0 = b < r0 ? b : r0;
+                r1 = e > r1 ? e : r1;
+                const uint64_t key = (uint64_t)(uint32_t)s.len << 32 | (uint32_t)i;  // distinct: the largest is srt[n - 1]
+                if (key > best) best = key, top = i;
+                P.pre_ok[ch.seed_off + i] = 0;
+            }
+            qb -= 50, qe += 50, rb -= 50, re += 50;  // MEM_SHORT_EXT
+            bool decline = qb <= 10 || qe >= L - 10;
+            rb = rb > 0 ? rb : 0;
+            re = re < l2 ? re : l2;
+            if (rb < P.l_pac && P.l_pac < re) {
+                if (S[0].rbeg < P.l_pac) re = P.l_pac;
+                else rb = P.l_pac;
+            }
+            decline = decline || (re - rb) - (qe - qb) > 50 || (qe - qb) - (re - rb) > 50;
+            decline = decline || qe - qb >= P.w * 4 || re - rb >= P.w * 4;
+            decline = decline || qe - qb >= 200 || re - rb >= 200;  // MEM_SHORT_LEN
+            r0 = r0 > 0 ? r0 : 0;
+            r1 = r1 < l2 ? r1 : l2;
+            if (r0 < P.l_pac && P.l_pac < r1) {
+                if (S[0].rbeg < P.l_pac) r1 = P.l_pac;
+                else r0 = P.l_pac;
+            }
+            P.span[2 * c] = r0;
+            P.span[2 * c + 1] = r1;
+            P.sdec[c] = (uint8_t)decline;
+            if (decline) P.tasks[atomicAdd(&P.lq[LQ_NTASK], 1u)] = RegTask{c, (uint32_t)r, (uint32_t)top};
+        }
+    }
+}
+
+// the query length of task t's extension in pass `side` (0 left, 1 right);
+// LQ_BUCKETS - 1: not run by the lanes (longer than 128, or failed before)
+__device__ __forceinline__ int task_key(const AlnParams& P, uint32_t t, int side) {
+    const RegTask T = P.tasks[t];
+    const SeedRec s = P.seeds[P.chains[T.c].seed_off + T.si];
+    int q;
+    if (side == 0) {
+        q = s.qbeg;
+    } else {
+        if (P.tfail[t]) return LQ_BUCKETS - 1;
+        q = (int)(P.offs[T.r + 1] - P.offs[T.r]) - s.qbeg - s.len;
+    }
+    return q <= 128 ? q : LQ_BUCKETS - 1;
+}
+
+// counting sort of the tasks by the pass's query length: block histograms in
+// LDS, one global add per length per block
+__global__ __launch_bounds__(256) void aln_task_hist_kernel(AlnParams P, int side) {
+    __shared__ uint32_t h[LQ_BUCKETS];
+    for (int k = threadIdx.x; k < LQ_BUCKETS; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    const uint32_t n = P.lq[LQ_NTASK];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        if (side == 0) P.tfail[t] = 0;
+        atomicAdd(&h[task_key(P, t, side)], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < LQ_BUCKETS; k += blockDim.x)
+        if (h[k]) atomicAdd(&P.lq[LQ_HIST + k], h[k]);
+}
+
+// cursors (exclusive scan) and the 16-column queues; heads cleared
+__global__ __launch_bounds__(64) void aln_task_scan_kernel(AlnParams P) {
+    if (threadIdx.x != 0) return;
+    uint32_t a = 0;
+    uint32_t c[LQ_BUCKETS];
+    for (int k = 0; k < LQ_BUCKETS; ++k) {
+        c[k] = a;
+        a += P.lq[LQ_HIST + k];
+    }
+    for (int k = 0; k < LQ_BUCKETS; ++k) P.lq[LQ_HIST + k] = c[k];
+    P.lq[LQ_BOUNDS] = 0;
+    for (int q = 1; q <= 8; ++q) P.lq[LQ_BOUNDS + q] = c[16 * q + 1];
+    for (int q = 0; q < 8; ++q) P.lq[LQ_HEADS + q] = 0;
+}
+
+// the tasks in pass order (a block reserves its share of each length with one
+// global add); tasks past 128 columns are marked failed (left to the walk)
+__global__ __launch_bounds__(256) void aln_task_scatter_kernel(AlnParams P, int side) {
+    __shared__ uint32_t h[LQ_BUCKETS], base[LQ_BUCKETS];
+    const uint32_t n = P.lq[LQ_NTASK];
+    const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint32_t t0 = blockIdx.x * per, t1 = t0 + per < n ? t0 + per : n;
+    for (int k = threadIdx.x; k < LQ_BUCKETS; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    for (uint32_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) atomicAdd(&h[task_key(P, t, side)], 1u);
+    __syncthreads();
+    for (int k = threadIdx.x; k < LQ_BUCKETS; k += blockDim.x) {
+        base[k] = h[k] ? atomicAdd(&P.lq[LQ_HIST + k], h[k]) : 0u;
+        h[k] = 0;
+    }
+    __syncthreads();
+    for (uint32_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
+        const int k = task_key(P, t, side);
+        P.torder[base[k] + atomicAdd(&h[k], 1u)] = t;
+        if (k == LQ_BUCKETS - 1) P.tfail[t] = 1;
+    }
+}
+
+// A task's pass through the lane engine: the left extension (reversed query
+// and reference, software/bwamem.c:1118-1137) or the right one (:1144-1166)
+// with MAX_BAND_TRY, the pass's share of the region written to pre (the left
+// pass: qb, rb, score, truesc, w; the right pass: the rest, then
+// aln_region_cov_kernel the seed coverage and pre_ok).
+struct RegionPol {
+    const AlnParams* P;
+    int side, top;
+    uint32_t t = 0;
+    AlnReg* out = nullptr;
+    int64_t tpos = 0;  // the reference position of row 0; left rows run downwards
+    int64_t rbeg = 0;
+    int qbeg = 0, len = 0, L = 0, tr = 0, prev = 0, sc0 = 0;
+
+    template <int KCOL>
+    __device__ __forceinline__ bool start(uint32_t k, kswd::ExtIn& T, uint2* qs) {
+        t = P->torder[k];
+        const RegTask R = P->tasks[t];
+        const OutChain ch = P->chains[R.c];
+        const SeedRec s = P->seeds[ch.seed_off + R.si];
+        const uint64_t q0 = P->offs[R.r];
+        const uint8_t* query = P->codes + q0;
+        L = (int)(P->offs[R.r + 1] - q0);
+        out = P->pre + ch.seed_off + R.si;
+        rbeg = s.rbeg, qbeg = s.qbeg, len = s.len, tr = 0;
+        if (side == 0) {
+            if (qbeg == 0) {  // no left extension
+                out->qb = 0, out->rb = rbeg, out->score = out->truesc = len * P->a, out->w = P->w;
+                return false;
+            }
+            T = kswd::ExtIn{qbeg, (int)(rbeg - P->span[2 * R.c]), P->w, P->pen_clip5, P->zdrop, len * P->a};
+            if (!kswl::extend_lane_ok(KCOL, T.qlen, T.h0, top)) {
+                P->tfail[t] = 1;
+                return false;
+            }
+            kswl::load_query_rev<KCOL>(qs, query + qbeg, qbeg);
+            tpos = rbeg - 1, prev = -1;
+        } else {
+            const int qe = qbeg + len;
+            sc0 = prev = out->score;
+            if (qe == L) {  // no right extension
+                out->qe = L, out->re = rbeg + len, out->w = P->w > out->w ? P->w : out->w;
+                return false;
+            }
+            const int64_t rs = rbeg + len;
+            T = kswd::ExtIn{L - qe, (int)(P->span[2 * R.c + 1] - rs), P->w, P->pen_clip3, P->zdrop, sc0};
+            if (!kswl::extend_lane_ok(KCOL, T.qlen, T.h0, top)) {
+                P->tfail[t] = 1;
+                return false;
+            }
+            kswl::load_query_fwd<KCOL>(qs, query + qe, L - qe);
+            tpos = rs;
+        }
+        return true;
+    }
+    __device__ __forceinline__ int tsym(int i) const { return ref_at(*P, side == 0 ? tpos - i : tpos + i); }
+    __device__ __forceinline__ bool finish(const KswResult& x, kswd::ExtIn& T) {
+        const int aw = P->w << tr;
+        if (tr == 0 && !(x.score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {  // MAX_BAND_TRY
+            prev = x.score, tr = 1, T.w = P->w << 1;
+            return true;
+        }
+        if (side == 0) {
+            out->score = x.score, out->w = aw;
+            if (x.gscore <= 0 || x.gscore <= x.score - P->pen_clip5) {
+                out->qb = qbeg - x.qle, out->rb = rbeg - x.tle, out->truesc = x.score;
+            } else {
+                out->qb = 0, out->rb = rbeg - x.gtle, out->truesc = x.gscore;
+            }
+        } else {
+            const int qe = qbeg + len;
+            const int64_t rs = rbeg + len;
+            out->score = x.score, out->w = aw > out->w ? aw : out->w;
+            if (x.gscore <= 0 || x.gscore <= x.score - P->pen_clip3) {
+                out->qe = qe + x.qle, out->re = rs + x.tle, out->truesc += x.score - sc0;
+            } else {
+                out->qe = L, out->re = rs + x.gtle, out->truesc += x.gscore - sc0;
+            }
+        }
+        return false;
+    }
+};
+
+// KCOL-column lane engine over the pass's queues of query lengths up to KCOL
+// (32: queues 0-1, 64: 2-3, 128: 4-7)
+template <int KCOL>
+__global__ __launch_bounds__(256, KCOL > 64 ? 2 : 4) void aln_region_lane_kernel(AlnParams P, int side) {
+    __shared__ uint32_t stab[10];
+    __shared__ uint2 qsl[4][KCOL / 8 * 64];
+    if (threadIdx.x < 5) kswl::row_scores(P.mat, threadIdx.x, stab[2 * threadIdx.x], stab[2 * threadIdx.x + 1]);
+    __syncthreads();
+    RegionPol pol{&P, side, P.top};
+    kswl::lane_engine<KCOL, 8>(pol, P.lq + LQ_BOUNDS, P.lq + LQ_HEADS, KCOL == 32 ? 0 : KCOL / 32, KCOL / 16, stab,
+                               qsl[threadIdx.x >> 6], P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
+}
+
+// the tasks the lanes left (a query past 128 columns, scores past 16 bits):
+// the whole region one wave per task, as the heavy chain tasks did (left to
+// the walks, they made the human-like profile's heavy walk 4x slower)
+template <int KC>
+__global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_region_rest_kernel(AlnParams P) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = P.lq[LQ_NTASK];
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t t = wave; t < n; t += n_waves) {
+        if (!uni((int)P.tfail[t])) continue;
+        const RegTask R = P.tasks[t];
+        const uint64_t q0 = P.offs[R.r];
+        const int L = uni((int)(P.offs[R.r + 1] - q0));
+        if ((L > 256) != (KC > 4)) continue;  // the other instantiation's read
+        const OutChain ch = P.chains[R.c];
+        const SeedRec* S = P.seeds + ch.seed_off;
+        const AlnReg a = seed_region<KC>(P, P.codes + q0, L, S, uni(ch.n), S[R.si], P.span[2 * R.c],
+                                         P.span[2 * R.c + 1], lane);
+        if (lane == 0) {
+            P.pre[ch.seed_off + R.si] = a;
+            P.pre_ok[ch.seed_off + R.si] = 1;
+        }
+    }
+}
+
+// the regions' seed coverage (software/bwamem.c:1180-1184) and pre_ok, one
+// task per thread
+__global__ __launch_bounds__(256) void aln_region_cov_kernel(AlnParams P) {
+    const uint32_t n = P.lq[LQ_NTASK];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        if (P.tfail[t]) continue;
+        const RegTask R = P.tasks[t];
+        const OutChain ch = P.chains[R.c];
+        const SeedRec* S = P.seeds + ch.seed_off;
+        AlnReg* a = P.pre + ch.seed_off + R.si;
+        const int64_t rb = a->rb, re = a->re;
+        const int qb = a->qb, qe = a->qe;
+        int cov = 0;
+        for (int i = 0; i < ch.n; ++i) {
+            const SeedRec u = S[i];
+            if (u.qbeg >= qb && u.qbeg + u.len <= qe && u.rbeg >= rb && u.rbeg + u.len <= re) cov += u.len;
+        }
+        a->sub = 0, a->csub = 0, a->sub_n = 0, a->seedcov = cov, a->secondary = 0, a->hash = 0;
+        P.pre_ok[ch.seed_off + R.si] = 1;
+    }
+}
+
 // regions compacted per read (one thread per read)
 __global__ __launch_bounds__(256) void aln_write_kernel(AlnParams P) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -855,12 +1160,22 @@ extern "C" hipError_t smem_launch_aln(const smem::AlnParams* P, int n_cu, int lo
         const uint64_t per_block = 4ull * 4 * P->light_claims;  // 4 waves x 4 reads per claim
         blocks = blocks16 = (int)std::max<uint64_t>(1, (P->n_reads + per_block - 1) / per_block);
     }
-    if (P->split) hipLaunchKernelGGL((smem::aln_kernel<4, true>), dim3(blocks), dim3(256), 0, st, *P);
-    else hipLaunchKernelGGL(smem::aln_kernel<4>, dim3(blocks), dim3(256), 0, st, *P);
+    if (P->lane_on) {
+        if (P->split) hipLaunchKernelGGL((smem::aln_kernel<4, true, true>), dim3(blocks), dim3(256), 0, st, *P);
+        else hipLaunchKernelGGL((smem::aln_kernel<4, false, true>), dim3(blocks), dim3(256), 0, st, *P);
+    } else {
+        if (P->split) hipLaunchKernelGGL((smem::aln_kernel<4, true>), dim3(blocks), dim3(256), 0, st, *P);
+        else hipLaunchKernelGGL(smem::aln_kernel<4>, dim3(blocks), dim3(256), 0, st, *P);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !long_reads) return e;
-    if (P->split) hipLaunchKernelGGL((smem::aln_kernel<16, true>), dim3(blocks16), dim3(256), 0, st, *P);
-    else hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(blocks16), dim3(256), 0, st, *P);
+    if (P->lane_on) {
+        if (P->split) hipLaunchKernelGGL((smem::aln_kernel<16, true, true>), dim3(blocks16), dim3(256), 0, st, *P);
+        else hipLaunchKernelGGL((smem::aln_kernel<16, false, true>), dim3(blocks16), dim3(256), 0, st, *P);
+    } else {
+        if (P->split) hipLaunchKernelGGL((smem::aln_kernel<16, true>), dim3(blocks16), dim3(256), 0, st, *P);
+        else hipLaunchKernelGGL(smem::aln_kernel<16>, dim3(blocks16), dim3(256), 0, st, *P);
+    }
     return hipGetLastError();
 }
 
@@ -870,9 +1185,13 @@ extern "C" hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStre
     return hipGetLastError();
 }
 
-extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
-    hipLaunchKernelGGL(smem::aln_heavy_task_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
-    if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_task_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
+extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, int parts,
+                                            hipStream_t st) {
+    if (parts & 1) {
+        hipLaunchKernelGGL(smem::aln_heavy_task_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
+        if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_task_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
+    }
+    if (!(parts & 2)) return hipGetLastError();
     // the walk kernels use the per-wave hash tables in turn (same stream);
     // walk_guard != 0: the inlined, guarded walk (diagnostic)
     if (P->walk_guard) {
@@ -885,6 +1204,29 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
     hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
     if (long_reads)
         hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+// the lane path between the heavy chain tasks and the walks: the light
+// reads' tasks, then per pass (left, right) the sort and the three tiers of
+// the lane engine, then the coverage pass (P->lq zeroed by the caller)
+extern "C" hipError_t smem_launch_aln_lane(const smem::AlnParams* P, int n_cu, hipStream_t st) {
+    if (P->n_reads <= 0) return hipSuccess;
+    const int rb = std::max(1, std::min(n_cu * 4, (P->n_reads + 255) / 256));
+    hipLaunchKernelGGL(smem::aln_light_prep_kernel, dim3(rb), dim3(256), 0, st, *P);
+    for (int side = 0; side < 2; ++side) {
+        hipError_t e = hipMemsetAsync(P->lq + smem::LQ_HIST, 0, sizeof(uint32_t) * smem::LQ_BUCKETS, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(smem::aln_task_hist_kernel, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_task_scan_kernel, dim3(1), dim3(64), 0, st, *P);
+        hipLaunchKernelGGL(smem::aln_task_scatter_kernel, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_region_lane_kernel<32>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_region_lane_kernel<64>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_region_lane_kernel<128>, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
+    }
+    hipLaunchKernelGGL(smem::aln_region_cov_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
+    hipLaunchKernelGGL(smem::aln_region_rest_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
+    hipLaunchKernelGGL(smem::aln_region_rest_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

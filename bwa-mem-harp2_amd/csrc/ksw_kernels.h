@@ -30,3 +30,6 @@ struct KswParams {
 }  // namespace smem
 
 extern "C" hipError_t smem_launch_ksw(const smem::KswParams* K, int n_cu, hipStream_t st);
+// one problem per lane (kswl::lane_engine), scratch of smem_ksw_lane_scratch(n) bytes
+extern "C" size_t smem_ksw_lane_scratch(int n);
+extern "C" hipError_t smem_launch_ksw_lane(const smem::KswParams* K, void* scratch, int n_cu, hipStream_t st);

@@ -157,10 +157,15 @@ struct AlnHeavyBufs {
     DevBuf<int32_t> rnext;
     DevBuf<smem::AlnReg> pre, pre_short, loc;
     DevBuf<uint8_t> short_ok, pre_ok, tmp;
+    // the lane path (regions computed ahead one seed per lane)
+    DevBuf<smem::RegTask> tasks;
+    DevBuf<uint32_t> torder, lq;
+    DevBuf<uint8_t> tfail, sdec;
     void release() {
         heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); ht.release(); rnext.release();
         pre.release();
         pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
+        tasks.release(); torder.release(); lq.release(); tfail.release(); sdec.release();
     }
 };
 
@@ -1153,8 +1158,18 @@ int smem_ksw_extend(smem_gpu_t* g, int n, const smem_ksw_task_t* tasks, const ui
     K.o_ins = opt->o_ins;
     K.e_ins = opt->e_ins;
     K.out = dr.p;
+    // SMEM_KSW_LANE=1: one problem per lane (kswl::lane_engine), tiers by query length
+    const char* lane_e = getenv("SMEM_KSW_LANE");
+    const bool lane = lane_e && atoi(lane_e);
+    DevBuf<uint8_t> dsc;
+    struct FreeSc {
+        DevBuf<uint8_t>& b;
+        ~FreeSc() { b.release(); }
+    } free_sc{dsc};
+    if (lane) HIP_TRY(dsc.ensure(smem_ksw_lane_scratch(n)));
     HIP_TRY(hipEventRecord(ev[0], st));
-    HIP_TRY(smem_launch_ksw(&K, g->n_cu, st));
+    if (lane) HIP_TRY(smem_launch_ksw_lane(&K, dsc.p, g->n_cu, st));
+    else HIP_TRY(smem_launch_ksw(&K, g->n_cu, st));
     HIP_TRY(hipEventRecord(ev[1], st));
     HIP_TRY(hipMemcpyAsync(out, dr.p, sizeof(smem::KswResult) * n, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -1323,6 +1338,12 @@ static uint32_t aln_heavy_seeds() {
     const char* e = getenv("SMEM_ALN_HEAVY_SEEDS");
     return e ? (uint32_t)atoi(e) : 48u;
 }
+// SMEM_ALN_LANE=0: no regions computed ahead one seed per lane (the walks
+// extend every seed one wave per problem, round-2 style)
+static bool aln_lane_on() {
+    const char* e = getenv("SMEM_ALN_LANE");
+    return !(e && atoi(e) == 0);
+}
 
 // mem_chain2aln of every chain of every read (P filled, ctr zeroed for
 // smem::ALN_CTRS): heavy reads listed, their chains' and seeds' regions
@@ -1371,6 +1392,21 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         const char* w = getenv("SMEM_ALN_WALK_INLINE");
         P.walk_guard = (w && atoi(w) > 0) ? (atoi(w) > 1 ? (uint32_t)atoi(w) : (1u << 26)) : 0u;
     }
+    P.lane_on = aln_lane_on() && n > 0 ? 1u : 0u;
+    if (P.lane_on) {
+        const uint64_t nt = std::max<uint64_t>(n_seeds + n_chains, 1);
+        HIP_TRY(H.pre.grow(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.pre_ok.grow(std::max<uint64_t>(n_seeds, 1)));
+        HIP_TRY(H.span.grow(2 * std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.sdec.grow(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.tasks.grow(nt));
+        HIP_TRY(H.torder.grow(nt));
+        HIP_TRY(H.tfail.grow(nt));
+        HIP_TRY(H.lq.grow(smem::LQ_WORDS));
+        HIP_TRY(hipMemsetAsync(H.lq.p, 0, sizeof(uint32_t) * smem::LQ_WORDS, st));
+        P.pre = H.pre.p, P.pre_ok = H.pre_ok.p, P.span = H.span.p, P.sdec = H.sdec.p;
+        P.tasks = H.tasks.p, P.torder = H.torder.p, P.tfail = H.tfail.p, P.lq = H.lq.p;
+    }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
         HIP_TRY(H.heavy.grow(n));
@@ -1398,11 +1434,34 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.hoff = H.hoff.p, P.pre = H.pre.p, P.loc = H.loc.p, P.pre_ok = H.pre_ok.p, P.pre_short = H.pre_short.p;
         P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
+    }
+    if (P.lane_on) {
+        // heavy chain tasks (they list their seeds as tasks), the lane engine's
+        // passes over every task, then the walks: the heavy one on st, the
+        // light reads beside it on st2
+        if (n_heavy) HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 1, st));
+        HIP_TRY(smem_launch_aln_lane(&P, g->n_cu, st));
+        if (n_heavy && st2 && ev_join) {
+            HIP_TRY(hipEventRecord(ev_join, st));
+            HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
+            HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 2, st));
+            P.light_claims = aln_light_claims();
+            HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st2));
+            P.light_claims = 0;
+            HIP_TRY(hipEventRecord(ev_join, st2));
+            HIP_TRY(hipStreamWaitEvent(st, ev_join, 0));
+            return SMEM_OK;
+        }
+        if (n_heavy) HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 2, st));
+        HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
+        return SMEM_OK;
+    }
+    if (n_heavy) {
         if (st2 && ev_join) {
             // the heavy kernels first (their chain tasks then the walk are the
             // critical path); classify finished (synchronised above), so st2
             // has nothing to wait for
-            HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, st));
+            HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 3, st));
             P.light_claims = aln_light_claims();  // its blocks retire, so the walk finds CU slots
             HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st2));
             P.light_claims = 0;
@@ -1410,7 +1469,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
             HIP_TRY(hipStreamWaitEvent(st, ev_join, 0));
             return SMEM_OK;
         }
-        HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, st));
+        HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 3, st));
     }
     HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
     return SMEM_OK;

@@ -16,12 +16,15 @@ from tests import golden_data
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["wave", "g16"], autouse=True)
+@pytest.fixture(params=["wave", "g16", "lane"], autouse=True)
 def ksw_kernel(request, monkeypatch):
-    """Every test on both kernels: one problem per wave, and four per wave on
-    16-lane groups (SMEM_KSW_G16, kswd::extend_group16)."""
+    """Every test on each kernel: one problem per wave, four per wave on
+    16-lane groups (SMEM_KSW_G16, kswd::extend_group16), and one per lane
+    (SMEM_KSW_LANE, kswl::extend_lane, with its fallbacks to one per wave)."""
     if request.param == "g16":
         monkeypatch.setenv("SMEM_KSW_G16", "1")
+    if request.param == "lane":
+        monkeypatch.setenv("SMEM_KSW_LANE", "1")
     return request.param
 
 
@@ -63,14 +66,18 @@ def test_ksw_vs_oracle(gpu, scoring):
 
 def test_ksw_edges(gpu):
     """qlen 1 and 255 (the column limit), empty targets, h0 = 0, z-drop off,
-    bands of 1, all-N queries."""
+    bands of 1, all-N queries, scores past 16 bits (h0 near 2^16: the lane
+    kernel hands those to one wave each), query lengths at the lane tiers'
+    edges (32, 33, 64, 65, 128, 129)."""
     from smemgpu import synth
     rng = np.random.default_rng(150)
     tasks, qs, ts = [], [], []
     qo = to = 0
     for qlen, tlen, w, zd, h0 in [(1, 0, 100, 100, 10), (1, 1, 100, 100, 0), (255, 300, 100, 100, 40),
                                   (255, 255, 1, 0, 200), (200, 0, 100, 100, 30), (64, 64, 5, 100, 19),
-                                  (65, 130, 200, 100, 100), (128, 90, 100, 0, 0), (191, 192, 50, 3, 60)]:
+                                  (65, 130, 200, 100, 100), (128, 90, 100, 0, 0), (191, 192, 50, 3, 60),
+                                  (100, 120, 100, 100, 65500), (30, 40, 100, 100, 65400), (32, 40, 10, 100, 30),
+                                  (33, 50, 100, 100, 30), (129, 140, 100, 100, 50), (8, 300, 100, 0, 20)]:
         for rep in range(3):
             q = rng.integers(0, 4, size=qlen).astype(np.uint8)
             t = np.concatenate([q[:min(qlen, tlen)], rng.integers(0, 4, size=max(0, tlen - qlen))]).astype(np.uint8)

@@ -19,7 +19,9 @@ def main():
     p.add_argument("--launches", type=int, default=2)
     p.add_argument("--cycles", default=None, help="write per-read shader cycles of the last launch here (u64)")
     p.add_argument("--lib", default=None, help="another libsmemgpu build (diagnostics)")
-    p.add_argument("--env-sweep", default="", help="';'-separated settings, each ','-separated VAR=value: "
+    p.add_argument("--compare", action="store_true", help="fetch the regions after each setting: all settings must "
+                   "give the same bytes (e.g. SMEM_ALN_LANE=0 / 1)")
+    p.add_argument("--env-sweep", default="", help="';'- (or '/'-) separated settings, each ','-separated VAR=value: "
                    "--launches launches under each, in turn (the library reads them per call)")
     own, rest = p.parse_known_args()
     import torch
@@ -41,7 +43,8 @@ def main():
     b.run(opt)
     b.sa(opt.min_seed_len, 10000)
     b.chain(idx.seq_len // 2)
-    settings = [s for s in own.env_sweep.split(";") if s] or [""]
+    settings = [s for s in own.env_sweep.replace("/", ";").split(";") if s] or [""]
+    first = None
     for setting in settings:
         kv = dict(x.split("=", 1) for x in setting.split(",") if x)
         saved = {k: os.environ.get(k) for k in kv}
@@ -54,6 +57,18 @@ def main():
             st = b.stats()
             print(f"chain2aln{' [' + setting + ']' if setting else ''}: {st['aln_ms']:.3f} ms, {st['n_regs']} regions, "
                   f"{st['n_chains']} chains, wall {1e3 * (time.time() - t):.1f} ms", flush=True)
+        if own.compare:
+            import numpy as np
+            res = b.fetch(8)  # FETCH_REGS
+            regs = (res.regs.copy(), np.asarray(res.reg_off).copy())
+            if first is None:
+                first = regs
+            same = regs[0].size == first[0].size and bool((regs[0] == first[0]).all()) and \
+                bool((regs[1] == first[1]).all())
+            print(f"regions [{setting}] {regs[0].size // 64}: {'same as' if same else 'DIFFER from'} the first setting's",
+                  flush=True)
+            if not same:
+                raise SystemExit(1)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
