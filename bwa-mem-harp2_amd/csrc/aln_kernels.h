@@ -31,6 +31,7 @@ struct RegTask {
 
 // the lane path's queue words (AlnParams::lq)
 constexpr int LQ_NTASK = 0;     // tasks listed
+constexpr int LQ_NSW = 1;       // heavy chains listed for mem_chain2aln_short's SW
 constexpr int LQ_BOUNDS = 8;    // [10] queue q = order[bounds[q] .. bounds[q + 1]): pass lengths 16q + 1 .. 16q + 16
 constexpr int LQ_HEADS = 24;    // [8] claim counters
 constexpr int LQ_HIST = 32;     // [130] tasks per pass length (0..128, longer), then cursors
@@ -91,6 +92,8 @@ struct AlnParams {
     uint8_t* tfail;           // [n_seeds + n_chains] 1: left to the walk (query past 128 columns, or scores past 16 bits)
     uint8_t* sdec;            // [n_chains] light chains: 1 when mem_chain2aln_short declines before its SW
     uint32_t* lq;             // [LQ_WORDS] the lane path's counters, queue bounds and histogram
+    uint32_t* chain_read;     // [n_chains] the read of each chain, bit 31: a heavy read
+    uint32_t* swlist;         // [n_chains] heavy chains whose mem_chain2aln_short runs its SW (lq[LQ_NSW] of them)
     // compaction
     const uint64_t* reg_off;  // [n_reads + 1]
     AlnReg* out;
@@ -127,7 +130,7 @@ hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st);
 hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st);
 // parts: 1 the chain tasks, 2 the walk, 3 both
 hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, int parts, hipStream_t st);
-// lane_on: the regions computed ahead one seed per lane (after the heavy chain
-// tasks, before the walks; lq zeroed)
-hipError_t smem_launch_aln_lane(const smem::AlnParams* P, int n_cu, hipStream_t st);
+// lane_on: the regions computed ahead one seed per lane, before the walks
+// (lq zeroed; the heavy reads classified: heavy_min / heavy_seeds set)
+hipError_t smem_launch_aln_lane(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st);
 }

@@ -106,7 +106,7 @@ __device__ __forceinline__ void count(Split* sp, int k) {
 // declines are flags, not early returns (an early return out of this wave-
 // cooperative body, inlined into a persistent loop, hung gfx950 waves).
 __device__ __forceinline__ int chain_short(const AlnParams& P, const uint8_t* query, int L, const SeedRec* S, int n,
-                                           AlnReg* out, int lane) {
+                                           AlnReg* out, int lane, uint32_t* sw_ctr = nullptr) {
     int64_t qb = L, qe = 0, rb = P.l_pac << 1, re = 0;
     int cov = 0;
     for (int i = lane; i < n; i += 64) {
@@ -131,6 +131,7 @@ __device__ __forceinline__ int chain_short(const AlnParams& P, const uint8_t* qu
     decline = decline || qe - qb >= P.w * 4 || re - rb >= P.w * 4;
     decline = decline || qe - qb >= 200 || re - rb >= 200;  // MEM_SHORT_LEN
     if (!decline) {
+        if (sw_ctr && lane == 0) atomicAdd(sw_ctr, 1u);  // SMEM_ALN_STATS: chains that run the SW
         const int ql = (int)(qe - qb), tl = (int)(re - rb);
         const int xtra =
             kswd::SW_XSUBO | kswd::SW_XSTART | (ql * P.a < 250 ? kswd::SW_XBYTE : 0) | (P.min_seed_len * P.a);
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_kernel(AlnParams P) {
                 if (ch.n <= 0) continue;  // mem_chain2aln_short returns -1, nothing is made
                 count(sp, 9);
                 const SeedRec* S = P.seeds + ch.seed_off;
-                // lane_on: the chains aln_light_prep_kernel saw declined skip the
+                // lane_on: the chains aln_chain_prep_kernel saw declined skip the
                 // SW, and their seeds' regions come from pre where computed
                 const int declined = LANE && uni((int)P.sdec[c]) ? 1 : chain_short(P, query, L, S, ch.n, regs + nreg, lane);
                 stamp(sp, 1);
@@ -500,7 +501,8 @@ __device__ __forceinline__ void heavy_chain_task(const AlnParams& P, uint32_t nh
     if ((L > 256) == (KC > 4) && ch.n > 0) {  // this instantiation's read, a chain with seeds
         const uint8_t* query = P.codes + q0;
         const SeedRec* S = P.seeds + ch.seed_off;
-        const int ok = chain_short(P, query, L, S, ch.n, P.pre_short + c, lane) == 0;
+        if (lane == 0) atomicAdd(&P.ctr[11], 1u);  // SMEM_ALN_STATS: heavy chains
+        const int ok = chain_short(P, query, L, S, ch.n, P.pre_short + c, lane, P.ctr + 12) == 0;
         int64_t r0, r1;
         chain_span(P, L, S, ch.n, lane, r0, r1);
         if (lane == 0) {
@@ -845,59 +847,108 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
 // score), then a pass adds the seed coverage.  The walks take the regions
 // from pre / pre_ok and extend what is left one wave per problem, as before.
 
-// light reads, one lane each: every chain's reference span (chain_span),
-// whether mem_chain2aln_short declines it without its SW (chain_short's tests
-// on the seeds alone, software/bwamem.c:815-828), and, when it does, its first
-// seed in the order as a task; pre_ok cleared for the chain's seeds
-__global__ __launch_bounds__(256) void aln_light_prep_kernel(AlnParams P) {
-    const int64_t l2 = P.l_pac << 1;
+// the read of every chain (bit 31: a heavy read), one thread per read
+__global__ __launch_bounds__(256) void aln_chain_read_kernel(AlnParams P) {
     for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < P.n_reads; r += gridDim.x * blockDim.x) {
         const uint64_t c0 = P.chain_off[r], c1 = P.chain_off[r + 1];
-        if (P.heavy_min && (c1 - c0 >= P.heavy_min || P.seed_off[r + 1] - P.seed_off[r] >= P.heavy_seeds)) continue;
+        const bool heavy =
+            P.heavy_min && (c1 - c0 >= P.heavy_min || P.seed_off[r + 1] - P.seed_off[r] >= P.heavy_seeds);
+        const uint32_t v = (uint32_t)r | (heavy ? 0x80000000u : 0u);
+        for (uint64_t c = c0; c < c1; ++c) P.chain_read[c] = v;
+    }
+}
+
+// Every chain, one lane each: its reference span (chain_span), whether
+// mem_chain2aln_short declines it without its SW (chain_short's tests on the
+// seeds alone, software/bwamem.c:815-828), and its tasks:
+//   a light read's chain: when declined, its first seed in the order (the
+//     walk, aln_kernel, runs the SW of the others itself);
+//   a heavy read's chain: when declined, every seed (short_ok = 0); else it is
+//     listed for its SW (aln_heavy_sw_kernel).
+// pre_ok cleared for the chain's seeds.  (One wave per heavy chain, with a
+// binary search for its read and wave reductions, took 75 ms on the human-like
+// profile's 3.2 M heavy chains: latency-bound.)
+__global__ __launch_bounds__(256) void aln_chain_prep_kernel(AlnParams P, uint32_t n_chains) {
+    const int64_t l2 = P.l_pac << 1;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n_chains; c += gridDim.x * blockDim.x) {
+        const uint32_t rv = P.chain_read[c];
+        const uint32_t r = rv & 0x7fffffffu;
+        const bool heavy = (rv >> 31) != 0;
+        const OutChain ch = P.chains[c];
+        P.sdec[c] = 0;
+        if (heavy) P.short_ok[c] = 0;
+        if (ch.n <= 0) continue;
         const int L = (int)(P.offs[r + 1] - P.offs[r]);
-        for (uint64_t c = c0; c < c1; ++c) {
-            const OutChain ch = P.chains[c];
-            P.sdec[c] = 0;
-            if (ch.n <= 0) continue;
-            const SeedRec* S = P.seeds + ch.seed_off;
-            int64_t qb = L, qe = 0, rb = l2, re = 0, r0 = l2, r1 = 0;
-            uint64_t best = 0;
-            int top = 0;
-            for (int i = 0; i < ch.n; ++i) {
-                const SeedRec s = S[i];
-                qb = s.qbeg < qb ? s.qbeg : qb;
-                qe = s.qbeg + s.len > qe ? s.qbeg + s.len : qe;
-                rb = s.rbeg < rb ? s.rbeg : rb;
-                re = s.rbeg + s.len > re ? s.rbeg + s.len : re;
-                const int64_t b = s.rbeg - (s.qbeg + max_gap(P, s.qbeg));
-                const int64_t e = s.rbeg + s.len + ((L - s.qbeg - s.len) + max_gap(P, L - s.qbeg - s.len));
-                r0 = b < r0 ? b : r0;
-                r1 = e > r1 ? e : r1;
-                const uint64_t key = (uint64_t)(uint32_t)s.len << 32 | (uint32_t)i;  // distinct: the largest is srt[n - 1]
-                if (key > best) best = key, top = i;
-                P.pre_ok[ch.seed_off + i] = 0;
-            }
-            qb -= 50, qe += 50, rb -= 50, re += 50;  // MEM_SHORT_EXT
-            bool decline = qb <= 10 || qe >= L - 10;
-            rb = rb > 0 ? rb : 0;
-            re = re < l2 ? re : l2;
-            if (rb < P.l_pac && P.l_pac < re) {
-                if (S[0].rbeg < P.l_pac) re = P.l_pac;
-                else rb = P.l_pac;
-            }
-            decline = decline || (re - rb) - (qe - qb) > 50 || (qe - qb) - (re - rb) > 50;
-            decline = decline || qe - qb >= P.w * 4 || re - rb >= P.w * 4;
-            decline = decline || qe - qb >= 200 || re - rb >= 200;  // MEM_SHORT_LEN
-            r0 = r0 > 0 ? r0 : 0;
-            r1 = r1 < l2 ? r1 : l2;
-            if (r0 < P.l_pac && P.l_pac < r1) {
-                if (S[0].rbeg < P.l_pac) r1 = P.l_pac;
-                else r0 = P.l_pac;
-            }
-            P.span[2 * c] = r0;
-            P.span[2 * c + 1] = r1;
-            P.sdec[c] = (uint8_t)decline;
-            if (decline) P.tasks[atomicAdd(&P.lq[LQ_NTASK], 1u)] = RegTask{c, (uint32_t)r, (uint32_t)top};
+        const SeedRec* S = P.seeds + ch.seed_off;
+        int64_t qb = L, qe = 0, rb = l2, re = 0, r0 = l2, r1 = 0;
+        uint64_t best = 0;
+        int top = 0;
+        for (int i = 0; i < ch.n; ++i) {
+            const SeedRec s = S[i];
+            qb = s.qbeg < qb ? s.qbeg : qb;
+            qe = s.qbeg + s.len > qe ? s.qbeg + s.len : qe;
+            rb = s.rbeg < rb ? s.rbeg : rb;
+            re = s.rbeg + s.len > re ? s.rbeg + s.len : re;
+            const int64_t b = s.rbeg - (s.qbeg + max_gap(P, s.qbeg));
+            const int64_t e = s.rbeg + s.len + ((L - s.qbeg - s.len) + max_gap(P, L - s.qbeg - s.len));
+            r0 = b < r0 ? b : r0;
+            r1 = e > r1 ? e : r1;
+            const uint64_t key = (uint64_t)(uint32_t)s.len << 32 | (uint32_t)i;  // distinct: the largest is srt[n - 1]
+            if (key > best) best = key, top = i;
+            P.pre_ok[ch.seed_off + i] = 0;
+        }
+        qb -= 50, qe += 50, rb -= 50, re += 50;  // MEM_SHORT_EXT
+        bool decline = qb <= 10 || qe >= L - 10;
+        rb = rb > 0 ? rb : 0;
+        re = re < l2 ? re : l2;
+        if (rb < P.l_pac && P.l_pac < re) {
+            if (S[0].rbeg < P.l_pac) re = P.l_pac;
+            else rb = P.l_pac;
+        }
+        decline = decline || (re - rb) - (qe - qb) > 50 || (qe - qb) - (re - rb) > 50;
+        decline = decline || qe - qb >= P.w * 4 || re - rb >= P.w * 4;
+        decline = decline || qe - qb >= 200 || re - rb >= 200;  // MEM_SHORT_LEN
+        r0 = r0 > 0 ? r0 : 0;
+        r1 = r1 < l2 ? r1 : l2;
+        if (r0 < P.l_pac && P.l_pac < r1) {
+            if (S[0].rbeg < P.l_pac) r1 = P.l_pac;
+            else r0 = P.l_pac;
+        }
+        P.span[2 * (uint64_t)c] = r0;
+        P.span[2 * (uint64_t)c + 1] = r1;
+        P.sdec[c] = (uint8_t)decline;
+        if (!heavy) {
+            if (decline) P.tasks[atomicAdd(&P.lq[LQ_NTASK], 1u)] = RegTask{c, r, (uint32_t)top};
+        } else if (decline) {
+            const uint32_t base = atomicAdd(&P.lq[LQ_NTASK], (uint32_t)ch.n);
+            for (int i = 0; i < ch.n; ++i) P.tasks[base + i] = RegTask{c, r, (uint32_t)i};
+        } else {
+            P.swlist[atomicAdd(&P.lq[LQ_NSW], 1u)] = c;
+        }
+    }
+}
+
+// the listed heavy chains, one wave each: mem_chain2aln_short's SW (its
+// region to pre_short, short_ok = 1), or, when it declines, every seed as a task
+__global__ __launch_bounds__(256) void aln_heavy_sw_kernel(AlnParams P) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = P.lq[LQ_NSW];
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t k = wave; k < n; k += n_waves) {
+        const uint32_t c = (uint32_t)uni((int)P.swlist[k]);
+        const uint32_t r = (uint32_t)uni((int)(P.chain_read[c] & 0x7fffffffu));
+        const uint64_t q0 = P.offs[r];
+        const int L = uni((int)(P.offs[r + 1] - q0));
+        OutChain ch = P.chains[c];
+        ch.n = uni(ch.n);
+        const SeedRec* S = P.seeds + ch.seed_off;
+        const int ok = chain_short(P, P.codes + q0, L, S, ch.n, P.pre_short + c, lane, P.ctr + 12) == 0;
+        if (lane == 0) P.short_ok[c] = (uint8_t)ok;
+        if (!ok) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&P.lq[LQ_NTASK], (uint32_t)ch.n);
+            base = (uint32_t)uni((int)base);
+            for (int i = lane; i < ch.n; i += 64) P.tasks[base + i] = RegTask{c, r, (uint32_t)i};
         }
     }
 }
@@ -1077,6 +1128,7 @@ __global__ __launch_bounds__(256, KC > 4 ? 1 : 4) void aln_region_rest_kernel(Al
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t t = wave; t < n; t += n_waves) {
         if (!uni((int)P.tfail[t])) continue;
+        if (lane == 0) atomicAdd(&P.ctr[14], 1u);  // SMEM_ALN_STATS: tasks left by the lanes
         const RegTask R = P.tasks[t];
         const uint64_t q0 = P.offs[R.r];
         const int L = uni((int)(P.offs[R.r + 1] - q0));
@@ -1207,13 +1259,17 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
     return hipGetLastError();
 }
 
-// the lane path between the heavy chain tasks and the walks: the light
-// reads' tasks, then per pass (left, right) the sort and the three tiers of
-// the lane engine, then the coverage pass (P->lq zeroed by the caller)
-extern "C" hipError_t smem_launch_aln_lane(const smem::AlnParams* P, int n_cu, hipStream_t st) {
+// the lane path before the walks: every chain's prep and tasks, the heavy
+// chains' SWs, then per pass (left, right) the sort and the three tiers of
+// the lane engine, the coverage pass and the tasks the lanes left (P->lq
+// zeroed by the caller)
+extern "C" hipError_t smem_launch_aln_lane(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;
     const int rb = std::max(1, std::min(n_cu * 4, (P->n_reads + 255) / 256));
-    hipLaunchKernelGGL(smem::aln_light_prep_kernel, dim3(rb), dim3(256), 0, st, *P);
+    const int cb = std::max<int>(1, (int)std::min<uint64_t>((uint64_t)n_cu * 8, (n_chains + 255) / 256));
+    hipLaunchKernelGGL(smem::aln_chain_read_kernel, dim3(rb), dim3(256), 0, st, *P);
+    hipLaunchKernelGGL(smem::aln_chain_prep_kernel, dim3(cb), dim3(256), 0, st, *P, (uint32_t)n_chains);
+    hipLaunchKernelGGL(smem::aln_heavy_sw_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
     for (int side = 0; side < 2; ++side) {
         hipError_t e = hipMemsetAsync(P->lq + smem::LQ_HIST, 0, sizeof(uint32_t) * smem::LQ_BUCKETS, st);
         if (e != hipSuccess) return e;

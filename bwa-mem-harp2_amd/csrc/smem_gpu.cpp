@@ -159,13 +159,14 @@ struct AlnHeavyBufs {
     DevBuf<uint8_t> short_ok, pre_ok, tmp;
     // the lane path (regions computed ahead one seed per lane)
     DevBuf<smem::RegTask> tasks;
-    DevBuf<uint32_t> torder, lq;
+    DevBuf<uint32_t> torder, lq, chain_read, swlist;
     DevBuf<uint8_t> tfail, sdec;
     void release() {
         heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); ht.release(); rnext.release();
         pre.release();
         pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
-        tasks.release(); torder.release(); lq.release(); tfail.release(); sdec.release();
+        tasks.release(); torder.release(); lq.release(); tfail.release(); sdec.release(); chain_read.release();
+        swlist.release();
     }
 };
 
@@ -1360,11 +1361,13 @@ static bool aln_lane_on() {
 // computed ahead, the walk's regions taken from them / computed serially)
 static int aln_guard_check(const smem::AlnParams& P, hipStream_t st) {
     if (getenv("SMEM_ALN_STATS")) {
-        uint32_t c[3] = {0, 0, 0};
-        HIP_TRY(hipMemcpyAsync(c, P.ctr + 8, sizeof(c), hipMemcpyDeviceToHost, st));
+        uint32_t c[smem::ALN_CTRS], nt = 0;
+        HIP_TRY(hipMemcpyAsync(c, P.ctr, sizeof(c), hipMemcpyDeviceToHost, st));
+        if (P.lane_on) HIP_TRY(hipMemcpyAsync(&nt, P.lq + smem::LQ_NTASK, sizeof(nt), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        fprintf(stderr, "[smem aln] heavy path: %u seed regions computed ahead, %u used by the walks, %u computed "
-                        "serially in the walks\n", c[0], c[1], c[2]);
+        fprintf(stderr, "[smem aln] heavy path: %u reads, %u chains (%u ran mem_chain2aln_short's SW), %u seed regions "
+                        "computed ahead, %u used by the walks, %u computed serially in the walks; lane tasks %u "
+                        "(%u left to one wave each)\n", c[2], c[11], c[12], c[8], c[9], c[10], nt, c[14]);
     }
     if (!P.walk_guard) return SMEM_OK;
     uint32_t trips = 0;
@@ -1403,9 +1406,14 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.torder.grow(nt));
         HIP_TRY(H.tfail.grow(nt));
         HIP_TRY(H.lq.grow(smem::LQ_WORDS));
+        HIP_TRY(H.chain_read.grow(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.swlist.grow(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.short_ok.grow(std::max<uint64_t>(n_chains, 1)));
+        HIP_TRY(H.pre_short.grow(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(hipMemsetAsync(H.lq.p, 0, sizeof(uint32_t) * smem::LQ_WORDS, st));
         P.pre = H.pre.p, P.pre_ok = H.pre_ok.p, P.span = H.span.p, P.sdec = H.sdec.p;
         P.tasks = H.tasks.p, P.torder = H.torder.p, P.tfail = H.tfail.p, P.lq = H.lq.p;
+        P.chain_read = H.chain_read.p, P.swlist = H.swlist.p, P.short_ok = H.short_ok.p, P.pre_short = H.pre_short.p;
     }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
@@ -1417,7 +1425,11 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(hipMemcpyAsync(&n_heavy, P.ctr + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
-    if (n_heavy) {
+    if (n_heavy && P.lane_on) {  // the walk's scratch (its chains were prepared by the lane path)
+        HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+        HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
+        P.ht = H.ht.p, P.rnext = H.rnext.p;
+    } else if (n_heavy) {
         HIP_TRY(H.hoff.grow(n_heavy + 1));
         size_t tb = 0;
         HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)n_heavy, nullptr, &tb, st));
@@ -1436,11 +1448,10 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
     }
     if (P.lane_on) {
-        // heavy chain tasks (they list their seeds as tasks), the lane engine's
-        // passes over every task, then the walks: the heavy one on st, the
-        // light reads beside it on st2
-        if (n_heavy) HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 1, st));
-        HIP_TRY(smem_launch_aln_lane(&P, g->n_cu, st));
+        // every chain prepared and its tasks listed, the lane engine's passes
+        // over every task, then the walks: the heavy one on st, the light
+        // reads beside it on st2
+        HIP_TRY(smem_launch_aln_lane(&P, n_chains, g->n_cu, st));
         if (n_heavy && st2 && ev_join) {
             HIP_TRY(hipEventRecord(ev_join, st));
             HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
