@@ -93,6 +93,10 @@ struct AlnParams {
     uint8_t* sdec;            // [n_chains] light chains: 1 when mem_chain2aln_short declines before its SW
     uint32_t* lq;             // [LQ_WORDS] the lane path's counters, queue bounds and histogram
     uint32_t* chain_read;     // [n_chains] the read of each chain, bit 31: a heavy read
+    // the heavy reads' task list (the prep kernels write it beside tasks / lq,
+    // the light reads' list; the two lists run their passes on two streams)
+    RegTask* htasks;
+    uint32_t* hlq;
     uint32_t* swlist;         // [n_chains] heavy chains whose mem_chain2aln_short runs its SW (lq[LQ_NSW] of them)
     // compaction
     const uint64_t* reg_off;  // [n_reads + 1]
@@ -131,6 +135,9 @@ hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st);
 // parts: 1 the chain tasks, 2 the walk, 3 both
 hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, int parts, hipStream_t st);
 // lane_on: the regions computed ahead one seed per lane, before the walks
-// (lq zeroed; the heavy reads classified: heavy_min / heavy_seeds set)
-hipError_t smem_launch_aln_lane(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st);
+// (lq / hlq zeroed; heavy_min / heavy_seeds set): every chain's prep and
+// tasks (light reads' to tasks / lq, heavy reads' to htasks / hlq), then, per
+// list (P with tasks / lq, torder, tfail of that list), the passes
+hipError_t smem_launch_aln_prep(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st);
+hipError_t smem_launch_aln_passes(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st);
 }

@@ -37,10 +37,15 @@ __device__ __forceinline__ int ref_at(const AlnParams& P, int64_t p) {
     return p < P.l_pac ? pac_at(P.pac, p) : 3 - pac_at(P.pac, (P.l_pac << 1) - 1 - p);
 }
 
-// cal_max_gap (software/bwamem.c:854-861)
+// cal_max_gap (software/bwamem.c:854-861) in integers: (int)(x / e + 1.) with
+// x = qlen a - o is trunc(x / e + 1) = (x + e) / e (C division truncates; the
+// double quotient is exact when e divides x and otherwise at least 1/e from
+// an integer, far past its rounding), without the double divisions (a
+// containment test of the heavy-read walk makes two per region)
+__device__ __forceinline__ int gap_div(int x, int e) { return e == 1 ? x + 1 : (x + e) / e; }
 __device__ __forceinline__ int max_gap(const AlnParams& P, int qlen) {
-    const int l_del = (int)((double)(qlen * P.a - P.o_del) / P.e_del + 1.);
-    const int l_ins = (int)((double)(qlen * P.a - P.o_ins) / P.e_ins + 1.);
+    const int l_del = gap_div(qlen * P.a - P.o_del, P.e_del);
+    const int l_ins = gap_div(qlen * P.a - P.o_ins, P.e_ins);
     int l = l_del > l_ins ? l_del : l_ins;
     l = l > 1 ? l : 1;
     return l < P.w << 1 ? l : P.w << 1;
@@ -641,6 +646,7 @@ template <int KC, bool GUARD>
 __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) {
     const int lane = threadIdx.x & 63;
     uint32_t guard = 0;
+    const uint64_t t_read = P.cyc ? __builtin_amdgcn_s_memtime() : 0;  // SMEM_ALN_CYCLES
     const int L = uni((int)(P.offs[r + 1] - P.offs[r]));
     const uint8_t* query = P.codes + P.offs[r];
     const uint64_t c0 = uni64(P.chain_off[r]), c1 = uni64(P.chain_off[r + 1]);
@@ -804,6 +810,7 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
         P.n_regs[r] = (uint64_t)nreg;
         if (n_used) atomicAdd(&P.ctr[9], n_used);
         if (n_serial) atomicAdd(&P.ctr[10], n_serial);
+        if (P.cyc) P.cyc[r] = __builtin_amdgcn_s_memtime() - t_read;
     }
 }
 #undef WALK_GUARD
@@ -920,10 +927,10 @@ __global__ __launch_bounds__(256) void aln_chain_prep_kernel(AlnParams P, uint32
         if (!heavy) {
             if (decline) P.tasks[atomicAdd(&P.lq[LQ_NTASK], 1u)] = RegTask{c, r, (uint32_t)top};
         } else if (decline) {
-            const uint32_t base = atomicAdd(&P.lq[LQ_NTASK], (uint32_t)ch.n);
-            for (int i = 0; i < ch.n; ++i) P.tasks[base + i] = RegTask{c, r, (uint32_t)i};
+            const uint32_t base = atomicAdd(&P.hlq[LQ_NTASK], (uint32_t)ch.n);
+            for (int i = 0; i < ch.n; ++i) P.htasks[base + i] = RegTask{c, r, (uint32_t)i};
         } else {
-            P.swlist[atomicAdd(&P.lq[LQ_NSW], 1u)] = c;
+            P.swlist[atomicAdd(&P.hlq[LQ_NSW], 1u)] = c;
         }
     }
 }
@@ -932,7 +939,7 @@ __global__ __launch_bounds__(256) void aln_chain_prep_kernel(AlnParams P, uint32
 // region to pre_short, short_ok = 1), or, when it declines, every seed as a task
 __global__ __launch_bounds__(256) void aln_heavy_sw_kernel(AlnParams P) {
     const int lane = threadIdx.x & 63;
-    const uint32_t n = P.lq[LQ_NSW];
+    const uint32_t n = P.hlq[LQ_NSW];
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t k = wave; k < n; k += n_waves) {
         const uint32_t c = (uint32_t)uni((int)P.swlist[k]);
@@ -946,9 +953,9 @@ __global__ __launch_bounds__(256) void aln_heavy_sw_kernel(AlnParams P) {
         if (lane == 0) P.short_ok[c] = (uint8_t)ok;
         if (!ok) {
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&P.lq[LQ_NTASK], (uint32_t)ch.n);
+            if (lane == 0) base = atomicAdd(&P.hlq[LQ_NTASK], (uint32_t)ch.n);
             base = (uint32_t)uni((int)base);
-            for (int i = lane; i < ch.n; i += 64) P.tasks[base + i] = RegTask{c, r, (uint32_t)i};
+            for (int i = lane; i < ch.n; i += 64) P.htasks[base + i] = RegTask{c, r, (uint32_t)i};
         }
     }
 }
@@ -1260,16 +1267,22 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
 }
 
 // the lane path before the walks: every chain's prep and tasks, the heavy
-// chains' SWs, then per pass (left, right) the sort and the three tiers of
-// the lane engine, the coverage pass and the tasks the lanes left (P->lq
-// zeroed by the caller)
-extern "C" hipError_t smem_launch_aln_lane(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st) {
+// chains' SWs (smem_launch_aln_prep); then, per task list, per pass (left,
+// right) the sort and the three tiers of the lane engine, the coverage pass
+// and the tasks the lanes left (smem_launch_aln_passes; long_reads: the batch
+// holds reads past 256 bp)
+extern "C" hipError_t smem_launch_aln_prep(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;
     const int rb = std::max(1, std::min(n_cu * 4, (P->n_reads + 255) / 256));
     const int cb = std::max<int>(1, (int)std::min<uint64_t>((uint64_t)n_cu * 8, (n_chains + 255) / 256));
     hipLaunchKernelGGL(smem::aln_chain_read_kernel, dim3(rb), dim3(256), 0, st, *P);
     hipLaunchKernelGGL(smem::aln_chain_prep_kernel, dim3(cb), dim3(256), 0, st, *P, (uint32_t)n_chains);
     hipLaunchKernelGGL(smem::aln_heavy_sw_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_passes(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st) {
+    if (P->n_reads <= 0) return hipSuccess;
     for (int side = 0; side < 2; ++side) {
         hipError_t e = hipMemsetAsync(P->lq + smem::LQ_HIST, 0, sizeof(uint32_t) * smem::LQ_BUCKETS, st);
         if (e != hipSuccess) return e;
@@ -1282,7 +1295,7 @@ extern "C" hipError_t smem_launch_aln_lane(const smem::AlnParams* P, uint64_t n_
     }
     hipLaunchKernelGGL(smem::aln_region_cov_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
     hipLaunchKernelGGL(smem::aln_region_rest_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
-    hipLaunchKernelGGL(smem::aln_region_rest_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
+    if (long_reads) hipLaunchKernelGGL(smem::aln_region_rest_kernel<16>, dim3(n_cu * 2), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

@@ -158,15 +158,15 @@ struct AlnHeavyBufs {
     DevBuf<smem::AlnReg> pre, pre_short, loc;
     DevBuf<uint8_t> short_ok, pre_ok, tmp;
     // the lane path (regions computed ahead one seed per lane)
-    DevBuf<smem::RegTask> tasks;
-    DevBuf<uint32_t> torder, lq, chain_read, swlist;
-    DevBuf<uint8_t> tfail, sdec;
+    DevBuf<smem::RegTask> tasks, htasks;
+    DevBuf<uint32_t> torder, lq, chain_read, swlist, htorder, hlq;
+    DevBuf<uint8_t> tfail, sdec, htfail;
     void release() {
         heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); ht.release(); rnext.release();
         pre.release();
         pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
         tasks.release(); torder.release(); lq.release(); tfail.release(); sdec.release(); chain_read.release();
-        swlist.release();
+        swlist.release(); htasks.release(); htorder.release(); hlq.release(); htfail.release();
     }
 };
 
@@ -1363,11 +1363,14 @@ static int aln_guard_check(const smem::AlnParams& P, hipStream_t st) {
     if (getenv("SMEM_ALN_STATS")) {
         uint32_t c[smem::ALN_CTRS], nt = 0;
         HIP_TRY(hipMemcpyAsync(c, P.ctr, sizeof(c), hipMemcpyDeviceToHost, st));
+        uint32_t nht = 0;
         if (P.lane_on) HIP_TRY(hipMemcpyAsync(&nt, P.lq + smem::LQ_NTASK, sizeof(nt), hipMemcpyDeviceToHost, st));
+        if (P.lane_on) HIP_TRY(hipMemcpyAsync(&nht, P.hlq + smem::LQ_NTASK, sizeof(nht), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         fprintf(stderr, "[smem aln] heavy path: %u reads, %u chains (%u ran mem_chain2aln_short's SW), %u seed regions "
                         "computed ahead, %u used by the walks, %u computed serially in the walks; lane tasks %u "
-                        "(%u left to one wave each)\n", c[2], c[11], c[12], c[8], c[9], c[10], nt, c[14]);
+                        "light + %u heavy (%u left to one wave each)\n", c[2], c[11], c[12], c[8], c[9], c[10], nt,
+                nht, c[14]);
     }
     if (!P.walk_guard) return SMEM_OK;
     uint32_t trips = 0;
@@ -1397,7 +1400,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
     }
     P.lane_on = aln_lane_on() && n > 0 ? 1u : 0u;
     if (P.lane_on) {
-        const uint64_t nt = std::max<uint64_t>(n_seeds + n_chains, 1);
+        const uint64_t nt = std::max<uint64_t>(n_chains, 1), nht = std::max<uint64_t>(n_seeds, 1);
         HIP_TRY(H.pre.grow(std::max<uint64_t>(n_seeds, 1)));
         HIP_TRY(H.pre_ok.grow(std::max<uint64_t>(n_seeds, 1)));
         HIP_TRY(H.span.grow(2 * std::max<uint64_t>(n_chains, 1)));
@@ -1406,6 +1409,11 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.torder.grow(nt));
         HIP_TRY(H.tfail.grow(nt));
         HIP_TRY(H.lq.grow(smem::LQ_WORDS));
+        HIP_TRY(H.htasks.grow(nht));
+        HIP_TRY(H.htorder.grow(nht));
+        HIP_TRY(H.htfail.grow(nht));
+        HIP_TRY(H.hlq.grow(smem::LQ_WORDS));
+        HIP_TRY(hipMemsetAsync(H.hlq.p, 0, sizeof(uint32_t) * smem::LQ_WORDS, st));
         HIP_TRY(H.chain_read.grow(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(H.swlist.grow(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(H.short_ok.grow(std::max<uint64_t>(n_chains, 1)));
@@ -1414,6 +1422,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         P.pre = H.pre.p, P.pre_ok = H.pre_ok.p, P.span = H.span.p, P.sdec = H.sdec.p;
         P.tasks = H.tasks.p, P.torder = H.torder.p, P.tfail = H.tfail.p, P.lq = H.lq.p;
         P.chain_read = H.chain_read.p, P.swlist = H.swlist.p, P.short_ok = H.short_ok.p, P.pre_short = H.pre_short.p;
+        P.htasks = H.htasks.p, P.hlq = H.hlq.p;
     }
     uint32_t n_heavy = 0;
     if (P.heavy_min && n > 0) {
@@ -1448,23 +1457,33 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
     }
     if (P.lane_on) {
-        // every chain prepared and its tasks listed, the lane engine's passes
-        // over every task, then the walks: the heavy one on st, the light
-        // reads beside it on st2
-        HIP_TRY(smem_launch_aln_lane(&P, n_chains, g->n_cu, st));
+        // every chain prepared and its tasks listed; then the heavy reads'
+        // tasks' passes and their walk (the critical path: one wave walks a
+        // read's thousands of chains) on st, beside the light reads' passes and
+        // walk on st2
+        const int lr = long_reads ? 1 : 0;
+        HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, st));
+        smem::AlnParams Ph = P;  // the heavy list
+        Ph.tasks = H.htasks.p, Ph.torder = H.htorder.p, Ph.tfail = H.htfail.p, Ph.lq = H.hlq.p;
         if (n_heavy && st2 && ev_join) {
             HIP_TRY(hipEventRecord(ev_join, st));
             HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
-            HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 2, st));
+            HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
+            HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));
+            HIP_TRY(smem_launch_aln_passes(&P, g->n_cu, lr, st2));
             P.light_claims = aln_light_claims();
-            HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st2));
+            HIP_TRY(smem_launch_aln(&P, g->n_cu, lr, st2));
             P.light_claims = 0;
             HIP_TRY(hipEventRecord(ev_join, st2));
             HIP_TRY(hipStreamWaitEvent(st, ev_join, 0));
             return SMEM_OK;
         }
-        if (n_heavy) HIP_TRY(smem_launch_aln_heavy(&P, g->n_cu, long_reads ? 1 : 0, 2, st));
-        HIP_TRY(smem_launch_aln(&P, g->n_cu, long_reads ? 1 : 0, st));
+        if (n_heavy) {
+            HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
+            HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));
+        }
+        HIP_TRY(smem_launch_aln_passes(&P, g->n_cu, lr, st));
+        HIP_TRY(smem_launch_aln(&P, g->n_cu, lr, st));
         return SMEM_OK;
     }
     if (n_heavy) {

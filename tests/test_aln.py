@@ -93,12 +93,16 @@ def _heavy_env(monkeypatch, heavy):
     then always uses the region bin hash (SMEM_ALN_HASH_MIN = 1).  A "/1"
     suffix: the light and heavy reads' kernels one after the other on the
     batch's stream (SMEM_ALN_STREAMS=1) instead of side by side."""
-    if heavy and heavy.endswith("+inline"):
-        # the heavy-read walk inlined into its kernel (the round-2 hang's
-        # shape), every loop iteration counted against a guard: a walk that
-        # would spin fails the call instead of hanging
-        heavy = heavy[:-len("+inline")]
-        monkeypatch.setenv("SMEM_ALN_WALK_INLINE", "1")
+    while heavy and "+" in heavy:
+        heavy, _, opt = heavy.rpartition("+")
+        if opt == "inline":
+            # the heavy-read walk inlined into its kernel (the round-2 hang's
+            # shape), every loop iteration counted against a guard: a walk that
+            # would spin fails the call instead of hanging
+            monkeypatch.setenv("SMEM_ALN_WALK_INLINE", "1")
+        elif opt == "nolane":
+            # no regions computed ahead one seed per lane (SMEM_ALN_LANE=0)
+            monkeypatch.setenv("SMEM_ALN_LANE", "0")
     if heavy and "/" in heavy:
         heavy, _, streams = heavy.partition("/")
         monkeypatch.setenv("SMEM_ALN_STREAMS", streams)
@@ -137,7 +141,8 @@ def test_pack_matches_reference_pac():
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,a,heavy", [(100, 1, None), (20, 1, None), (100, 2, None), (100, 1, "1"), (100, 2, "1"),
                                        (20, 1, "3"), (100, 1, "0"), (100, 1, "1000:3"), (100, 1, "3/1"),
-                                       (100, 1, "1+inline"), (100, 2, "3+inline")])
+                                       (100, 1, "1+inline"), (100, 2, "3+inline"), (100, 1, "0+nolane"),
+                                       (100, 1, "1+nolane"), (100, 2, "3+nolane")])
 def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a, heavy, monkeypatch):
     """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
     kernel instantiations) with substitutions and Ns; chains from the GPU
