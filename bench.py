@@ -120,6 +120,8 @@ def parse(argv=None):
                         "full resident batch, for rocprofv3 summaries)")
     p.add_argument("--e2e-reads", type=int, default=1_000_000,
                    help="reads of the end-to-end leg (bwa-gpu mem vs the reference pipeline; 0: skip; N=1 only)")
+    p.add_argument("--e2e-pairs", type=int, default=250_000,
+                   help="e2e: also this many interleaved pairs through bwa-gpu mem -p vs the reference (0: skip)")
     p.add_argument("--e2e-batch", type=int, default=0, help="-b of bwa-gpu mem (0: reads / threads)")
     p.add_argument("--human-like", type=int, default=1,
                    help="1: also measure the seeding step on the human-like genome profile (N=1 only)")
@@ -630,7 +632,6 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
     tests/test_bwa_integration.py).  Timed: each process's wall clock
     (index load + upload included) and the reference's own per-chunk
     mem_process_seqs real time.  SAM identity is checked on every read."""
-    import subprocess
     from smemgpu import synth
     if not (os.path.exists(BWA_GPU) and os.path.exists(REF_HARNESS)) or args.e2e_reads <= 0:
         return None
@@ -652,38 +653,73 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
     with tempfile.TemporaryDirectory(dir=args.cache) as d:
         fq = os.path.join(d, "r.fq")
         synth.write_fastq(fq, sub)
-        runs = {}
         env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu))
         legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq], {}),
                 ("gpu_chains_only", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq],
                  {"SMEM_GPU_STAGES": "1"}),
                 ("reference", [REF_HARNESS, "mem", base, fq, str(threads), "1", "0"], {})]
-        for name, cmd, env in legs:
-            sam = os.path.join(d, name + ".sam")
-            t = time.perf_counter()
-            with open(sam, "wb") as fh:
-                p = subprocess.run(cmd, stdout=fh, stderr=subprocess.PIPE, env=dict(env_base, **env), timeout=900)
-            wall = time.perf_counter() - t
-            err = p.stderr.decode(errors="replace")
-            if p.returncode != 0:
-                log(f"e2e {name} failed ({p.returncode}): {err[-800:]}")
-                return dict(out, error=f"{name} exit {p.returncode}")
-            n_proc, real = _mem_times(err)
-            digest, n_lines = _sam_body(sam)
-            runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
-                          "outside_mem_process_seqs_s": round(wall - real, 3),
-                          "reads_per_s_wall": round(m / wall, 1),
-                          "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
-                          "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
-                          "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
-            log(f"e2e {name}: {wall:.1f} s wall, mem_process_seqs {real:.1f} s")
+        runs = _e2e_legs(d, legs, env_base, m)
+        if runs is None:
+            return dict(out, error="a leg failed (see the bench log)")
         out.update(runs)
         out["sam_identical"] = runs["gpu"]["sam_sha256"] == runs["reference"]["sam_sha256"] == \
             runs["gpu_chains_only"]["sam_sha256"]
-        g, r = runs["gpu"], runs["reference"]
-        out["speedup_wall"] = round(r["wall_s"] / g["wall_s"], 2)
-        if g["mem_process_seqs_real_s"] > 0:
-            out["speedup_mem_process_seqs"] = round(r["mem_process_seqs_real_s"] / g["mem_process_seqs_real_s"], 2)
+        out.update(_e2e_speedups(runs))
+        if args.e2e_pairs > 0:
+            # C3's shape at human size: interleaved pairs (insert N(500, 50)), `bwa mem -p`; the
+            # reference pairs each chunk's mates itself (mem_sam_pe, insert statistics per chunk)
+            t = time.time()
+            pe = synth.make_pairs(genome_codes, args.e2e_pairs, args.read_len, seed=args.seed + 7)
+            fq2 = os.path.join(d, "p.fq")
+            synth.write_fastq(fq2, pe, prefix="p", pairs=True)
+            log(f"e2e pe: {args.e2e_pairs} pairs made in {time.time() - t:.1f} s")
+            pbatch = args.e2e_batch or max(1024, 2 * -(-args.e2e_pairs // threads))
+            legs = [("gpu", [BWA_GPU, "mem", "-p", "-t", str(threads), "-b", str(pbatch), base, fq2], {}),
+                    ("reference", [REF_HARNESS, "mem", base, fq2, str(threads), "1", "1"], {})]
+            pr = _e2e_legs(d, legs, env_base, 2 * args.e2e_pairs, tag="pe ")
+            if pr is None:
+                out["pe"] = {"error": "a leg failed (see the bench log)"}
+            else:
+                out["pe"] = {"pairs": args.e2e_pairs, "reads": 2 * args.e2e_pairs, "batch": pbatch,
+                             "insert": "N(500, 50)", **pr,
+                             "sam_identical": pr["gpu"]["sam_sha256"] == pr["reference"]["sam_sha256"],
+                             **_e2e_speedups(pr)}
+    return out
+
+
+def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | None:
+    """Run each (name, argv, env) leg with its SAM into d; wall clock, the
+    reference's own mem_process_seqs real time, SAM digest (minus @PG)."""
+    import subprocess
+    runs = {}
+    for name, cmd, env in legs:
+        sam = os.path.join(d, name + ".sam")
+        t = time.perf_counter()
+        with open(sam, "wb") as fh:
+            p = subprocess.run(cmd, stdout=fh, stderr=subprocess.PIPE, env=dict(env_base, **env), timeout=900)
+        wall = time.perf_counter() - t
+        err = p.stderr.decode(errors="replace")
+        if p.returncode != 0:
+            log(f"e2e {tag}{name} failed ({p.returncode}): {err[-800:]}")
+            return None
+        n_proc, real = _mem_times(err)
+        digest, n_lines = _sam_body(sam)
+        os.unlink(sam)
+        runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
+                      "outside_mem_process_seqs_s": round(wall - real, 3),
+                      "reads_per_s_wall": round(m / wall, 1),
+                      "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
+                      "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
+                      "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
+        log(f"e2e {tag}{name}: {wall:.1f} s wall, mem_process_seqs {real:.1f} s")
+    return runs
+
+
+def _e2e_speedups(runs: dict) -> dict:
+    g, r = runs["gpu"], runs["reference"]
+    out = {"speedup_wall": round(r["wall_s"] / g["wall_s"], 2)}
+    if g["mem_process_seqs_real_s"] > 0:
+        out["speedup_mem_process_seqs"] = round(r["mem_process_seqs_real_s"] / g["mem_process_seqs_real_s"], 2)
     return out
 
 

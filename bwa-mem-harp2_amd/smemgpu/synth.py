@@ -250,8 +250,11 @@ def write_fasta_contigs(path: str, codes: np.ndarray, n_contigs: int = 24, width
                 fh.write(s[k:k + width] + b"\n")
 
 
-def write_fastq(path: str, reads: "Reads", prefix: str = "r", qual: int = 40) -> None:
-    """Reads (codes 0..4) as FASTQ, named <prefix><index>."""
+def write_fastq(path: str, reads: "Reads", prefix: str = "r", qual: int = 40, pairs: bool = False) -> None:
+    """Reads (codes 0..4) as FASTQ, named <prefix><index>; pairs: interleaved
+    mates (make_pairs) named <prefix><index // 2>: bwa mem -p reads them as
+    consecutive pairs (software/fastmap.c:65, 215) and names both mates alike."""
+    sh = 1 if pairs else 0
     acgtn = np.frombuffer(b"ACGTN", dtype=np.uint8)
     q = chr(33 + qual)
     if reads.n and np.all(reads.lens == reads.lens[0]) and reads.lens[0] > 0:
@@ -263,13 +266,13 @@ def write_fastq(path: str, reads: "Reads", prefix: str = "r", qual: int = 40) ->
         with open(path, "wb") as fh:
             for i0 in range(0, reads.n, 65536):
                 blk = seqs[i0:i0 + 65536]
-                fh.write(b"".join(b"@%s%d\n%s%s" % (prefix.encode(), i0 + k, row.tobytes(), qline)
+                fh.write(b"".join(b"@%s%d\n%s%s" % (prefix.encode(), (i0 + k) >> sh, row.tobytes(), qline)
                                   for k, row in enumerate(blk)))
         return
     with open(path, "wb") as fh:
         for i in range(reads.n):
             s = acgtn[np.minimum(reads.read(i), 4)].tobytes()
-            fh.write(b"@%s%d\n%s\n+\n%s\n" % (prefix.encode(), i, s, (q * len(s)).encode()))
+            fh.write(b"@%s%d\n%s\n+\n%s\n" % (prefix.encode(), i >> sh, s, (q * len(s)).encode()))
 
 
 def forward_reverse_text(codes: np.ndarray) -> np.ndarray:

@@ -173,3 +173,44 @@ def test_human_sa_lookup(human):
         assert int(np.count_nonzero(res.sa_pos >= 2 ** 32)) > 100
     finally:
         osa.close()
+
+
+@pytest.mark.timeout(900)
+def test_human_pe_sam_identical(human, tmp_path):
+    """C3's shape at human size through the product path: 20k interleaved
+    pairs (150 bp, insert N(500, 50)) on the 6.2 G-symbol index, `bwa-gpu mem
+    -p -t 16` (seeding -> regions on the GPU, pairing / mate rescue / SAM on
+    the CPU) against the unpatched reference pipeline (`ref_harness mem`,
+    -b 1, every batch on the CPU) on the same index files: SAM byte-identical
+    apart from @PG (software/fastmap.c:213-228 -> software/bwamem.c:1614)."""
+    import os
+    import subprocess
+    from smemgpu import synth
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bwa = os.path.join(root, "oracle", "_ref", "bwa-gpu")
+    ref = os.path.join(root, "oracle", "_ref", "ref_harness")
+    if not (os.path.exists(bwa) and os.path.exists(ref)):
+        pytest.skip("oracle/_ref/bwa-gpu / ref_harness not built (need /root/reference at build time)")
+    base = str(tmp_path / "h")
+    human["idx"].write(base + ".bwt")
+    human["sa"].write(base + ".sa")
+    synth.write_bwa_bns(base, human["codes"])
+    pe = synth.make_pairs(human["codes"], 20_000, 150, seed=11)
+    fq = str(tmp_path / "p.fq")
+    synth.write_fastq(fq, pe, prefix="p", pairs=True)
+    sams = {}
+    for name, cmd in (("gpu", [bwa, "mem", "-p", "-t", "16", "-b", "2500", base, fq]),
+                      ("ref", [ref, "mem", base, fq, "16", "1", "1"])):
+        p = subprocess.run(cmd, capture_output=True, timeout=600, env=dict(os.environ, SMEM_GPU_DEVICES="0"))
+        err = p.stderr.decode(errors="replace")
+        assert p.returncode == 0, err[-2000:]
+        if name == "gpu":
+            assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
+        sams[name] = [l for l in p.stdout.split(b"\n") if l and not l.startswith(b"@PG")]
+    got, want = sams["gpu"], sams["ref"]
+    assert len(got) == len(want) > 40_000
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert not bad, f"{len(bad)} SAM lines differ, first: {got[bad[0]][:200]!r} vs {want[bad[0]][:200]!r}"
+    # pairs really were paired: most records carry a mate on the same contig (RNEXT "=")
+    paired = sum(1 for l in got if not l.startswith(b"@") and l.split(b"\t")[6] == b"=")
+    assert paired > 0.8 * 40_000
