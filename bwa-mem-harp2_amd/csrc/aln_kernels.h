@@ -61,7 +61,8 @@ struct AlnParams {
     AlnReg* raw;       // read r's regions at raw[seed_off[r] ..)
     uint64_t* n_regs;  // [n_reads]
     uint32_t* ctr;     // [ALN_CTRS]: work-queue heads (reads <= 256 bp, longer), heavy-read count, heavy-path heads
-    uint64_t* cyc;     // diagnostics (SMEM_ALN_CYCLES): [n_reads] shader cycles per read, nullptr: off
+    uint64_t* cyc;     // diagnostics (SMEM_ALN_CYCLES): [n_reads] shader cycles per read, then [4 n_reads]
+                       // the heavy walk's split (smem_gpu.cpp), nullptr: off
     uint64_t* split;   // diagnostics (SMEM_ALN_SPLIT): [ALN_SPLITS] aln_kernel's cycles by phase and counts, nullptr: off
     // heavy reads (at least heavy_min chains or heavy_seeds seeds; 0 = none):
     // every chain walked ahead on its own, one wave per chain, then the read's

@@ -573,11 +573,15 @@ __device__ __forceinline__ bool reg_contains(const AlnParams& P, int64_t s_rb, i
 }
 
 // A heavy read's regions hashed by 512-bp reference bin of their start, in
-// a per-wave table of ALN_HT slots in global memory: slot = bin << 20 |
-// (index of the bin's newest region + 1), 0 = empty; older regions of a bin
-// chain through rnext.  A region contains a seed only if it starts within
-// the read's longest region before the seed, so a containment test visits
-// one or two bins instead of every region made so far.
+// a per-wave table of ALN_HT slots in global memory: slot = the bin's region
+// count << 44 | bin << 20 | (index of the bin's newest region + 1), 0 =
+// empty; older regions of a bin chain through rnext.  A region contains a
+// seed only if it starts within the read's longest region before the seed,
+// so a containment test visits one or two bins instead of every region made
+// so far -- unless those bins hold more regions than a scan of all of them
+// 64 at a time takes rounds (a tandem-repeat read piles its regions into a
+// few bins: one round trip per hop made a 2,000-region read's walk 19 ms of
+// dependent loads), and then it scans.
 constexpr int HT_BIN = 9;
 // Fibonacci hashing onto all ALN_HT slots (the top log2(ALN_HT) bits of the product)
 constexpr uint32_t ALN_HT_BITS = __builtin_ctz((unsigned)ALN_HT);
@@ -591,7 +595,7 @@ __device__ __forceinline__ int ht_find(const uint64_t* ht, uint64_t bin, int lan
     for (int w = 0; w < ALN_HT / 64; ++w) {
         const uint32_t sl = (h + (uint32_t)lane) & (ALN_HT - 1);
         const uint64_t e = ht[sl];
-        const uint64_t m = __ballot(e == 0 || (e >> 20) == bin);
+        const uint64_t m = __ballot(e == 0 || ((e >> 20) & 0xFFFFFFu) == bin);
         if (m) {
             const int f = __builtin_ctzll(m);
             entry = rl64(e, f);
@@ -609,7 +613,7 @@ __device__ __forceinline__ void ht_insert(uint64_t* ht, int32_t* rnext, int64_t 
     const int sl = uni(ht_find(ht, bin, lane, e));
     if (lane == 0) {
         rnext[idx] = e ? (int32_t)(e & 0xFFFFF) - 1 : -1;
-        if (sl >= 0) ht[sl] = bin << 20 | (uint64_t)(idx + 1);
+        if (sl >= 0) ht[sl] = ((e >> 44) + 1) << 44 | bin << 20 | (uint64_t)(idx + 1);
     }
     __threadfence_block();  // the next probe of this wave must see the slot
 }
@@ -657,11 +661,13 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
     // the bin hash, for reads with many regions (not with more than the
     // table holds, or than 20-bit indices do)
     const uint64_t cap = uni64(P.seed_off[r + 1] - P.seed_off[r]);
-    const bool hashed = c1 - c0 >= P.hash_min && cap < (1u << 20) - 1 && cap + (c1 - c0) < ALN_HT / 2;
+    const bool hashed = c1 - c0 >= P.hash_min && cap < (1u << 20) - 1 && cap + (c1 - c0) < ALN_HT / 2 &&
+                        ((uint64_t)(2 * P.l_pac) >> HT_BIN) < (1ull << 24);  // bins fit the slot's 24 bits
     uint64_t* ht = P.ht + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * ALN_HT;
     int32_t* rnext = P.rnext + P.seed_off[r];
     int64_t maxlen = 0;  // the longest region so far
     uint32_t n_used = 0, n_serial = 0;  // regions taken from the chain tasks / computed here (SMEM_ALN_STATS)
+    uint64_t w_full = 0, w_hash = 0, w_big = 0, w_hops = 0;  // SMEM_ALN_CYCLES: the walk's split
     if (hashed) {
         for (int i = lane; i < ALN_HT; i += 64) ht[i] = 0;
         __threadfence_block();
@@ -686,12 +692,17 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             continue;
         }
         const SeedRec* S = P.seeds + ch.seed_off;
-        if (n > 64) {
+        if (n > 128) {
             __threadfence_block();
             const int before = nreg;
+            const uint64_t tf = P.cyc ? __builtin_amdgcn_s_memtime() : 0;
             chain_full<KC, CM_REPLAY>(P, query, L, S, n, P.srt + ch.seed_off, regs, nreg, lane, P.pre + ch.seed_off,
                                       P.pre_ok + ch.seed_off, P.span[2 * c], P.span[2 * c + 1]);
             rc = 0;
+            if (P.cyc) {
+                w_full += __builtin_amdgcn_s_memtime() - tf;
+                w_big += 1 + ((uint64_t)n << 32);
+            }
             if (hashed) {
                 __threadfence_block();
                 for (int i = before; i < nreg; ++i) {
@@ -703,52 +714,108 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             }
             continue;
         }
-        // the chain's seeds, rank-ordered across the lanes
-        SeedRec my{0, 0, 0};
-        if (lane < n) my = S[lane];
-        const uint64_t key = lane < n ? ((uint64_t)(uint32_t)my.len << 32 | (uint32_t)lane) : ~0ull;
-        int rank = 0;
-        for (int t = 0; t < n; ++t) {
-            WALK_GUARD();
-            rank += rl64(key, t) < key;
-        }
-        const int dst = (lane < n ? rank : lane) << 2;  // a permutation of the 64 lanes
-        const int64_t s_rb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)my.rbeg) |
-                                       (uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(my.rbeg >> 32)) << 32);
-        const int s_qb = __builtin_amdgcn_ds_permute(dst, my.qbeg);
-        const int s_len = __builtin_amdgcn_ds_permute(dst, my.len);
-        const int s_idx = __builtin_amdgcn_ds_permute(dst, lane);
+        // the chain's seeds in the reference's order (len << 32 | index ascending,
+        // software/bwamem.c:1070-1073), rank k at lane k & 63 of slot k >> 6:
+        // up to 64 seeds in slot 0 (ranked and permuted across the lanes), up
+        // to 128 with slot 1 (two: ranked through the chain's srt rows; the
+        // regions computed ahead then come from memory when a seed is made)
+        const bool two = n > 64;
+        int64_t s_rb, s_rb1 = 0;
+        int s_qb, s_len, s_idx, s_qb1 = 0, s_len1 = 0, s_idx1 = 0;
         AlnReg mine{};
-        int mine_ok = 0;
-        if (lane < n) {
-            mine = P.pre[ch.seed_off + s_idx];
+        int mine_ok = 0, mine_ok1 = 0;
+        if (!two) {
+            SeedRec my{0, 0, 0};
+            if (lane < n) my = S[lane];
+            const uint64_t key = lane < n ? ((uint64_t)(uint32_t)my.len << 32 | (uint32_t)lane) : ~0ull;
+            int rank = 0;
+            for (int t = 0; t < n; ++t) {
+                WALK_GUARD();
+                rank += rl64(key, t) < key;
+            }
+            const int dst = (lane < n ? rank : lane) << 2;  // a permutation of the 64 lanes
+            s_rb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)my.rbeg) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(my.rbeg >> 32)) << 32);
+            s_qb = __builtin_amdgcn_ds_permute(dst, my.qbeg);
+            s_len = __builtin_amdgcn_ds_permute(dst, my.len);
+            s_idx = __builtin_amdgcn_ds_permute(dst, lane);
+            if (lane < n) {
+                mine = P.pre[ch.seed_off + s_idx];
+                mine_ok = P.pre_ok[ch.seed_off + s_idx];
+            }
+        } else {
+            uint64_t* srt = P.srt + ch.seed_off;
+            const bool v1 = 64 + lane < n;
+            const SeedRec m0 = S[lane];
+            const SeedRec m1 = v1 ? S[64 + lane] : SeedRec{0, 0, 0};
+            const uint64_t k0 = (uint64_t)(uint32_t)m0.len << 32 | (uint32_t)lane;
+            const uint64_t k1 = v1 ? ((uint64_t)(uint32_t)m1.len << 32 | (uint32_t)(64 + lane)) : ~0ull;
+            int r0 = 0, r1 = 0;
+            for (int t = 0; t < 64; ++t) {
+                const uint64_t v = rl64(k0, t);
+                r0 += v < k0, r1 += v < k1;
+            }
+            for (int t = 0; t < n - 64; ++t) {
+                WALK_GUARD();
+                const uint64_t v = rl64(k1, t);
+                r0 += v < k0, r1 += v < k1;
+            }
+            srt[r0] = k0;
+            if (v1) srt[r1] = k1;
+            __threadfence_block();
+            s_idx = (int)(uint32_t)srt[lane];
+            s_idx1 = v1 ? (int)(uint32_t)srt[64 + lane] : 0;
+            const SeedRec q0 = S[s_idx], q1 = S[s_idx1];
+            s_rb = q0.rbeg, s_qb = q0.qbeg, s_len = q0.len;
+            s_rb1 = q1.rbeg, s_qb1 = q1.qbeg, s_len1 = q1.len;
             mine_ok = P.pre_ok[ch.seed_off + s_idx];
+            mine_ok1 = v1 ? P.pre_ok[ch.seed_off + s_idx1] : 0;
         }
-        bool skipped = false;
+        bool skipped = false, skipped1 = false;
         for (int k = n - 1; k >= 0; --k) {
             WALK_GUARD();
-            const int64_t k_rb = (int64_t)rl64((uint64_t)s_rb, k);
-            const int k_qb = kswd::rl(s_qb, k), k_len = kswd::rl(s_len, k);
+            const bool hi = k >= 64;  // wave-uniform: which slot holds rank k
+            const int kl = k & 63;
+            const int64_t k_rb = (int64_t)rl64((uint64_t)(hi ? s_rb1 : s_rb), kl);
+            const int k_qb = kswd::rl(hi ? s_qb1 : s_qb, kl), k_len = kswd::rl(hi ? s_len1 : s_len, kl);
             bool hit = __ballot(lane < rc && reg_contains(P, k_rb, k_qb, k_len, g_rb, g_re, g_qb, g_qe)) != 0;
             const int older = nreg - rc;  // regions only in memory: regs[0 .. older)
+            bool scan = !hit && older > 0 && !hashed;
             if (!hit && older > 0 && hashed) {  // the bins a containing region can start in
+                const uint64_t th = P.cyc ? __builtin_amdgcn_s_memtime() : 0;
                 __threadfence_block();
                 const uint64_t b1 = (uint64_t)k_rb >> HT_BIN;
                 const uint64_t b0 = (uint64_t)(k_rb - maxlen > 0 ? k_rb - maxlen : 0) >> HT_BIN;
-                for (uint64_t b = b0; b <= b1 && !hit; ++b) {
+                // their heads and counts first: one round per bin (usually 1-2 bins)
+                const bool wide = b1 - b0 >= 64;  // (not with reads of <= 1024 bp)
+                uint64_t heads = 0, in_bins = 0;  // lane (b - b0) holds bin b's entry
+                for (uint64_t b = b0; b <= b1 && !wide; ++b) {
                     WALK_GUARD();
                     uint64_t e;
                     (void)ht_find(ht, b, lane, e);
-                    int i = e ? uni((int)(e & 0xFFFFF) - 1) : -1;
-                    while (i >= 0 && !hit) {
+                    if ((uint64_t)lane == b - b0) heads = e;
+                    in_bins += e >> 44;
+                }
+                if (wide || in_bins > (uint64_t)(older >> 6) + 2) {
+                    scan = true;  // fewer rounds 64 regions at a time than one per hop
+                } else {
+                    for (uint64_t b = b0; b <= b1 && !hit; ++b) {
                         WALK_GUARD();
-                        const AlnReg* p = regs + i;
-                        hit = reg_contains(P, k_rb, k_qb, k_len, (int64_t)uni64((uint64_t)p->rb),
-                                           (int64_t)uni64((uint64_t)p->re), uni(p->qb), uni(p->qe));
-                        i = uni(rnext[i]);
+                        const uint64_t e = rl64(heads, (int)(b - b0));
+                        int i = e ? uni((int)(e & 0xFFFFF) - 1) : -1;
+                        while (i >= 0 && !hit) {
+                            WALK_GUARD();
+                            const AlnReg* p = regs + i;
+                            hit = reg_contains(P, k_rb, k_qb, k_len, (int64_t)uni64((uint64_t)p->rb),
+                                               (int64_t)uni64((uint64_t)p->re), uni(p->qb), uni(p->qe));
+                            i = uni(rnext[i]);
+                            ++w_hops;
+                        }
                     }
                 }
-            } else if (!hit && older > 0) {
+                if (P.cyc) w_hash += __builtin_amdgcn_s_memtime() - th;
+            }
+            if (scan) {  // every older region, newest first, 64 a round
                 __threadfence_block();
                 for (int ib = 0; ib < older && !hit; ib += 64) {
                     WALK_GUARD();
@@ -763,34 +830,46 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             }
             bool wanted = !hit;
             if (hit) {  // extended anyway if a longer overlapping seed above k disagrees with it
-                bool ok = false;
-                if (lane > k && lane < n && !skipped && !(s_len < k_len * .95)) {
-                    if (k_qb <= s_qb && k_qb + k_len - s_qb >= k_len >> 2 && (int64_t)(s_qb - k_qb) != s_rb - k_rb)
-                        ok = true;
-                    if (s_qb <= k_qb && s_qb + s_len - k_qb >= k_len >> 2 && (int64_t)(k_qb - s_qb) != k_rb - s_rb)
-                        ok = true;
-                }
+                // (software/bwamem.c:1098-1109; a skipped seed no longer counts)
+                auto disagrees = [&](int i, bool skp, int64_t t_rb, int t_qb, int t_len) {
+                    if (i <= k || i >= n || skp || t_len < k_len * .95) return false;
+                    if (k_qb <= t_qb && k_qb + k_len - t_qb >= k_len >> 2 && (int64_t)(t_qb - k_qb) != t_rb - k_rb)
+                        return true;
+                    return t_qb <= k_qb && t_qb + t_len - k_qb >= k_len >> 2 && (int64_t)(k_qb - t_qb) != k_rb - t_rb;
+                };
+                bool ok = disagrees(lane, skipped, s_rb, s_qb, s_len);
+                if (two) ok = ok || disagrees(64 + lane, skipped1, s_rb1, s_qb1, s_len1);
                 wanted = __ballot(ok) != 0;
-                if (!wanted && lane == k) skipped = true;
+                if (!wanted && lane == kl) {
+                    if (hi) skipped1 = true;
+                    else skipped = true;
+                }
             }
             if (!wanted) continue;
             int64_t a_rb, a_re;
             int a_qb, a_qe;
-            if (kswd::rl(mine_ok, k)) {
+            if (kswd::rl(hi ? mine_ok1 : mine_ok, kl)) {
                 ++n_used;
-                if (lane == k) regs[nreg] = mine;
-                a_rb = (int64_t)rl64((uint64_t)mine.rb, k), a_re = (int64_t)rl64((uint64_t)mine.re, k);
-                a_qb = kswd::rl(mine.qb, k), a_qe = kswd::rl(mine.qe, k);
+                if (!two) {
+                    if (lane == k) regs[nreg] = mine;
+                    a_rb = (int64_t)rl64((uint64_t)mine.rb, k), a_re = (int64_t)rl64((uint64_t)mine.re, k);
+                    a_qb = kswd::rl(mine.qb, k), a_qe = kswd::rl(mine.qe, k);
+                } else {
+                    const AlnReg* pr = P.pre + ch.seed_off + kswd::rl(hi ? s_idx1 : s_idx, kl);
+                    const AlnReg a = *pr;
+                    if (lane == 0) regs[nreg] = a;
+                    a_rb = (int64_t)uni64((uint64_t)a.rb), a_re = (int64_t)uni64((uint64_t)a.re);
+                    a_qb = uni(a.qb), a_qe = uni(a.qe);
+                }
             } else {
                 ++n_serial;
+                const int si = kswd::rl(hi ? s_idx1 : s_idx, kl);
                 __threadfence_block();
                 if constexpr (GUARD) {  // inlined too
-                    const AlnReg a = seed_region<KC>(P, query, L, S, n, S[kswd::rl(s_idx, k)], P.span[2 * c],
-                                                     P.span[2 * c + 1], lane);
+                    const AlnReg a = seed_region<KC>(P, query, L, S, n, S[si], P.span[2 * c], P.span[2 * c + 1], lane);
                     if (lane == 0) regs[nreg] = a;
                 } else {
-                    seed_region_call<KC>(P, query, L, S, n, kswd::rl(s_idx, k), P.span[2 * c], P.span[2 * c + 1],
-                                         regs + nreg);
+                    seed_region_call<KC>(P, query, L, S, n, si, P.span[2 * c], P.span[2 * c + 1], regs + nreg);
                 }
                 __threadfence_block();
                 a_rb = (int64_t)uni64((uint64_t)regs[nreg].rb), a_re = (int64_t)uni64((uint64_t)regs[nreg].re);
@@ -810,7 +889,11 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
         P.n_regs[r] = (uint64_t)nreg;
         if (n_used) atomicAdd(&P.ctr[9], n_used);
         if (n_serial) atomicAdd(&P.ctr[10], n_serial);
-        if (P.cyc) P.cyc[r] = __builtin_amdgcn_s_memtime() - t_read;
+        if (P.cyc) {
+            P.cyc[r] = __builtin_amdgcn_s_memtime() - t_read;
+            uint64_t* w = P.cyc + P.n_reads + 4ull * r;
+            w[0] = w_full, w[1] = w_hash, w[2] = w_big, w[3] = w_hops;
+        }
     }
 }
 #undef WALK_GUARD

@@ -1532,7 +1532,9 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     P.pac = g->d_pac, P.l_pac = g->l_pac, P.n_reads = n;
     aln_opt_params(opt, P);
     P.srt = b->d_aln_srt.p, P.raw = b->d_aln_raw.p, P.n_regs = b->d_aln_nregs.p, P.ctr = b->d_aln_ctr.p;
-    // diagnostics: SMEM_ALN_CYCLES=<file> writes the shader cycles each read took (u64 per read)
+    // diagnostics: SMEM_ALN_CYCLES=<file> writes the shader cycles each read took (u64 per read),
+    // and <file>.walk the heavy walk's split (4 x u64 per read: cycles in chain_full, cycles in the
+    // bin-hash containment walks, chains over 64 seeds | their seeds << 32, bin-list hops)
     const char* cyc_path = getenv("SMEM_ALN_CYCLES");
     DevBuf<uint64_t> d_cyc;
     struct Free {
@@ -1540,7 +1542,8 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
         ~Free() { b.release(); }  // every return path, HIP_TRY's included
     } free_cyc{d_cyc};
     if (cyc_path) {
-        HIP_TRY(d_cyc.ensure(std::max(n, 1)));
+        HIP_TRY(d_cyc.ensure(5 * (uint64_t)std::max(n, 1)));
+        HIP_TRY(hipMemsetAsync(d_cyc.p, 0, 5 * sizeof(uint64_t) * (uint64_t)std::max(n, 1), b->st));
         P.cyc = d_cyc.p;
     }
     // SMEM_ALN_SPLIT=1: aln_kernel's cycles by phase and its counts (smem::Split), on stderr
@@ -1580,10 +1583,14 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     b->stats.aln_ms = ms;
     b->stats.n_regs = b->tot_regs;
     if (cyc_path && n > 0) {
-        std::vector<uint64_t> h(n);
-        HIP_TRY(hipMemcpy(h.data(), d_cyc.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> h(5 * (uint64_t)n);
+        HIP_TRY(hipMemcpy(h.data(), d_cyc.p, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
         if (FILE* f = fopen(cyc_path, "wb")) {
             fwrite(h.data(), sizeof(uint64_t), n, f);
+            fclose(f);
+        }
+        if (FILE* f = fopen((std::string(cyc_path) + ".walk").c_str(), "wb")) {
+            fwrite(h.data() + n, sizeof(uint64_t), 4 * (uint64_t)n, f);
             fclose(f);
         }
     }

@@ -74,11 +74,27 @@ def main():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    if own.cycles:  # per-read chain / seed counts beside the cycles
+    if own.cycles:  # the slowest reads' cycles, walk split and chain / seed counts (small enough to copy back)
+        import json
         import numpy as np
         res = b.fetch()
-        np.savez(own.cycles + ".chains.npz", chain_off=res.chain_off, chain_n=res.chains["n"],
-                 lens=np.diff(reads.offs.astype(np.int64)))
+        cyc = np.fromfile(own.cycles, dtype=np.uint64).astype(np.int64)
+        walk = np.fromfile(own.cycles + ".walk", dtype=np.uint64).astype(np.int64).reshape(-1, 4)
+        off = np.asarray(res.chain_off, dtype=np.int64)
+        cn = np.asarray(res.chains["n"], dtype=np.int64)
+        top = []
+        for r in np.argsort(-cyc)[:30]:
+            ns = cn[off[r]:off[r + 1]]
+            top.append(dict(read=int(r), cycles=int(cyc[r]), ms_at_2_4ghz=round(cyc[r] / 2.4e6, 3),
+                            chains=int(ns.size), seeds=int(ns.sum()), chains_over_64=int((ns > 64).sum()),
+                            max_chain=int(ns.max()) if ns.size else 0,
+                            walk_full_cycles=int(walk[r, 0]), walk_hash_cycles=int(walk[r, 1]),
+                            walk_big_chains=int(walk[r, 2] & 0xFFFFFFFF), walk_big_seeds=int(walk[r, 2] >> 32),
+                            walk_hops=int(walk[r, 3])))
+        with open(own.cycles + ".top.json", "w") as fh:
+            json.dump(top, fh, indent=1)
+        os.unlink(own.cycles)
+        os.unlink(own.cycles + ".walk")
     b.close()
     gpu.close()
 
