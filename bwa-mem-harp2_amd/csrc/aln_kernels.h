@@ -99,9 +99,36 @@ struct AlnParams {
     RegTask* htasks;
     uint32_t* hlq;
     uint32_t* swlist;         // [n_chains] heavy chains whose mem_chain2aln_short runs its SW (lq[LQ_NSW] of them)
+    // the heavy walk's candidate index (lane_on, SMEM_ALN_CAND != 0; nullptr: off): every region a
+    // heavy read's walk can make -- its short chains' pre_short, its other chains' seeds' pre -- sorted
+    // by (heavy read, rb).  A seed the ring misses is tested against the candidates that start within
+    // the read's longest candidate before it, 64 a round, counting only those the walk made so far
+    int64_t* cand_rb;         // [m] sorted candidates: reference start (INT64_MAX: no region)
+    int64_t* cand_re;
+    uint32_t* cand_q;         // qb | qe << 16
+    uint8_t* cand_made;       // [m] 1: the walk made this region
+    uint32_t* cand_pos_s;     // [n_seeds] a heavy read's seed's region: its index position
+    uint32_t* cand_pos_c;     // [n_chains] a heavy read's short chain's region: its position
+    uint2* cand_rng;          // [n_seeds] the positions [x, y) a heavy read's seed is tested against
     // compaction
     const uint64_t* reg_off;  // [n_reads + 1]
     AlnReg* out;
+};
+
+// building the candidate index: per heavy read h (ordinal in AlnParams::heavy)
+// slots [off[h], off[h + 1]) -- its seeds, then its chains -- keyed by rb
+// (no region: all 34 bits ones), each read's segment sorted by key
+struct CandParams {
+    uint64_t* key;   // [m] unsorted, then
+    uint64_t* key2;  // [m] sorted
+    uint32_t* val;   // [m] seed index, or 0x80000000 | chain index
+    uint32_t* val2;
+    uint64_t* off;   // [n_heavy + 1]
+    int64_t* hmax;   // [n_heavy] the longest candidate region of the read
+    uint32_t* hord;  // [n_reads] a heavy read's ordinal
+    uint32_t n_heavy;
+    uint64_t m;
+    uint64_t n_chains;
 };
 
 // one ksw_align2 call (software/ksw.c:342) as mem_chain2aln_short makes it
@@ -135,6 +162,13 @@ hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st);
 hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st);
 // parts: 1 the chain tasks, 2 the walk, 3 both
 hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, int parts, hipStream_t st);
+// the candidate index: slot counts per heavy read (hcnt + hscnt) into cnt[n_heavy];
+// then (C.off scanned, C.m slots) fill, sort, place and every heavy seed's range;
+// tmp / tmp_bytes: the sort's scratch (tmp nullptr: *tmp_bytes is set, nothing runs)
+hipError_t smem_launch_aln_cand_count(const smem::AlnParams* P, uint32_t n_heavy, uint64_t* cnt, uint32_t* hord,
+                                      hipStream_t st);
+hipError_t smem_launch_aln_cand(const smem::AlnParams* P, const smem::CandParams* C, void* tmp, size_t* tmp_bytes,
+                                int n_cu, hipStream_t st);
 // lane_on: the regions computed ahead one seed per lane, before the walks
 // (lq / hlq zeroed; heavy_min / heavy_seeds set): every chain's prep and
 // tasks (light reads' to tasks / lq, heavy reads' to htasks / hlq), then, per

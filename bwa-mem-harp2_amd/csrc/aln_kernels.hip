@@ -19,6 +19,7 @@
 // Reads up to 256 bp go to aln_kernel<4> (query columns in 4 registers per
 // lane), longer ones (up to 1024 bp) to aln_kernel<16>.
 #include <algorithm>
+#include <hipcub/hipcub.hpp>
 
 #include "aln_kernels.h"
 #include "ksw_device.h"
@@ -639,6 +640,14 @@ __device__ __forceinline__ int64_t shr64(int64_t v, int64_t first) {  // wave_sh
 // loop iteration of the walk counts against P.walk_guard; past it the wave
 // sets ctr[15] and leaves the read, so a walk that would spin ends instead of
 // hanging the GPU (the round-2 hang).
+#define WALK_GUARD_L()                                                        \
+    if constexpr (GUARD) {                                                    \
+        if (++guard > P.walk_guard) {                                         \
+            if (lane == 0) atomicAdd(&P.ctr[15], 1u);                         \
+            tripped = true;                                                   \
+            return true;                                                      \
+        }                                                                     \
+    }
 #define WALK_GUARD()                                                          \
     if constexpr (GUARD) {                                                    \
         if (++guard > P.walk_guard) {                                         \
@@ -661,7 +670,13 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
     // the bin hash, for reads with many regions (not with more than the
     // table holds, or than 20-bit indices do)
     const uint64_t cap = uni64(P.seed_off[r + 1] - P.seed_off[r]);
-    const bool hashed = c1 - c0 >= P.hash_min && cap < (1u << 20) - 1 && cap + (c1 - c0) < ALN_HT / 2 &&
+    // the candidate index (built for every heavy read when P.cand_made is set)
+    // until the walk makes a region the index does not hold (dirty: a region
+    // computed here, or chain_full's); then, as without the index, the bin
+    // hash or a scan of every older region
+    const bool indexed = P.cand_made != nullptr;
+    bool dirty = false;
+    const bool hashed = !indexed && c1 - c0 >= P.hash_min && cap < (1u << 20) - 1 && cap + (c1 - c0) < ALN_HT / 2 &&
                         ((uint64_t)(2 * P.l_pac) >> HT_BIN) < (1ull << 24);  // bins fit the slot's 24 bits
     uint64_t* ht = P.ht + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * ALN_HT;
     int32_t* rnext = P.rnext + P.seed_off[r];
@@ -672,23 +687,173 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
         for (int i = lane; i < ALN_HT; i += 64) ht[i] = 0;
         __threadfence_block();
     }
-    for (uint64_t c = c0; c < c1; ++c) {
-        WALK_GUARD();
-        OutChain ch = P.chains[c];
-        const int n = uni(ch.n);
-        if (n <= 0) continue;
-        if (uni((int)P.short_ok[c])) {
-            const AlnReg* a = P.pre_short + c;
-            if (lane == 0) regs[nreg] = *a;
-            g_rb = shr64(g_rb, uni64((uint64_t)a->rb)), g_re = shr64(g_re, uni64((uint64_t)a->re));
-            g_qb = kswd::wave_shr1(g_qb, uni(a->qb)), g_qe = kswd::wave_shr1(g_qe, uni(a->qe));
-            rc = rc < 64 ? rc + 1 : 64;
-            if (hashed) {
-                const int64_t rb = (int64_t)uni64((uint64_t)a->rb), re = (int64_t)uni64((uint64_t)a->re);
-                maxlen = re - rb > maxlen ? re - rb : maxlen;
-                ht_insert(ht, rnext, rb, nreg, lane);
+    // a seed contained in a region made before it (software/bwamem.c:1079-1094):
+    // the ring of the newest 64 in registers, then the candidate index (x, y:
+    // the seed's candidates), the bin hash or a scan of every older region
+    bool tripped = false;  // GUARD: a lambda's loop ran past the guard
+    auto contained = [&](int64_t k_rb, int k_qb, int k_len, uint32_t x, uint32_t y) -> bool {
+        bool hit = __ballot(lane < rc && reg_contains(P, k_rb, k_qb, k_len, g_rb, g_re, g_qb, g_qe)) != 0;
+        const int older = nreg - rc;  // regions only in memory: regs[0 .. older)
+        bool scan = !hit && older > 0 && !hashed && (!indexed || dirty);
+        if (!hit && older > 0 && indexed && !dirty) {  // the candidates that contain it, made so far
+            if (x < y) __threadfence_block();
+            for (uint32_t q0 = x; q0 < y && !hit; q0 += 64) {
+                WALK_GUARD_L();
+                const uint32_t q = q0 + (uint32_t)lane;
+                bool ok = false;
+                if (q < y) {
+                    const uint8_t made = P.cand_made[q];
+                    const int64_t prb = P.cand_rb[q], pre_ = P.cand_re[q];
+                    const uint32_t pq = P.cand_q[q];
+                    ok = made && reg_contains(P, k_rb, k_qb, k_len, prb, pre_, (int)(pq & 0xFFFFu), (int)(pq >> 16));
+                }
+                hit = __ballot(ok) != 0;
+                ++w_hops;
             }
-            ++nreg;
+        } else if (!hit && older > 0 && hashed) {  // the bins a containing region can start in
+            const uint64_t th = P.cyc ? __builtin_amdgcn_s_memtime() : 0;
+            __threadfence_block();
+            const uint64_t b1 = (uint64_t)k_rb >> HT_BIN;
+            const uint64_t b0 = (uint64_t)(k_rb - maxlen > 0 ? k_rb - maxlen : 0) >> HT_BIN;
+            // their heads and counts first: one round per bin (usually 1-2 bins)
+            const bool wide = b1 - b0 >= 64;  // (not with reads of <= 1024 bp)
+            uint64_t heads = 0, in_bins = 0;  // lane (b - b0) holds bin b's entry
+            for (uint64_t b = b0; b <= b1 && !wide; ++b) {
+                WALK_GUARD_L();
+                uint64_t e;
+                (void)ht_find(ht, b, lane, e);
+                if ((uint64_t)lane == b - b0) heads = e;
+                in_bins += e >> 44;
+            }
+            if (wide || in_bins > (uint64_t)(older >> 6) + 2) {
+                scan = true;  // fewer rounds 64 regions at a time than one per hop
+            } else {
+                for (uint64_t b = b0; b <= b1 && !hit; ++b) {
+                    WALK_GUARD_L();
+                    const uint64_t e = rl64(heads, (int)(b - b0));
+                    int i = e ? uni((int)(e & 0xFFFFF) - 1) : -1;
+                    while (i >= 0 && !hit) {
+                        WALK_GUARD_L();
+                        const AlnReg* p = regs + i;
+                        hit = reg_contains(P, k_rb, k_qb, k_len, (int64_t)uni64((uint64_t)p->rb),
+                                           (int64_t)uni64((uint64_t)p->re), uni(p->qb), uni(p->qe));
+                        i = uni(rnext[i]);
+                        ++w_hops;
+                    }
+                }
+            }
+            if (P.cyc) w_hash += __builtin_amdgcn_s_memtime() - th;
+        }
+        if (scan) {  // every older region, newest first, 64 a round
+            __threadfence_block();
+            for (int ib = 0; ib < older && !hit; ib += 64) {
+                WALK_GUARD_L();
+                const int i = older - 1 - ib - lane;
+                bool ok = false;
+                if (i >= 0) {
+                    const AlnReg p = regs[i];
+                    ok = reg_contains(P, k_rb, k_qb, k_len, p.rb, p.re, p.qb, p.qe);
+                }
+                hit = __ballot(ok) != 0;
+            }
+        }
+        return hit;
+    };
+    // a made region: into regs (done by the caller), the ring, the hash
+    auto push = [&](int64_t a_rb, int64_t a_re, int a_qb, int a_qe) {
+        g_rb = shr64(g_rb, a_rb), g_re = shr64(g_re, a_re);
+        g_qb = kswd::wave_shr1(g_qb, a_qb), g_qe = kswd::wave_shr1(g_qe, a_qe);
+        rc = rc < 64 ? rc + 1 : 64;
+        if (hashed) {
+            maxlen = a_re - a_rb > maxlen ? a_re - a_rb : maxlen;
+            ht_insert(ht, rnext, a_rb, nreg, lane);
+        }
+        ++nreg;
+    };
+    // The chains 64 at a time: lane t loads chain cb + t's header, and for a
+    // short chain (mem_chain2aln_short made its region) or a single-seed chain
+    // everything its walk step reads, so such a chain costs no round trip of
+    // its own (on the human-like profile's heavy reads ~90 % of the chains
+    // have one seed, and the walk waited on 3 round trips per chain).
+    for (uint64_t cb = c0; cb < c1; cb += 64) {
+        WALK_GUARD();
+        const uint64_t cl = cb + (uint64_t)lane;
+        int h_n = 0, h_sh = 0, h_ok = 0;
+        uint64_t h_so = 0;
+        uint32_t h_pc = 0, h_ps = 0;
+        uint2 h_rng = {0, 0};
+        SeedRec h_s{0, 0, 0};
+        AlnReg h_reg{};
+        if (cl < c1) {
+            const OutChain hc = P.chains[cl];
+            h_n = hc.n, h_so = hc.seed_off;
+            h_sh = P.short_ok[cl];
+            if (indexed) h_pc = P.cand_pos_c[cl];
+            if (h_n > 0 && h_sh) {
+                h_reg = P.pre_short[cl];
+            } else if (h_n == 1) {
+                h_s = P.seeds[h_so];
+                h_reg = P.pre[h_so];
+                h_ok = P.pre_ok[h_so];
+                if (indexed) {
+                    h_rng = P.cand_rng[h_so];
+                    h_ps = P.cand_pos_s[h_so];
+                }
+            }
+        }
+        const uint64_t ce = cb + 64 < c1 ? cb + 64 : c1;
+        for (uint64_t c = cb; c < ce; ++c) {
+        WALK_GUARD();
+        const int t = (int)(c - cb);
+        const int n = kswd::rl(h_n, t);
+        if (n <= 0) continue;
+        if (kswd::rl(h_sh, t)) {  // mem_chain2aln_short's region
+            if (lane == t) {
+                regs[nreg] = h_reg;
+                if (indexed) P.cand_made[h_pc] = 1;
+            }
+            push((int64_t)rl64((uint64_t)h_reg.rb, t), (int64_t)rl64((uint64_t)h_reg.re, t), kswd::rl(h_reg.qb, t),
+                 kswd::rl(h_reg.qe, t));
+            continue;
+        }
+        OutChain ch;
+        ch.seed_off = rl64(h_so, t);
+        ch.n = n;
+        if (n == 1) {  // one seed: extended unless contained (no seed above it can disagree)
+            const int64_t k_rb = (int64_t)rl64((uint64_t)h_s.rbeg, t);
+            const int k_qb = kswd::rl(h_s.qbeg, t), k_len = kswd::rl(h_s.len, t);
+            const bool hit1 = contained(k_rb, k_qb, k_len, (uint32_t)kswd::rl((int)h_rng.x, t),
+                                        (uint32_t)kswd::rl((int)h_rng.y, t));
+            if constexpr (GUARD) {
+                if (tripped) return;
+            }
+            if (hit1) continue;
+            int64_t a_rb, a_re;
+            int a_qb, a_qe;
+            if (kswd::rl(h_ok, t)) {
+                ++n_used;
+                if (lane == t) {
+                    regs[nreg] = h_reg;
+                    if (indexed) P.cand_made[h_ps] = 1;
+                }
+                a_rb = (int64_t)rl64((uint64_t)h_reg.rb, t), a_re = (int64_t)rl64((uint64_t)h_reg.re, t);
+                a_qb = kswd::rl(h_reg.qb, t), a_qe = kswd::rl(h_reg.qe, t);
+            } else {
+                ++n_serial;
+                dirty = true;  // a region the index does not hold
+                const SeedRec* S = P.seeds + ch.seed_off;
+                __threadfence_block();
+                if constexpr (GUARD) {
+                    const AlnReg a = seed_region<KC>(P, query, L, S, 1, S[0], P.span[2 * c], P.span[2 * c + 1], lane);
+                    if (lane == 0) regs[nreg] = a;
+                } else {
+                    seed_region_call<KC>(P, query, L, S, 1, 0, P.span[2 * c], P.span[2 * c + 1], regs + nreg);
+                }
+                __threadfence_block();
+                a_rb = (int64_t)uni64((uint64_t)regs[nreg].rb), a_re = (int64_t)uni64((uint64_t)regs[nreg].re);
+                a_qb = uni(regs[nreg].qb), a_qe = uni(regs[nreg].qe);
+            }
+            push(a_rb, a_re, a_qb, a_qe);
             continue;
         }
         const SeedRec* S = P.seeds + ch.seed_off;
@@ -699,6 +864,7 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             chain_full<KC, CM_REPLAY>(P, query, L, S, n, P.srt + ch.seed_off, regs, nreg, lane, P.pre + ch.seed_off,
                                       P.pre_ok + ch.seed_off, P.span[2 * c], P.span[2 * c + 1]);
             rc = 0;
+            dirty = true;  // its regions are not marked in the index
             if (P.cyc) {
                 w_full += __builtin_amdgcn_s_memtime() - tf;
                 w_big += 1 + ((uint64_t)n << 32);
@@ -724,6 +890,8 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
         int s_qb, s_len, s_idx, s_qb1 = 0, s_len1 = 0, s_idx1 = 0;
         AlnReg mine{};
         int mine_ok = 0, mine_ok1 = 0;
+        uint2 rng = {0, 0}, rng1 = {0, 0};  // indexed: the candidates of rank lane / 64 + lane
+        uint32_t pos = 0, pos1 = 0;         // and the index position of its own region
         if (!two) {
             SeedRec my{0, 0, 0};
             if (lane < n) my = S[lane];
@@ -742,6 +910,10 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             if (lane < n) {
                 mine = P.pre[ch.seed_off + s_idx];
                 mine_ok = P.pre_ok[ch.seed_off + s_idx];
+                if (indexed) {
+                    rng = P.cand_rng[ch.seed_off + s_idx];
+                    pos = P.cand_pos_s[ch.seed_off + s_idx];
+                }
             }
         } else {
             uint64_t* srt = P.srt + ch.seed_off;
@@ -770,6 +942,14 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             s_rb1 = q1.rbeg, s_qb1 = q1.qbeg, s_len1 = q1.len;
             mine_ok = P.pre_ok[ch.seed_off + s_idx];
             mine_ok1 = v1 ? P.pre_ok[ch.seed_off + s_idx1] : 0;
+            if (indexed) {
+                rng = P.cand_rng[ch.seed_off + s_idx];
+                pos = P.cand_pos_s[ch.seed_off + s_idx];
+                if (v1) {
+                    rng1 = P.cand_rng[ch.seed_off + s_idx1];
+                    pos1 = P.cand_pos_s[ch.seed_off + s_idx1];
+                }
+            }
         }
         bool skipped = false, skipped1 = false;
         for (int k = n - 1; k >= 0; --k) {
@@ -778,55 +958,10 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             const int kl = k & 63;
             const int64_t k_rb = (int64_t)rl64((uint64_t)(hi ? s_rb1 : s_rb), kl);
             const int k_qb = kswd::rl(hi ? s_qb1 : s_qb, kl), k_len = kswd::rl(hi ? s_len1 : s_len, kl);
-            bool hit = __ballot(lane < rc && reg_contains(P, k_rb, k_qb, k_len, g_rb, g_re, g_qb, g_qe)) != 0;
-            const int older = nreg - rc;  // regions only in memory: regs[0 .. older)
-            bool scan = !hit && older > 0 && !hashed;
-            if (!hit && older > 0 && hashed) {  // the bins a containing region can start in
-                const uint64_t th = P.cyc ? __builtin_amdgcn_s_memtime() : 0;
-                __threadfence_block();
-                const uint64_t b1 = (uint64_t)k_rb >> HT_BIN;
-                const uint64_t b0 = (uint64_t)(k_rb - maxlen > 0 ? k_rb - maxlen : 0) >> HT_BIN;
-                // their heads and counts first: one round per bin (usually 1-2 bins)
-                const bool wide = b1 - b0 >= 64;  // (not with reads of <= 1024 bp)
-                uint64_t heads = 0, in_bins = 0;  // lane (b - b0) holds bin b's entry
-                for (uint64_t b = b0; b <= b1 && !wide; ++b) {
-                    WALK_GUARD();
-                    uint64_t e;
-                    (void)ht_find(ht, b, lane, e);
-                    if ((uint64_t)lane == b - b0) heads = e;
-                    in_bins += e >> 44;
-                }
-                if (wide || in_bins > (uint64_t)(older >> 6) + 2) {
-                    scan = true;  // fewer rounds 64 regions at a time than one per hop
-                } else {
-                    for (uint64_t b = b0; b <= b1 && !hit; ++b) {
-                        WALK_GUARD();
-                        const uint64_t e = rl64(heads, (int)(b - b0));
-                        int i = e ? uni((int)(e & 0xFFFFF) - 1) : -1;
-                        while (i >= 0 && !hit) {
-                            WALK_GUARD();
-                            const AlnReg* p = regs + i;
-                            hit = reg_contains(P, k_rb, k_qb, k_len, (int64_t)uni64((uint64_t)p->rb),
-                                               (int64_t)uni64((uint64_t)p->re), uni(p->qb), uni(p->qe));
-                            i = uni(rnext[i]);
-                            ++w_hops;
-                        }
-                    }
-                }
-                if (P.cyc) w_hash += __builtin_amdgcn_s_memtime() - th;
-            }
-            if (scan) {  // every older region, newest first, 64 a round
-                __threadfence_block();
-                for (int ib = 0; ib < older && !hit; ib += 64) {
-                    WALK_GUARD();
-                    const int i = older - 1 - ib - lane;
-                    bool ok = false;
-                    if (i >= 0) {
-                        const AlnReg p = regs[i];
-                        ok = reg_contains(P, k_rb, k_qb, k_len, p.rb, p.re, p.qb, p.qe);
-                    }
-                    hit = __ballot(ok) != 0;
-                }
+            bool hit = contained(k_rb, k_qb, k_len, (uint32_t)kswd::rl((int)(hi ? rng1.x : rng.x), kl),
+                                 (uint32_t)kswd::rl((int)(hi ? rng1.y : rng.y), kl));
+            if constexpr (GUARD) {
+                if (tripped) return;
             }
             bool wanted = !hit;
             if (hit) {  // extended anyway if a longer overlapping seed above k disagrees with it
@@ -850,6 +985,7 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
             int a_qb, a_qe;
             if (kswd::rl(hi ? mine_ok1 : mine_ok, kl)) {
                 ++n_used;
+                if (indexed && lane == kl) P.cand_made[hi ? pos1 : pos] = 1;
                 if (!two) {
                     if (lane == k) regs[nreg] = mine;
                     a_rb = (int64_t)rl64((uint64_t)mine.rb, k), a_re = (int64_t)rl64((uint64_t)mine.re, k);
@@ -863,6 +999,7 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
                 }
             } else {
                 ++n_serial;
+                dirty = true;  // a region the index does not hold
                 const int si = kswd::rl(hi ? s_idx1 : s_idx, kl);
                 __threadfence_block();
                 if constexpr (GUARD) {  // inlined too
@@ -875,14 +1012,8 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
                 a_rb = (int64_t)uni64((uint64_t)regs[nreg].rb), a_re = (int64_t)uni64((uint64_t)regs[nreg].re);
                 a_qb = uni(regs[nreg].qb), a_qe = uni(regs[nreg].qe);
             }
-            g_rb = shr64(g_rb, a_rb), g_re = shr64(g_re, a_re);
-            g_qb = kswd::wave_shr1(g_qb, a_qb), g_qe = kswd::wave_shr1(g_qe, a_qe);
-            rc = rc < 64 ? rc + 1 : 64;
-            if (hashed) {
-                maxlen = a_re - a_rb > maxlen ? a_re - a_rb : maxlen;
-                ht_insert(ht, rnext, a_rb, nreg, lane);
-            }
-            ++nreg;
+            push(a_rb, a_re, a_qb, a_qe);
+        }
         }
     }
     if (lane == 0) {
@@ -897,6 +1028,7 @@ __device__ __forceinline__ void heavy_read_walk_body(const AlnParams& P, int r) 
     }
 }
 #undef WALK_GUARD
+#undef WALK_GUARD_L
 
 // The product instantiation: the walk behind a call.  Round 2 saw gfx950
 // waves hang with the walk inlined into aln_heavy_kernel's persistent loop;
@@ -924,6 +1056,132 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
     }
 }
 
+
+// ---- the heavy walk's candidate index (AlnParams::cand_*) ----
+// Every region a heavy read's walk can make is known before the walk: its
+// short chains' pre_short and its other chains' seeds' pre.  Sorted by
+// reference start per read, the regions that can contain a seed are those
+// starting within the read's longest candidate before it, and the walk tests
+// them 64 a round, counting only those it made so far (cand_made) -- instead
+// of one dependent round trip per region of a bin (the bin hash) on reads
+// whose regions pile into few bins.
+constexpr uint64_t CAND_RB_NONE = (1ull << 34) - 1;
+
+__global__ __launch_bounds__(256) void aln_cand_count_kernel(AlnParams P, uint32_t nh, uint64_t* cnt, uint32_t* hord) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h < nh) {
+        cnt[h] = P.hcnt[h] + P.hscnt[h];
+        hord[P.heavy[h]] = h;
+    }
+}
+
+// one thread per chain of a heavy read (chain_read bit 31): its slot and its
+// seeds' slots keyed, the read's longest candidate by atomicMax (hmax zeroed).
+// A read's seeds are exactly its chains' seeds, so every slot is written.
+__global__ __launch_bounds__(256) void aln_cand_fill_kernel(AlnParams P, CandParams C, uint64_t n_chains) {
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n_chains;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t cr = P.chain_read[c];
+        if (!(cr & 0x80000000u)) continue;
+        const int r = (int)(cr & 0x7FFFFFFFu);
+        const uint32_t h = C.hord[r];
+        const uint64_t base = C.off[h], s0 = P.seed_off[r], ns = P.seed_off[r + 1] - s0;
+        const uint64_t c0 = P.chain_off[r];
+        const uint64_t hk = 0;  // the segments are the reads' slots: keys are rb alone
+        const OutChain ch = P.chains[c];
+        const bool sh = ch.n > 0 && P.short_ok[c];
+        int64_t mx = 0;
+        uint64_t kc = hk | CAND_RB_NONE;
+        if (sh) {
+            const int64_t rb = P.pre_short[c].rb, re = P.pre_short[c].re;
+            kc = hk | (uint64_t)rb;
+            mx = re - rb;
+        }
+        C.key[base + ns + (c - c0)] = kc;
+        C.val[base + ns + (c - c0)] = 0x80000000u | (uint32_t)c;
+        for (int i = 0; i < ch.n; ++i) {
+            const uint64_t j = ch.seed_off + (uint64_t)i;
+            uint64_t k = hk | CAND_RB_NONE;
+            if (!sh && P.pre_ok[j]) {
+                const int64_t rb = P.pre[j].rb, re = P.pre[j].re;
+                k = hk | (uint64_t)rb;
+                mx = re - rb > mx ? re - rb : mx;
+            }
+            C.key[base + (j - s0)] = k;
+            C.val[base + (j - s0)] = (uint32_t)j;
+        }
+        if (mx > 0) atomicMax(reinterpret_cast<unsigned long long*>(C.hmax + h), (unsigned long long)mx);
+    }
+}
+
+// one thread per sorted slot: the candidate's fields in index order, its position
+__global__ __launch_bounds__(256) void aln_cand_place_kernel(AlnParams P, CandParams C) {
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < C.m; q += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = C.key2[q];
+        const uint32_t v = C.val2[q];
+        P.cand_made[q] = 0;
+        if ((key & CAND_RB_NONE) == CAND_RB_NONE) {
+            P.cand_rb[q] = INT64_MAX;
+            P.cand_re[q] = 0;
+            P.cand_q[q] = 0;
+            continue;
+        }
+        const bool sc = (v & 0x80000000u) != 0;
+        const AlnReg& a = sc ? P.pre_short[v & 0x7FFFFFFFu] : P.pre[v];
+        P.cand_rb[q] = a.rb;
+        P.cand_re[q] = a.re;
+        P.cand_q[q] = (uint32_t)a.qb | (uint32_t)a.qe << 16;
+        if (sc) P.cand_pos_c[v & 0x7FFFFFFFu] = (uint32_t)q;
+        else P.cand_pos_s[v] = (uint32_t)q;
+    }
+}
+
+// the first position in [lo, hi) whose key is >= k (> k: upper)
+__device__ __forceinline__ uint64_t cand_bound(const uint64_t* key, uint64_t lo, uint64_t hi, uint64_t k, bool upper) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const uint64_t v = key[mid];
+        if (upper ? v <= k : v < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// one thread per chain of a heavy read, for each of its seeds: the
+// candidates starting in [rbeg - the read's longest candidate, rbeg] (a
+// region that contains the seed starts there), narrowed to the first .. last
+// of them that contain it (a static test: whether the walk made them is its
+// own business) other than the seed's own region (made, if at all, after the
+// seed is tested).  A seed no other candidate contains gets an empty range and
+// costs the walk no round trip.
+__global__ __launch_bounds__(256) void aln_cand_range_kernel(AlnParams P, CandParams C, uint64_t n_chains) {
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n_chains;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t cr = P.chain_read[c];
+        if (!(cr & 0x80000000u)) continue;
+        const uint32_t h = C.hord[cr & 0x7FFFFFFFu];
+        const uint64_t lo = C.off[h], hi = C.off[h + 1];
+        const int64_t mx = C.hmax[h];
+        const OutChain ch = P.chains[c];
+        for (int i = 0; i < ch.n; ++i) {
+            const uint64_t j = ch.seed_off + (uint64_t)i;
+            const SeedRec sd = P.seeds[j];
+            const uint64_t x = cand_bound(C.key2, lo, hi, (uint64_t)(sd.rbeg - mx > 0 ? sd.rbeg - mx : 0), false);
+            const uint64_t y = cand_bound(C.key2, x, hi, (uint64_t)sd.rbeg, true);
+            const uint32_t own = P.pre_ok[j] ? P.cand_pos_s[j] : 0xFFFFFFFFu;
+            uint32_t f = 0xFFFFFFFFu, l = 0;
+            for (uint64_t q = x; q < y; ++q) {
+                const uint32_t pq = P.cand_q[q];
+                if ((uint32_t)q != own &&
+                    reg_contains(P, sd.rbeg, sd.qbeg, sd.len, P.cand_rb[q], P.cand_re[q], (int)(pq & 0xFFFFu), (int)(pq >> 16))) {
+                    f = f < (uint32_t)q ? f : (uint32_t)q;
+                    l = (uint32_t)q + 1;
+                }
+            }
+            P.cand_rng[j] = f == 0xFFFFFFFFu ? make_uint2(0, 0) : make_uint2(f, l);
+        }
+    }
+}
 
 // ---- regions computed ahead, one seed per lane (lane_on) ----
 // The light reads' walk (aln_kernel) extends a seed of a chain only where no
@@ -1346,6 +1604,34 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
     hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
     if (long_reads)
         hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_cand_count(const smem::AlnParams* P, uint32_t n_heavy, uint64_t* cnt,
+                                                 uint32_t* hord, hipStream_t st) {
+    if (!n_heavy) return hipSuccess;
+    hipLaunchKernelGGL(smem::aln_cand_count_kernel, dim3((n_heavy + 255) / 256), dim3(256), 0, st, *P, n_heavy, cnt,
+                       hord);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_cand(const smem::AlnParams* P, const smem::CandParams* C, void* tmp,
+                                           size_t* tmp_bytes, int n_cu, hipStream_t st) {
+    // each read's slots sorted by rb (its segment [off[h], off[h + 1]))
+    if (!tmp) {
+        return hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, *tmp_bytes, C->key, C->key2, C->val, C->val2,
+                                                           (int)std::max<uint64_t>(C->m, 1), (int)C->n_heavy, C->off,
+                                                           C->off + 1, 0, 34, st);
+    }
+    if (!C->n_heavy || !C->m) return hipSuccess;
+    hipError_t e0 = hipMemsetAsync(C->hmax, 0, sizeof(int64_t) * C->n_heavy, st);
+    if (e0 != hipSuccess) return e0;
+    hipLaunchKernelGGL(smem::aln_cand_fill_kernel, dim3(n_cu * 16), dim3(256), 0, st, *P, *C, C->n_chains);
+    hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, *tmp_bytes, C->key, C->key2, C->val, C->val2,
+                                                               (int)C->m, (int)C->n_heavy, C->off, C->off + 1, 0, 34, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(smem::aln_cand_place_kernel, dim3(n_cu * 16), dim3(256), 0, st, *P, *C);
+    hipLaunchKernelGGL(smem::aln_cand_range_kernel, dim3(n_cu * 16), dim3(256), 0, st, *P, *C, C->n_chains);
     return hipGetLastError();
 }
 

@@ -1270,111 +1270,73 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
         }
         uint32_t n_ch = 0;
         bool cdup = false;
-        // Seeds p + 1 and p + 2 are in flight while seed p is decided: their
-        // records, their lower chains (the marks when they were looked up)
-        // and those chains' records.  Each decision then corrects both from
-        // registers -- a new mark between a seed's lower chain and it, or an
-        // append to that chain -- through an override record, so no decision
-        // waits on a load issued after its own (one look-ahead left the lane
-        // waiting on the chain record's round trip at every seed: ~900
-        // cycles a seed on the giants).  Three named slots rotate (a copy of
-        // a slot whose loads are in flight would wait for them).
-        struct Ahead {
-            uint64_t e;
-            SeedRec sd;
-            int L;
-            uint32_t id;
-            ChainRec c;
-            bool ov;
-            ChainRec ovc;
-        };
-        auto lookup = [&](uint32_t q, Ahead& a) {
-            a.e = key[q];
-            a.sd = seed[(uint32_t)(a.e >> CL_OBITS) & (uint32_t)CL_OMASK];
-            a.L = mark_pred(bm, sm, cs, (uint32_t)a.e & (uint32_t)CL_OMASK);
-            a.ov = false;
-            if (a.L >= 0) {
-                a.id = (uint32_t)(key[a.L] >> (2 * CL_OBITS));
-                a.c = chn[a.id];
-            }
-        };
-        auto correct = [&](Ahead& a, bool appended, int L, const ChainRec& c, bool marked, uint32_t rk, uint32_t o,
-                           const ChainRec& nc) {
-            if (appended && a.L == L) {  // the looked-up record is this chain's, before the append
-                a.ov = true;
-                a.ovc = c;
-            }
-            if (marked && rk < ((uint32_t)a.e & (uint32_t)CL_OMASK) && (a.L < 0 || (uint32_t)a.L < rk)) {
-                a.L = (int)rk;
-                a.id = o;
-                a.ov = true;
-                a.ovc = nc;
-            }
-        };
-        // decide seed p (cur), look up p + 2 (into n2), correct p + 1 (n1) and p + 2
-        auto step = [&](uint32_t p, Ahead& cur, Ahead& n1, Ahead& n2) {
-            if (p + 2 < ce) {
-                if (!cdup) lookup(p + 2, n2);
-                else n2.e = key[p + 2];
-            }
-            const uint64_t e = cur.e;
+        // seed p + 1's record and its lower chain's record are loaded while
+        // seed p is decided (against the marks before p); p's own mark or
+        // append then corrects them from registers
+        uint64_t e_n = 0;
+        SeedRec sd_n{0, 0, 0};
+        int L_n = -1;
+        ChainRec c_n{};
+        if (cs < ce) {
+            e_n = key[cs];
+            sd_n = seed[(uint32_t)(e_n >> CL_OBITS) & (uint32_t)CL_OMASK];
+        }
+        for (uint32_t p = cs; p < ce; ++p) {
+            const uint64_t e = e_n;
             const uint32_t o = (uint32_t)(e >> CL_OBITS) & (uint32_t)CL_OMASK, rk = (uint32_t)e & (uint32_t)CL_OMASK;
+            const SeedRec sd = sd_n;
+            const int Lp = L_n;
+            ChainRec cp = c_n;
+            uint32_t rk_n = 0;
+            if (!cdup && p + 1 < ce) {
+                e_n = key[p + 1];
+                const uint32_t o_n = (uint32_t)(e_n >> CL_OBITS) & (uint32_t)CL_OMASK;
+                rk_n = (uint32_t)e_n & (uint32_t)CL_OMASK;
+                sd_n = seed[o_n];
+                L_n = mark_pred(bm, sm, cs, rk_n);
+                if (L_n >= 0) c_n = chn[(uint32_t)(key[L_n] >> (2 * CL_OBITS))];
+            } else if (p + 1 < ce) {
+                e_n = key[p + 1];
+            }
             if (cdup) {  // past an equal chain key: the tree replay decides
                 code[o] = CODE_REPLAY;
                 ++n_mine;
-                return;
+                continue;
             }
-            const SeedRec sd = cur.sd;
             const int64_t rb = sd.rbeg;
             // lower chain: the highest mark below the seed's rank (the first
             // seed of the cluster has none)
-            const int L = cur.L;
-            bool make = true, appended = false;
-            ChainRec c{};
+            const int L = p == cs ? -1 : Lp;
+            bool make = true;
+            uint32_t id = 0;
+            ChainRec c = cp;
             if (L >= 0) {
-                c = cur.ov ? cur.ovc : cur.c;
+                id = (uint32_t)(key[L] >> (2 * CL_OBITS));
                 const int mg = merge_test(P, c, rb, sd.qbeg, sd.len);
                 if (mg == MERGE_APPEND) {
                     P.next[S + c.last] = o;
                     chain_append(c, o, rb, sd.qbeg, sd.len);
-                    chn[cur.id] = c;
-                    appended = true;
+                    chn[id] = c;
+                    if (L_n == L) c_n = c;  // the prefetched record is this chain's
                 }
                 make = mg == MERGE_NEW;
                 if (make && c.pos == rb) cdup = true;
             }
             code[o] = make ? CODE_NEW : CODE_SKIP;
-            bool marked = false;
-            ChainRec nc{};
             if (make) {
-                nc = ChainRec{rb, rb, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
+                const ChainRec nc{rb, rb, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
                 chn[o] = nc;
                 ++n_mine;
                 if (!cdup) {
                     mark_set(bm, sm, rk);
                     ++n_ch;
-                    marked = true;
+                    // the new mark is seed p + 1's lower chain when it lies between
+                    if (p + 1 < ce && rk < rk_n && (L_n < 0 || (uint32_t)L_n < rk)) {
+                        L_n = (int)rk;
+                        c_n = nc;
+                    }
                 }
             }
-            if (appended || marked) {
-                if (p + 1 < ce) correct(n1, appended, L, c, marked, rk, o, nc);
-                if (p + 2 < ce) correct(n2, appended, L, c, marked, rk, o, nc);
-            }
-        };
-        Ahead A{}, B{}, C{};
-        if (cs < ce) {
-            A.e = key[cs];
-            A.sd = seed[(uint32_t)(A.e >> CL_OBITS) & (uint32_t)CL_OMASK];
-            A.L = -1;
-            A.ov = false;
-        }
-        if (cs + 1 < ce) lookup(cs + 1, B);
-        for (uint32_t p = cs; p < ce; p += 3) {
-            step(p, A, B, C);
-            if (p + 1 >= ce) break;
-            step(p + 1, B, C, A);
-            if (p + 2 >= ce) break;
-            step(p + 2, C, A, B);
         }
         dup = dup || cdup;
         uint32_t tot;

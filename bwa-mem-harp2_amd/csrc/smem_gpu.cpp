@@ -161,7 +161,16 @@ struct AlnHeavyBufs {
     DevBuf<smem::RegTask> tasks, htasks;
     DevBuf<uint32_t> torder, lq, chain_read, swlist, htorder, hlq;
     DevBuf<uint8_t> tfail, sdec, htfail;
+    // the heavy walk's candidate index
+    DevBuf<uint64_t> ckey, ckey2, coff, ccnt;
+    DevBuf<uint32_t> cval, cval2, cq, cpos_s, cpos_c, chord;
+    DevBuf<int64_t> chmax, crb, cre;
+    DevBuf<uint8_t> cmade, ctmp;
+    DevBuf<uint2> crng;
     void release() {
+        ckey.release(); ckey2.release(); coff.release(); ccnt.release(); cval.release(); cval2.release();
+        cq.release(); cpos_s.release(); cpos_c.release(); chord.release(); chmax.release(); crb.release(); cre.release();
+        cmade.release(); ctmp.release(); crng.release();
         heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); ht.release(); rnext.release();
         pre.release();
         pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
@@ -1339,6 +1348,12 @@ static uint32_t aln_heavy_seeds() {
     const char* e = getenv("SMEM_ALN_HEAVY_SEEDS");
     return e ? (uint32_t)atoi(e) : 48u;
 }
+// SMEM_ALN_CAND=0: the heavy walk without the candidate index (the bin hash
+// of the regions made so far, as before it)
+static bool aln_cand_on() {
+    const char* e = getenv("SMEM_ALN_CAND");
+    return !e || atoi(e) != 0;
+}
 // SMEM_ALN_LANE=0: no regions computed ahead one seed per lane (the walks
 // extend every seed one wave per problem, round-2 style)
 static bool aln_lane_on() {
@@ -1434,10 +1449,46 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(hipMemcpyAsync(&n_heavy, P.ctr + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    smem::CandParams C{};
     if (n_heavy && P.lane_on) {  // the walk's scratch (its chains were prepared by the lane path)
         HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
         HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.ht = H.ht.p, P.rnext = H.rnext.p;
+        if (aln_cand_on()) {
+            // the candidate index's size: every heavy read's seeds and chains
+            HIP_TRY(H.ccnt.grow(n_heavy));
+            HIP_TRY(H.coff.grow(n_heavy + 1));
+            HIP_TRY(H.chord.grow(std::max(n, 1)));
+            HIP_TRY(smem_launch_aln_cand_count(&P, n_heavy, H.ccnt.p, H.chord.p, st));
+            size_t tb = 0;
+            HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)n_heavy, nullptr, &tb, st));
+            HIP_TRY(H.tmp.grow(tb + 256));
+            tb = H.tmp.n;
+            HIP_TRY(smem_launch_offsets(H.ccnt.p, H.coff.p, (int)n_heavy, H.tmp.p, &tb, st));
+            uint64_t m = 0;
+            HIP_TRY(hipMemcpyAsync(&m, H.coff.p + n_heavy, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const uint64_t mm = std::max<uint64_t>(m, 1);
+            HIP_TRY(H.ckey.grow(mm));
+            HIP_TRY(H.ckey2.grow(mm));
+            HIP_TRY(H.cval.grow(mm));
+            HIP_TRY(H.cval2.grow(mm));
+            HIP_TRY(H.chmax.grow(n_heavy));
+            HIP_TRY(H.crb.grow(mm));
+            HIP_TRY(H.cre.grow(mm));
+            HIP_TRY(H.cq.grow(mm));
+            HIP_TRY(H.cmade.grow(mm));
+            HIP_TRY(H.cpos_s.grow(std::max<uint64_t>(n_seeds, 1)));
+            HIP_TRY(H.cpos_c.grow(std::max<uint64_t>(n_chains, 1)));
+            HIP_TRY(H.crng.grow(std::max<uint64_t>(n_seeds, 1)));
+            C.key = H.ckey.p, C.key2 = H.ckey2.p, C.val = H.cval.p, C.val2 = H.cval2.p, C.off = H.coff.p;
+            C.hmax = H.chmax.p, C.hord = H.chord.p, C.n_heavy = n_heavy, C.m = m, C.n_chains = n_chains;
+            size_t sb = 0;
+            HIP_TRY(smem_launch_aln_cand(&P, &C, nullptr, &sb, g->n_cu, st));
+            HIP_TRY(H.ctmp.grow(sb + 256));
+            P.cand_rb = H.crb.p, P.cand_re = H.cre.p, P.cand_q = H.cq.p, P.cand_made = H.cmade.p;
+            P.cand_pos_s = H.cpos_s.p, P.cand_pos_c = H.cpos_c.p, P.cand_rng = H.crng.p;
+        }
     } else if (n_heavy) {
         HIP_TRY(H.hoff.grow(n_heavy + 1));
         size_t tb = 0;
@@ -1465,10 +1516,17 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, st));
         smem::AlnParams Ph = P;  // the heavy list
         Ph.tasks = H.htasks.p, Ph.torder = H.htorder.p, Ph.tfail = H.htfail.p, Ph.lq = H.hlq.p;
+        // the heavy walk's candidate index once the regions it holds are computed
+        auto cand = [&]() -> hipError_t {
+            if (!Ph.cand_made) return hipSuccess;
+            size_t sb = H.ctmp.n;
+            return smem_launch_aln_cand(&Ph, &C, H.ctmp.p, &sb, g->n_cu, st);
+        };
         if (n_heavy && st2 && ev_join) {
             HIP_TRY(hipEventRecord(ev_join, st));
             HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
             HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
+            HIP_TRY(cand());
             HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));
             HIP_TRY(smem_launch_aln_passes(&P, g->n_cu, lr, st2));
             P.light_claims = aln_light_claims();
@@ -1480,6 +1538,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         }
         if (n_heavy) {
             HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
+            HIP_TRY(cand());
             HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));
         }
         HIP_TRY(smem_launch_aln_passes(&P, g->n_cu, lr, st));

@@ -64,7 +64,8 @@ def test_aln_oracle_vs_reference(fix):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("heavy", [None, "1", "1000:2"], ids=["default", "all_heavy", "seed_heavy"])
+@pytest.mark.parametrize("heavy", [None, "1", "1000:2", "1+nocand"],
+                         ids=["default", "all_heavy", "seed_heavy", "all_heavy_bin_hash"])
 @pytest.mark.parametrize("fix", FIX, ids=[f["file"].split(".")[0] for f in FIX])
 def test_aln_gpu_vs_reference(gpu_device, fix, heavy, monkeypatch):
     """heavy = "1": every read takes the heavy-read path (regions computed
@@ -90,7 +91,9 @@ def test_aln_gpu_vs_reference(gpu_device, fix, heavy, monkeypatch):
 def _heavy_env(monkeypatch, heavy):
     """heavy = "min[:seeds]": SMEM_ALN_HEAVY_MIN / SMEM_ALN_HEAVY_SEEDS, the
     chain / seed counts from which a read takes the heavy-read path; its walk
-    then always uses the region bin hash (SMEM_ALN_HASH_MIN = 1).  A "/1"
+    then tests containment through the candidate index, or, with "+nocand"
+    (SMEM_ALN_CAND=0), always through the region bin hash (SMEM_ALN_HASH_MIN
+    = 1).  A "/1"
     suffix: the light and heavy reads' kernels one after the other on the
     batch's stream (SMEM_ALN_STREAMS=1) instead of side by side."""
     while heavy and "+" in heavy:
@@ -103,6 +106,10 @@ def _heavy_env(monkeypatch, heavy):
         elif opt == "nolane":
             # no regions computed ahead one seed per lane (SMEM_ALN_LANE=0)
             monkeypatch.setenv("SMEM_ALN_LANE", "0")
+        elif opt == "nocand":
+            # the heavy walk without the candidate index (the bin hash of the
+            # regions made so far)
+            monkeypatch.setenv("SMEM_ALN_CAND", "0")
     if heavy and "/" in heavy:
         heavy, _, streams = heavy.partition("/")
         monkeypatch.setenv("SMEM_ALN_STREAMS", streams)
@@ -142,7 +149,8 @@ def test_pack_matches_reference_pac():
 @pytest.mark.parametrize("w,a,heavy", [(100, 1, None), (20, 1, None), (100, 2, None), (100, 1, "1"), (100, 2, "1"),
                                        (20, 1, "3"), (100, 1, "0"), (100, 1, "1000:3"), (100, 1, "3/1"),
                                        (100, 1, "1+inline"), (100, 2, "3+inline"), (100, 1, "0+nolane"),
-                                       (100, 1, "1+nolane"), (100, 2, "3+nolane")])
+                                       (100, 1, "1+nolane"), (100, 2, "3+nolane"), (100, 1, "1+nocand"),
+                                       (100, 2, "3+nocand")])
 def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a, heavy, monkeypatch):
     """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
     kernel instantiations) with substitutions and Ns; chains from the GPU
