@@ -1147,39 +1147,44 @@ __device__ __forceinline__ uint64_t cand_bound(const uint64_t* key, uint64_t lo,
     return lo;
 }
 
-// one thread per chain of a heavy read, for each of its seeds: the
+// one thread per seed slot of the index (the unsorted slots: a heavy read's
+// seeds first, in seed order; its read from the slot offsets): the
 // candidates starting in [rbeg - the read's longest candidate, rbeg] (a
 // region that contains the seed starts there), narrowed to the first .. last
 // of them that contain it (a static test: whether the walk made them is its
 // own business) other than the seed's own region (made, if at all, after the
 // seed is tested).  A seed no other candidate contains gets an empty range and
-// costs the walk no round trip.
-__global__ __launch_bounds__(256) void aln_cand_range_kernel(AlnParams P, CandParams C, uint64_t n_chains) {
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n_chains;
-         c += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t cr = P.chain_read[c];
-        if (!(cr & 0x80000000u)) continue;
-        const uint32_t h = C.hord[cr & 0x7FFFFFFFu];
+// costs the walk no round trip.  (A thread per chain left the tandem-repeat
+// reads' long ranges to a few threads: 2.7 / 4.9 ms on the walk's path.)
+__global__ __launch_bounds__(256) void aln_cand_range_kernel(AlnParams P, CandParams C) {
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < C.m; u += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t lo_h = 0, hi_h = C.n_heavy;  // the read h with off[h] <= u < off[h + 1]
+        while (hi_h - lo_h > 1) {
+            const uint32_t mid = (lo_h + hi_h) >> 1;
+            if (C.off[mid] <= u) lo_h = mid;
+            else hi_h = mid;
+        }
+        const uint32_t h = lo_h;
+        const int r = P.heavy[h];
+        const uint64_t s0 = P.seed_off[r];
+        if (u - C.off[h] >= P.seed_off[r + 1] - s0) continue;  // a chain slot
+        const uint64_t j = s0 + (u - C.off[h]);
         const uint64_t lo = C.off[h], hi = C.off[h + 1];
         const int64_t mx = C.hmax[h];
-        const OutChain ch = P.chains[c];
-        for (int i = 0; i < ch.n; ++i) {
-            const uint64_t j = ch.seed_off + (uint64_t)i;
-            const SeedRec sd = P.seeds[j];
-            const uint64_t x = cand_bound(C.key2, lo, hi, (uint64_t)(sd.rbeg - mx > 0 ? sd.rbeg - mx : 0), false);
-            const uint64_t y = cand_bound(C.key2, x, hi, (uint64_t)sd.rbeg, true);
-            const uint32_t own = P.pre_ok[j] ? P.cand_pos_s[j] : 0xFFFFFFFFu;
-            uint32_t f = 0xFFFFFFFFu, l = 0;
-            for (uint64_t q = x; q < y; ++q) {
-                const uint32_t pq = P.cand_q[q];
-                if ((uint32_t)q != own &&
-                    reg_contains(P, sd.rbeg, sd.qbeg, sd.len, P.cand_rb[q], P.cand_re[q], (int)(pq & 0xFFFFu), (int)(pq >> 16))) {
-                    f = f < (uint32_t)q ? f : (uint32_t)q;
-                    l = (uint32_t)q + 1;
-                }
+        const SeedRec sd = P.seeds[j];
+        const uint64_t x = cand_bound(C.key2, lo, hi, (uint64_t)(sd.rbeg - mx > 0 ? sd.rbeg - mx : 0), false);
+        const uint64_t y = cand_bound(C.key2, x, hi, (uint64_t)sd.rbeg, true);
+        const uint32_t own = P.pre_ok[j] ? P.cand_pos_s[j] : 0xFFFFFFFFu;
+        uint32_t f = 0xFFFFFFFFu, l = 0;
+        for (uint64_t q = x; q < y; ++q) {
+            const uint32_t pq = P.cand_q[q];
+            if ((uint32_t)q != own &&
+                reg_contains(P, sd.rbeg, sd.qbeg, sd.len, P.cand_rb[q], P.cand_re[q], (int)(pq & 0xFFFFu), (int)(pq >> 16))) {
+                f = f < (uint32_t)q ? f : (uint32_t)q;
+                l = (uint32_t)q + 1;
             }
-            P.cand_rng[j] = f == 0xFFFFFFFFu ? make_uint2(0, 0) : make_uint2(f, l);
         }
+        P.cand_rng[j] = f == 0xFFFFFFFFu ? make_uint2(0, 0) : make_uint2(f, l);
     }
 }
 
@@ -1631,7 +1636,7 @@ extern "C" hipError_t smem_launch_aln_cand(const smem::AlnParams* P, const smem:
                                                                (int)C->m, (int)C->n_heavy, C->off, C->off + 1, 0, 34, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(smem::aln_cand_place_kernel, dim3(n_cu * 16), dim3(256), 0, st, *P, *C);
-    hipLaunchKernelGGL(smem::aln_cand_range_kernel, dim3(n_cu * 16), dim3(256), 0, st, *P, *C, C->n_chains);
+    hipLaunchKernelGGL(smem::aln_cand_range_kernel, dim3(n_cu * 16), dim3(256), 0, st, *P, *C);
     return hipGetLastError();
 }
 
