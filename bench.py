@@ -37,7 +37,7 @@ same with the 32-B buckets this build actually reads.  The kernel is bound by
 random-request rate, not bytes: request_roofline compares its L2 fabric read
 requests per second (rocprofv3 TCC_EA0_RDREQ recorded by tools/traffic.py for
 this build and workload) with the random-gather ceiling measured on this GPU
-(tools/gather_ceiling.hip, profiles/r02/gather_ceiling.json).
+(tools/gather_ceiling.hip, profiles/gather_ceiling.json).
 
 cpu_baseline: the reference's own C (oracle/_ref/ref_harness, compiled from
 the reference sources) when present, else the C restatement, timed on this
@@ -128,7 +128,7 @@ def parse(argv=None):
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch TCC_EA0_RDREQ / FETCH_SIZE recorded by tools/traffic.py for this build + workload")
-    p.add_argument("--ceiling-json", default=os.path.join(ROOT, "profiles", "r02", "gather_ceiling.json"))
+    p.add_argument("--ceiling-json", default=os.path.join(ROOT, "profiles", "gather_ceiling.json"))
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     a.read_len = a.read_len or cfg["read_len"]
