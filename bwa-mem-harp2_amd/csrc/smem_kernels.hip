@@ -479,8 +479,12 @@ __device__ __forceinline__ uint64_t stamp() {
 // result is the one bwt_extend computes.  The lane keeps the 2-bit codes of
 // its forward string (first kt_k bases) and, in the backward phase, of the
 // kt_k bases from the current position (rolled one base per step).
+// PRIO (A/B): wave priority by phase -- 1: raised from the top of an
+// iteration (the advance) until its loads are issued, 2: raised for the
+// extend arithmetic after the wait (s_setprio; the SQ's arbitration between
+// the three waves of a SIMD)
 template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
-          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool PFCH = false>
+          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool PFCH = false, int PRIO = 0>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -596,6 +600,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     for (;;) {
         uint64_t ta = 0;
         if constexpr (STAMP) ta = stamp();
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(2);
         // claiming the next read and loading its offsets: here, at the top of the
         // iteration, where no bucket DMA is in flight yet for their waits to cover
         if constexpr (PFCH) {
@@ -1134,7 +1139,9 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     s_l2 = bl2 == tag0 ? 0 : 1;
                 }
             }
+            if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(2);
             const int ks = fks < 0 ? 0 : fks, ls = fls < 0 ? 0 : fls;
             wk = ks == 0 ? Bucket32{s0a, s0b} : Bucket32{s1a, s1b};
             wl = ls == 0 ? Bucket32{s0a, s0b} : Bucket32{s1a, s1b};
@@ -1213,6 +1220,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
             else
                 extend_counts(P, ra, rb, rs, rc, kk, ll, vk, vl, na, nb, ns);
         }
+        if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
         if (helper) {  // entry + result for the owner's next BWD_RES
             W->pn[vlane()] = hent;
             W->q[vlane()] = pack_p(na, nb, ns, 0);
@@ -1322,10 +1330,10 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
 #ifdef SMEM_AB_VARIANTS
-    return variant == 0 || (variant >= 2 && variant <= 25);
+    return variant == 0 || (variant >= 2 && variant <= 27);
 #else
     return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23 || variant == 24 ||
-           variant == 25;
+           variant == 25 || variant == 26 || variant == 27;
 #endif
 }
 
@@ -1338,6 +1346,9 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 24: the default with the next read claimed and loaded in the uniform section (PFCH); 25: its stamped twin
         case 24: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 25: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 26 / 27: the default with wave priority raised in the advance / in the extend arithmetic (PRIO)
+        case 26: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 27: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 2>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
