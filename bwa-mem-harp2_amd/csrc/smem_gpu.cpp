@@ -354,7 +354,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
     g_err[0] = 0;
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 27))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 28))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
 
     if (!smem_seed_variant_built(variant))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: A/B variant not in this build (make AB=1)");

@@ -1323,17 +1323,17 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 }  // namespace smem
 
 // ------------------------------------------------------------ host launchers
-// The product build instantiates the default kernel (2; 0 and 20 name it too),
+// The product build instantiates the default kernel (2; 0, 20 and 26 name it too),
 // its stamped diagnostic twin (9) and the k-mer table variant (23).  The other
 // A/B variants measured in rounds 1-2 are compiled only with
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
 #ifdef SMEM_AB_VARIANTS
-    return variant == 0 || (variant >= 2 && variant <= 27);
+    return variant == 0 || (variant >= 2 && variant <= 28);
 #else
     return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23 || variant == 24 ||
-           variant == 25 || variant == 26 || variant == 27;
+           variant == 25 || variant == 26 || variant == 27 || variant == 28;
 #endif
 }
 
@@ -1346,8 +1346,9 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 24: the default with the next read claimed and loaded in the uniform section (PFCH); 25: its stamped twin
         case 24: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 25: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
-        // 26 / 27: the default with wave priority raised in the advance / in the extend arithmetic (PRIO)
-        case 26: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 27: wave priority raised in the extend arithmetic instead (PRIO 2: no change measured);
+        // 28: the default without wave priority (round-2 default; 2 % slower, profiles/r03/ab/prio)
+        case 28: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 27: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 2>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
@@ -1376,9 +1377,12 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 21: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 7, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 22: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, true, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
 #endif
-        // default (2): Occ64, the two bucket slots per lane in registers, 11 list
-        // entries per lane in LDS (the forward list as a ring of its last 11 pushes)
-        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // default (2; 0, 20 and 26 name it too): Occ64, the two bucket slots per
+        // lane in registers, 11 list entries per lane in LDS (the forward list as
+        // a ring of its last 11 pushes), wave priority raised from the top of an
+        // iteration until its loads are issued (PRIO 1: busy 24.93 -> 24.44 ms
+        // uniform, 32.38 -> 31.88 ms human-like against variant 28)
+        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }
