@@ -653,7 +653,7 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
     with tempfile.TemporaryDirectory(dir=args.cache) as d:
         fq = os.path.join(d, "r.fq")
         synth.write_fastq(fq, sub)
-        env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu))
+        env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu), SMEM_GPU_TIMES="1")
         legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq], {}),
                 ("gpu_chains_only", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq],
                  {"SMEM_GPU_STAGES": "1"}),
@@ -703,6 +703,8 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
             log(f"e2e {tag}{name} failed ({p.returncode}): {err[-800:]}")
             return None
         n_proc, real = _mem_times(err)
+        import re
+        gt = [float(x) for x in re.findall(r"\[M::mem_batch_gpu\] \d+ reads through the GPU stages in ([\d.]+) s", err)]
         digest, n_lines = _sam_body(sam)
         os.unlink(sam)
         runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
@@ -711,6 +713,13 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
                       "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
                       "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
                       "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
+        if gt:  # the integration patch's per-batch wall time of mem_batch_gpu (SMEM_GPU_TIMES=1)
+            runs[name].update(gpu_batches=len(gt), gpu_stage_s_sum=round(sum(gt), 3),
+                              gpu_stage_s_max=round(max(gt), 4),
+                              gpu_stage_note="sum over the kt_for_batch workers' batches of the time each spent in "
+                                             "mem_batch_gpu (seeding -> regions on the GPU, waits included); "
+                                             "workers run concurrently, so sum / threads is the per-worker share of "
+                                             "mem_process_seqs")
         log(f"e2e {tag}{name}: {wall:.1f} s wall, mem_process_seqs {real:.1f} s")
     return runs
 
