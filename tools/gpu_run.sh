@@ -17,6 +17,8 @@
 #   stamps[:ARGS]     tools/stamps.py (variant-9 cycle split)        -> stamps<k>.log
 #   aln[:ARGS] / chain[:ARGS]   tools/aln_prof.py / tools/chain_prof.py under rocprofv3 --kernel-trace --stats
 #   py:SCRIPT[:ARGS]  python SCRIPT ARGS                              -> py<k>.log
+#   dist2[:ARGS]      bench.py --gpus 2 ARGS under torch.distributed.run, two ranks (on a one-GPU box both
+#                     share cuda:0 over gloo: the driver's N>1 launch line rehearsed) -> dist2_<k>.json / .err
 #   env:VAR=v[,VAR=v] exported for the steps after it (e.g. env:PMC_PROG=tools/aln_prof.py,PMC_KERNEL=aln_kernel)
 # Replaces round 2's one-off tools/gpu_r02*.sh scripts (their outputs are under profiles/r02/).
 set -o pipefail
@@ -64,6 +66,10 @@ for step in "$@"; do
     aln|chain)
       timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name$k" -o run -- \
         python3 -u tools/${name}_prof.py $args > "$OUT/$name$k.log" 2>&1 || { echo "$name failed"; exit $k; } ;;
+    dist2)
+      timeout -k 10 900 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 2 $args > "$OUT/dist2_$k.json" 2> "$OUT/dist2_$k.err" \
+        || { echo "dist2 failed"; tail -5 "$OUT/dist2_$k.err"; exit $k; } ;;
     env)
       export $args ;;
     py)
