@@ -705,6 +705,8 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
         n_proc, real = _mem_times(err)
         import re
         gt = [float(x) for x in re.findall(r"\[M::mem_batch_gpu\] \d+ reads through the GPU stages in ([\d.]+) s", err)]
+        gparts = [tuple(float(v) for v in m) for m in re.findall(
+            r"\(seed ([\d.]+) sa ([\d.]+) chain ([\d.]+) regions ([\d.]+) fetch ([\d.]+)\)", err)]
         digest, n_lines = _sam_body(sam)
         os.unlink(sam)
         runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
@@ -714,6 +716,10 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
                       "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
                       "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
         if gt:  # the integration patch's per-batch wall time of mem_batch_gpu (SMEM_GPU_TIMES=1)
+            if gparts:
+                runs[name]["gpu_stage_s_sum_by_stage"] = {
+                    k: round(sum(p[i] for p in gparts), 3)
+                    for i, k in enumerate(("seed", "sa", "chain", "regions", "fetch"))}
             runs[name].update(gpu_batches=len(gt), gpu_stage_s_sum=round(sum(gt), 3),
                               gpu_stage_s_max=round(max(gt), 4),
                               gpu_stage_note="sum over the kt_for_batch workers' batches of the time each spent in "
