@@ -1,0 +1,61 @@
+"""Run the product path (bwa-gpu mem) on the bench's human-size index and reads
+with the stderr kept: per-batch GPU timings, refusals and their error text.
+
+    python tools/e2e_probe.py [--reads 200000] [--threads 16] [bench args]  (env passes through)
+"""
+import argparse
+import hashlib
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--reads", type=int, default=200_000)
+    p.add_argument("--threads", type=int, default=16)
+    p.add_argument("--out", default=None)
+    own, rest = p.parse_known_args()
+    import torch
+    torch.cuda.device_count()
+    import bench
+    from smemgpu import synth
+    a = bench.parse(rest)
+    idx, _, sa, codes = bench.get_index(a, 0, lambda: None, 0)
+    reads = bench.make_reads(a, 0, codes, 1)
+    base = bench.genome_key(a)
+    if not all(os.path.exists(base + e) for e in (".pac", ".ann", ".amb")):
+        synth.write_bwa_bns(base + ".tmp", codes)
+        for e in (".pac", ".ann", ".amb"):
+            os.replace(base + ".tmp" + e, base + e)
+    m = min(own.reads, reads.n)
+    sub = reads.subset(range(m))
+    with tempfile.TemporaryDirectory(dir=a.cache) as d:
+        fq = os.path.join(d, "r.fq")
+        synth.write_fastq(fq, sub)
+        batch = max(1024, -(-m // own.threads))
+        for name, cmd in (("gpu", [bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(batch), base, fq]),
+                          ("ref", [bench.REF_HARNESS, "mem", base, fq, str(own.threads), "1", "0"])):
+            t = time.time()
+            p2 = subprocess.run(cmd, capture_output=True, env=dict(os.environ, SMEM_GPU_TIMES="1"), timeout=900)
+            body = b"\n".join(l for l in p2.stdout.split(b"\n") if not l.startswith(b"@PG"))
+            err = p2.stderr.decode(errors="replace")
+            keep = [l for l in err.split("\n") if "mem_batch_gpu" in l or "[W::" in l or "[E::" in l or "rror" in l]
+            nl = body.count(b"\n")
+            print(f"== {name}: rc {p2.returncode}, {time.time() - t:.1f} s, sha {hashlib.sha256(body).hexdigest()[:16]}, "
+                  f"{nl} lines", flush=True)
+            for l in keep[:60]:
+                print("   ", l, flush=True)
+            if own.out:
+                with open(os.path.join(own.out, name + ".sam"), "wb") as fh:
+                    fh.write(body)
+
+
+if __name__ == "__main__":
+    main()
