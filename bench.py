@@ -604,6 +604,14 @@ def _mem_times(stderr: str) -> tuple:
     return n, real
 
 
+def _mem_chunks(stderr: str) -> list:
+    """(reads, real seconds) of each mem_process_seqs chunk: the first chunk
+    also pays each worker batch's first-use device and pinned allocations."""
+    import re
+    return [(int(m.group(1)), float(m.group(3))) for m in re.finditer(
+        r"\[M::mem_process_seqs\] Processed (\d+) reads in ([\d.]+) CPU sec, ([\d.]+) real sec", stderr)]
+
+
 def _sam_body(path: str):
     """sha256 and line count of a SAM file without its @PG line."""
     import hashlib
@@ -715,6 +723,11 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
                       "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
                       "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
                       "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
+        ch = _mem_chunks(err)
+        if len(ch) > 1:
+            runs[name]["mem_process_seqs_chunks"] = [[c, round(t, 3)] for c, t in ch]
+            rest = ch[1:]
+            runs[name]["reads_per_s_after_first_chunk"] = round(sum(c for c, _ in rest) / max(sum(t for _, t in rest), 1e-9), 1)
         if gt:  # the integration patch's per-batch wall time of mem_batch_gpu (SMEM_GPU_TIMES=1)
             if gparts:
                 runs[name]["gpu_stage_s_sum_by_stage"] = {
