@@ -1823,7 +1823,7 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
                          smem_stream_stats_t* stats) {
     g_err[0] = 0;
     if (!g || !opt || n_reads < 0 || (n_reads > 0 && (!codes || !offs)) || chunk_reads <= 0 || n_workers <= 0 ||
-        n_workers > 64 || (flags & ~(SMEM_STREAM_PAIRS | SMEM_STREAM_PACKED)))
+        n_workers > 64 || (flags & ~(SMEM_STREAM_PAIRS | SMEM_STREAM_PACKED | SMEM_STREAM_RELEASE)))
         return fail(SMEM_E_ARG, "smem_gpu_seed_stream: bad arguments");
     const bool pairs = flags & SMEM_STREAM_PAIRS, packed = flags & SMEM_STREAM_PACKED;
     if (pairs) {
@@ -1940,9 +1940,17 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
                 b->packed = false;
                 // kept for the next call, at most this call's worker count (each
                 // pins its staging and result buffers: ~1 GB per 1M-read chunk)
-                if (rc == SMEM_OK && g->stream_pool.size() < (size_t)nw) g->stream_pool.push_back(b);
-                else smem_batch_destroy(b);
+                if (rc == SMEM_OK && !(flags & SMEM_STREAM_RELEASE) && g->stream_pool.size() < (size_t)nw)
+                    g->stream_pool.push_back(b);
+                else
+                    smem_batch_destroy(b);
             }
+        // an earlier call's larger pool shrinks to this call's workers
+        const size_t keep = (flags & SMEM_STREAM_RELEASE) ? 0 : (size_t)nw;
+        while (g->stream_pool.size() > keep) {
+            smem_batch_destroy(g->stream_pool.back());
+            g->stream_pool.pop_back();
+        }
     }
     if (rc != SMEM_OK) {
         if (!emsg.empty()) snprintf(g_err, sizeof(g_err), "smem_gpu_seed_stream: %s", emsg.c_str());

@@ -442,11 +442,13 @@ class Gpu:
         return Batch(self, max_reads, max_bases, max_len)
 
     def seed_stream(self, codes: np.ndarray, offs: np.ndarray, opt: "Options" = None, chunk_reads: int = 1 << 20,
-                    workers: int = 3, pairs: bool = False, collect: bool = False, packed: bool = False) -> tuple:
+                    workers: int = 3, pairs: bool = False, collect: bool = False, packed: bool = False,
+                    release: bool = False) -> tuple:
         """Stream a read set through smem_gpu_seed_stream (chunks of
         chunk_reads, `workers` host workers each with its own batch and HIP
-        stream; packed: 16-B wire entries).  Returns (stats dict, per-chunk
-        Results in chunk order when collect else None)."""
+        stream; packed: 16-B wire entries; release: free the workers'
+        batches instead of keeping them for the next call).  Returns (stats
+        dict, per-chunk Results in chunk order when collect else None)."""
         lib = load()
         codes = np.ascontiguousarray(codes, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
@@ -465,7 +467,7 @@ class Gpu:
 
         cb = CHUNK_FN(on_chunk) if collect else None
         rc = lib.smem_gpu_seed_stream(self._h, offs.size - 1, codes.ctypes.data, offs.ctypes.data, C.byref(o),
-                                      int(chunk_reads), int(workers), (1 if pairs else 0) | (2 if packed else 0),
+                                      int(chunk_reads), int(workers), (1 if pairs else 0) | (2 if packed else 0) | (4 if release else 0),
                                       C.cast(cb, C.c_void_p) if cb else None, None, C.byref(st))
         if err:
             raise err[0]

@@ -177,11 +177,16 @@ int  smem_gpu_collect_ex(smem_gpu_t *gpu, int slot, int n_reads, const uint8_t *
  * software/bwamem.c:1600-1609 reads them) land in one chunk;
  * SMEM_STREAM_PACKED -- each interval crosses PCIe as a 16-B smem_pintv_t
  * (reads < 8192 bp), read with smem_batch_results_packed + smem_pintv_unpack
- * in the callback.  fn may be NULL; a non-zero return from fn stops the
- * stream and is returned. */
+ * in the callback; SMEM_STREAM_RELEASE -- free the workers' batches when the
+ * call returns.  Otherwise the handle keeps at most n_workers of them for
+ * the next call (each holds ~1 GB of pinned host memory per 1M-read chunk;
+ * a later call with fewer workers shrinks the pool, smem_gpu_destroy frees
+ * it).  fn may be NULL; a non-zero return from fn stops the stream and is
+ * returned. */
 typedef int (*smem_chunk_fn)(void *ctx, int64_t chunk, int64_t first_read, int n_reads, const smem_batch_t *b);
 #define SMEM_STREAM_PAIRS   1   /* interleaved mates: chunks keep pairs whole */
 #define SMEM_STREAM_PACKED  2   /* results as 16-B smem_pintv_t (smem_batch_results_packed): half the D2H */
+#define SMEM_STREAM_RELEASE 4   /* do not keep the workers' batches (pinned buffers) for the next call */
 typedef struct {
 	double wall_s;           /* first chunk claimed -> last chunk delivered */
 	uint64_t n_reads, n_chunks, n_intv;

@@ -88,6 +88,21 @@ def test_stream_options_and_edges(world):
     assert st["n_reads"] == 0 and chunks == []
 
 
+def test_stream_pool_reuse_and_release(world):
+    """Batches kept from a 4-worker call serve a 2-worker call (the pool then
+    shrinks to 2), SMEM_STREAM_RELEASE empties it, and the next call builds
+    fresh batches: every result equals the oracle's."""
+    import smemgpu
+    from smemgpu import synth
+    reads = synth.make_reads(world["codes"], 3000, 150, seed=11, sub_rate=0.03)
+    want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=8)
+    for workers, release in ((4, False), (2, False), (3, True), (2, False)):
+        st, chunks = world["gpu"].seed_stream(reads.codes, reads.offs, smemgpu.Options(), chunk_reads=500,
+                                              workers=workers, collect=True, packed=True, release=release)
+        assert st["workers"] == workers
+        assert _joined(chunks, reads.n).to_smgo() == want
+
+
 def test_pintv_roundtrip_limits(world):
     """The 16-B wire entry carries 34-bit coordinates and 13-bit query
     positions; reads past 8191 bp are refused in packed mode."""
