@@ -306,9 +306,12 @@ def cpu_inventory() -> dict:
     return inv
 
 
-def traffic_for(args, path: str, build_id: str):
+def traffic_for(args, path: str, build_id: str, kernel_id: str | None = None, launch: dict | None = None):
     """Per-launch memory-side counters of seed_kernel recorded by
-    tools/traffic.py for this exact workload AND this library build, or None."""
+    tools/traffic.py for this exact workload AND either this library build or
+    this seeding kernel (smem_gpu_kernel_id: its sources and compile flags) at
+    this launch shape (grid, block), or None.  The second form keeps the
+    counters of a kernel that a runtime-only change did not touch."""
     if not path or not os.path.exists(path):
         return None
     with open(path) as fh:
@@ -316,9 +319,13 @@ def traffic_for(args, path: str, build_id: str):
     w = t.get("workload", {})
     want = {"genome_mbp": args.genome_mbp, "reads": args.reads, "read_len": args.read_len, "seed": args.seed,
             "sub": args.sub, "genome_profile": args.genome_profile}
-    if any(w.get(k) != v for k, v in want.items()) or t.get("build_id") != build_id:
+    if any(w.get(k) != v for k, v in want.items()):
         return None
-    return t
+    if t.get("build_id") == build_id:
+        return dict(t, matched_on="build_id")
+    if kernel_id and t.get("kernel_id") == kernel_id and launch and t.get("launch") == launch:
+        return dict(t, matched_on="kernel_id + launch shape")
+    return None
 
 
 def gather_ceiling(path: str):
@@ -764,7 +771,8 @@ def span_union(spans) -> float:
     return float(tot + (cur[1] - cur[0] if cur else 0))
 
 
-def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id, busy_ms, clock_check) -> dict:
+def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id, busy_ms, clock_check,
+             launch: dict | None = None) -> dict:
     achieved = bpr * reads_n / (busy_ms * 1e-3) / 1e9
     out = {
         "bound": "hbm",
@@ -795,8 +803,11 @@ def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id,
         "extends_per_read": round(ostats["n_ext"] / max(n_counted, 1), 1),
         "occ64_buckets_per_read": round(ostats["n_bkt64"] / max(n_counted, 1), 1),
     }
-    t = traffic_for(args, args.traffic_json, build_id)
+    import smemgpu
+    t = traffic_for(args, args.traffic_json, build_id, smemgpu.kernel_id(), launch)
     if t:
+        out["traffic_build"] = {"build_id": t.get("build_id"), "kernel_id": t.get("kernel_id"),
+                                "matched_on": t.get("matched_on")}
         rq = float(t["rdreq_per_launch"])
         out["traffic"] = round(rq * 64.0, 1)   # one 64-B line per fabric read request (FETCH_SIZE calibration)
         out["traffic_note"] = ("TCC_EA0_RDREQ x 64 B per launch (tools/traffic.py, " + t.get("measured", "?") +
@@ -919,7 +930,7 @@ def human_like_report(args, d, cores) -> dict:
     T["batch"].close()
     gpu.close()
     rf = roofline(h, bpr, bpr64, ostats, n_counted, reads.n, T["k_ms"], T["a_ms"], smemgpu.build_id(), T["busy_ms"],
-                  T["clock_check"])
+                  T["clock_check"], {"grid": T["st"]["grid"], "block": T["st"]["block"]})
     out = {"value": round(T["value"], 1), "unit": "reads/s", "ms_per_step": round(T["elapsed_max"] / args.steps * 1e3, 3),
            "steps": args.steps, "genome_profile": "human", "reads": reads.n, "read_len": args.read_len,
            "kernel_busy_ms": rf["kernel_busy_ms"], "kernel_ms_alone": rf["kernel_ms_alone"],
@@ -1019,7 +1030,7 @@ def main():
                 "kernel_variant": args.variant or 2, "kmer_k": args.kmer_k,
             },
             "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, T["k_ms"], T["a_ms"], smemgpu.build_id(),
-                                 T["busy_ms"], T["clock_check"]),
+                                 T["busy_ms"], T["clock_check"], {"grid": st["grid"], "block": st["block"]}),
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "compact_ms": round(T["compact_alone"], 3),
@@ -1030,6 +1041,7 @@ def main():
             "sw_extension": sw_rep,
             "overflow_reads": st["n_overflow"],
             "build_id": smemgpu.build_id(),
+            "kernel_id": smemgpu.kernel_id(),
             "build_id_matches_sources": smemgpu.build_id() == smemgpu.source_hash(),
         }
     batch.close()

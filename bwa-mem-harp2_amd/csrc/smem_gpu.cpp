@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -40,14 +41,56 @@ static_assert(sizeof(Intv) == sizeof(smem_intv_t), "interval layout");
 namespace {
 
 thread_local char g_err[512];
+// set when a HIP call of this thread's current entry point failed with a
+// runtime error (not an allocation failure): the device is then marked
+// faulted when the call leaves (see DeviceCall)
+thread_local int g_hip_fault = 0;
+// the library's own warm-up calls are not counted by SMEM_GPU_FAIL
+thread_local int g_no_inject = 0;
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     if (e != hipSuccess)
         snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
     else
         snprintf(g_err, sizeof(g_err), "%s", what);
+    // an allocation that does not fit is a refusal, not a broken device
+    if (code == SMEM_E_DEVICE && e == hipErrorOutOfMemory) return SMEM_E_NOMEM;
+    if (code == SMEM_E_DEVICE && e != hipSuccess) g_hip_fault = 1;
     return code;
 }
+
+// SMEM_GPU_FAIL=<stage>:<k>[:sticky] -- fault injection for the reject -> CPU
+// path: every k-th call (process-wide) of the stage returns SMEM_E_DEVICE
+// after its work is enqueued and before it is waited for, so the drain on the
+// way out is what keeps that work from landing after the caller resumed.
+// stage: upload (smem_batch_set_reads*), seed (smem_batch_run), sa, chain,
+// aln (smem_batch_chain2aln), fetch, or any.  ":sticky" also marks the
+// device faulted, as a real runtime failure does.
+enum { ST_UPLOAD, ST_SEED, ST_SA, ST_CHAIN, ST_ALN, ST_FETCH, ST_N };
+const char* const k_stage_name[ST_N] = {"upload", "seed", "sa", "chain", "aln", "fetch"};
+std::atomic<uint64_t> g_stage_calls[ST_N];
+
+int inject_fault(int stage) {
+    const char* e = getenv("SMEM_GPU_FAIL");
+    if (!e || !*e || g_no_inject) return SMEM_OK;
+    const char* c = strchr(e, ':');
+    if (!c) return SMEM_OK;
+    const std::string name(e, (size_t)(c - e));
+    if (name != "any" && name != k_stage_name[stage]) return SMEM_OK;
+    const long k = strtol(c + 1, nullptr, 10);
+    if (k <= 0) return SMEM_OK;
+    const uint64_t n = g_stage_calls[stage].fetch_add(1) + 1;
+    if (n % (uint64_t)k) return SMEM_OK;
+    snprintf(g_err, sizeof(g_err), "injected failure (SMEM_GPU_FAIL=%s): stage %s, call %llu", e, k_stage_name[stage],
+             (unsigned long long)n);
+    if (strstr(c + 1, ":sticky")) g_hip_fault = 1;
+    return SMEM_E_DEVICE;
+}
+
+#define INJECT(stage)                                   \
+    do {                                                \
+        if (int _r = inject_fault(stage)) return _r;    \
+    } while (0)
 
 #define HIP_TRY(expr)                                                   \
     do {                                                                \
@@ -146,6 +189,32 @@ struct smem_gpu {
     // smem_gpu_seed_stream's worker batches, kept between calls: creating one
     // pins ~1 GB of host memory and allocates its device buffers
     std::vector<smem_batch_t*> stream_pool;
+    // Admission (the role of the reference's HARP manager thread,
+    // software/fastmap.c:320-429, which let one worker batch at a time onto
+    // the FPGA and turned the others away): every entry point that runs work
+    // on the device leases one of at most max_active stream pairs (a normal
+    // and a low-priority stream) for the duration of the call; more
+    // concurrent calls wait for a pair.  So a device never carries more than
+    // 2 x max_active streams, however many kt_for_batch workers share it.
+    int max_active = 8;
+    std::mutex adm_mu;
+    std::condition_variable adm_cv;
+    std::vector<std::pair<hipStream_t, hipStream_t>> pairs;
+    std::vector<int> free_pairs;
+    int n_leased = 0;
+    // a HIP runtime failure seen by any call: every later call fails at once
+    // (SMEM_E_DEVICE) without touching the device, so the caller's reads take
+    // its CPU path (software/bwt.c:686-717) and nothing more is enqueued on a
+    // queue the runtime may have aborted
+    std::atomic<int> faulted{0};
+    char fault_msg[512] = {0};
+    // background preparation started by smem_gpu_init_devices /
+    // smem_gpu_reserve_slots: the densified SA (an event on init_st) and the
+    // worker slots' pre-sized batches (a host thread)
+    hipStream_t init_st = nullptr;
+    hipEvent_t sa_ready = nullptr;
+    uint64_t* d_sa_raw = nullptr;  // the .sa as uploaded, freed once sa_ready has passed
+    std::shared_future<int> reserve;
 };
 
 // scratch of the heavy-read path of chains -> regions
@@ -260,12 +329,95 @@ struct smem_batch {
     smem_batch_stats_t stats{};
 };
 
+// ---- admission and the drain on the way out of every device call
+static int gpu_check(smem_gpu_t* g) {
+    if (!g->faulted.load()) return SMEM_OK;
+    snprintf(g_err, sizeof(g_err), "device %d faulted earlier (%s): refused", g->device, g->fault_msg);
+    return SMEM_E_DEVICE;
+}
+
+// One entry point's tenure on the device: refused at once on a faulted
+// device, else it waits for one of the device's max_active stream pairs.  On
+// the way out -- success, refusal or error alike -- both streams are
+// synchronised before the pair goes back, so no kernel or copy of the call
+// is still in flight (into the caller's or the library's host memory) once
+// the caller resumes; a HIP runtime failure during the call marks the device
+// faulted.
+struct DeviceCall {
+    smem_gpu_t* g;
+    int pair = -1;
+    hipStream_t st = nullptr, st2 = nullptr;
+    int rc = SMEM_OK;
+    explicit DeviceCall(smem_gpu_t* g_) : g(g_) {
+        g_err[0] = 0;
+        g_hip_fault = 0;
+        if ((rc = gpu_check(g))) return;
+        hipError_t e = hipSetDevice(g->device);
+        if (e != hipSuccess) {
+            rc = fail(SMEM_E_DEVICE, "hipSetDevice", e);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(g->adm_mu);
+        g->adm_cv.wait(lk, [&] { return !g->free_pairs.empty() || (int)g->pairs.size() < g->max_active; });
+        if (!g->free_pairs.empty()) {
+            pair = g->free_pairs.back();
+            g->free_pairs.pop_back();
+        } else {
+            hipStream_t a = nullptr, b = nullptr;
+            int least = 0, greatest = 0;
+            e = hipStreamCreateWithFlags(&a, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+            if (e == hipSuccess) e = hipStreamCreateWithPriority(&b, hipStreamNonBlocking, least);
+            if (e != hipSuccess) {
+                if (a) (void)hipStreamDestroy(a);
+                rc = fail(SMEM_E_DEVICE, "admission: hipStreamCreate", e);
+                g->adm_cv.notify_one();
+                return;
+            }
+            g->pairs.emplace_back(a, b);
+            pair = (int)g->pairs.size() - 1;
+        }
+        ++g->n_leased;
+        st = g->pairs[(size_t)pair].first;
+        st2 = g->pairs[(size_t)pair].second;
+    }
+    DeviceCall(const DeviceCall&) = delete;
+    DeviceCall& operator=(const DeviceCall&) = delete;
+    ~DeviceCall() {
+        if (pair >= 0) {
+            (void)hipStreamSynchronize(st2);
+            (void)hipStreamSynchronize(st);
+            std::lock_guard<std::mutex> lk(g->adm_mu);
+            g->free_pairs.push_back(pair);
+            --g->n_leased;
+            g->adm_cv.notify_one();
+        }
+        if (g_hip_fault && !g->faulted.exchange(1)) {
+            std::lock_guard<std::mutex> lk(g->adm_mu);
+            snprintf(g->fault_msg, sizeof(g->fault_msg), "%s", g_err);
+        }
+    }
+};
+
+// a batch's call: the leased pair is the batch's st / st2 for its duration
+struct BatchCall : DeviceCall {
+    smem_batch_t* b;
+    explicit BatchCall(smem_batch_t* b_) : DeviceCall(b_->g), b(b_) {
+        if (rc == SMEM_OK) b->st = st, b->st2 = st2;
+    }
+    ~BatchCall() { b->st = b->st2 = nullptr; }
+};
+
 extern "C" {
 
 #ifndef SMEM_SRC_HASH
 #define SMEM_SRC_HASH "unknown"
 #endif
 const char* smem_gpu_build_id(void) { return SMEM_SRC_HASH; }
+#ifndef SMEM_KERNEL_HASH
+#define SMEM_KERNEL_HASH "unknown"
+#endif
+const char* smem_gpu_kernel_id(void) { return SMEM_KERNEL_HASH; }
 
 const char* smem_strerror(int code) {
     if (g_err[0]) return g_err;
@@ -315,6 +467,7 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
     if (!g) return fail(SMEM_E_NOMEM, "smem_gpu_init");
     g->device = device;
     g->n_cu = prop.multiProcessorCount;
+    if (const char* v = getenv("SMEM_GPU_MAX_ACTIVE")) g->max_active = std::max(1, std::min(256, atoi(v)));
     g->bwt_size = bwt_size;
     g->primary = primary;
     std::memcpy(g->L2, L2, sizeof(g->L2));
@@ -413,8 +566,9 @@ int smem_gpu_set_intv_cap(smem_gpu_t* g, int cap_per_read) {
 
 void smem_batch_destroy(smem_batch_t* b) {
     if (!b) return;
+    // (every call drained its work before returning: nothing of this batch
+    // is in flight, and its streams belong to the device's admission pool)
     (void)hipSetDevice(b->g->device);
-    if (b->st) (void)hipStreamSynchronize(b->st);
     b->h_codes.release(); b->h_offs.release(); b->d_codes.release(); b->d_offs.release();
     b->d_out_intv.release(); b->d_out_call.release(); b->d_n_intv.release(); b->d_n_calls.release();
     b->d_ctr.release(); b->d_ovf_items.release(); b->d_ovf_slot.release(); b->d_ovf_items2.release();
@@ -436,13 +590,12 @@ void smem_batch_destroy(smem_batch_t* b) {
         if (ev) (void)hipEventDestroy(ev);
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
-    if (b->st2) (void)hipStreamDestroy(b->st2);
-    if (b->st) (void)hipStreamDestroy(b->st);
     delete b;
 }
 
 void smem_gpu_shutdown(smem_gpu_t* g) {
     if (!g) return;
+    if (g->reserve.valid()) g->reserve.wait();
     (void)hipSetDevice(g->device);
     for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
     g->per_thread.clear();
@@ -454,8 +607,16 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     if (g->d_occ64) (void)hipFree(g->d_occ64);
     if (g->d_occ192) (void)hipFree(g->d_occ192);
     if (g->d_kt) (void)hipFree(g->d_kt);
+    if (g->init_st) (void)hipStreamSynchronize(g->init_st);
     if (g->d_sa) (void)hipFree(g->d_sa);
+    if (g->d_sa_raw) (void)hipFree(g->d_sa_raw);
     if (g->d_pac) (void)hipFree(g->d_pac);
+    for (auto& p : g->pairs) {
+        (void)hipStreamDestroy(p.first);
+        (void)hipStreamDestroy(p.second);
+    }
+    if (g->sa_ready) (void)hipEventDestroy(g->sa_ready);
+    if (g->init_st) (void)hipStreamDestroy(g->init_st);
     delete g;
 }
 
@@ -464,6 +625,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     if (!g || !out || max_reads <= 0 || max_len <= 0 || max_len > (1 << 24)) return fail(SMEM_E_ARG, "smem_batch_create");
     if (max_bases >= (1ull << 32) - 64) return fail(SMEM_E_ARG, "smem_batch_create: >= 2^32 bases per batch");
     *out = nullptr;
+    if (int r = gpu_check(g)) return r;
     HIP_TRY(hipSetDevice(g->device));
     smem_batch_t* b = new (std::nothrow) smem_batch_t();
     if (!b) return fail(SMEM_E_NOMEM, "smem_batch_create");
@@ -479,7 +641,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     const int read_lanes = (max_reads + 255) / 256 * 256;
     b->lanes = std::max(256, std::min(want_lanes, read_lanes));
     int rc = SMEM_OK;
-    hipError_t e = hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking);
+    hipError_t e = hipSuccess;
     for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&b->ev[k]);
     const size_t R = (size_t)max_reads;
     if (e == hipSuccess) e = b->h_codes.ensure(b->max_bases);
@@ -500,7 +662,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     if (e == hipSuccess) e = b->d_intv_off.ensure(R + 1);
     if (e == hipSuccess) e = b->d_call_off.ensure(R + 1);
     if (e == hipSuccess) e = b->h_ctr.ensure(8);
-    if (e == hipSuccess) e = b->h_tot.ensure(8);
+    if (e == hipSuccess) e = b->h_tot.ensure(16);  // [8, 16): run_aln's scalars
     if (e == hipSuccess) e = b->h_intv_off.ensure(R + 1);
     if (e == hipSuccess) e = b->h_call_off.ensure(R + 1);
     if (e == hipSuccess) {
@@ -518,13 +680,16 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     return SMEM_OK;
 }
 
+// the staged reads host -> device, under the caller's BatchCall
 static int upload_reads(smem_batch_t* b, int n_reads) {
-    HIP_TRY(hipSetDevice(b->g->device));
+    b->ran = b->fetched = false;
+    b->n_reads = 0;
     const uint64_t nb = b->h_offs.p[n_reads];
     HIP_TRY(hipMemcpyAsync(b->d_codes.p, b->h_codes.p, std::max<uint64_t>(nb, 1), hipMemcpyHostToDevice, b->st));
     HIP_TRY(hipMemcpyAsync(b->d_offs.p, b->h_offs.p, sizeof(uint64_t) * (n_reads + 1), hipMemcpyHostToDevice, b->st));
+    INJECT(ST_UPLOAD);
+    HIP_TRY(hipStreamSynchronize(b->st));
     b->n_reads = n_reads;
-    b->ran = b->fetched = false;
     return SMEM_OK;
 }
 
@@ -532,7 +697,7 @@ int smem_batch_set_reads(smem_batch_t* b, int n_reads, const uint8_t* const* seq
     g_err[0] = 0;
     if (!b || n_reads < 0 || (n_reads > 0 && (!seq || !len))) return fail(SMEM_E_ARG, "smem_batch_set_reads");
     if (n_reads > b->max_reads) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads: too many reads");
-    HIP_TRY(hipStreamSynchronize(b->st));  // staging buffer may still feed a copy
+    // (no copy from the staging buffers is in flight: every call drains its work)
     uint64_t o = 0;
     for (int i = 0; i < n_reads; ++i) {
         if (len[i] < 0 || len[i] > b->max_len) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads: read too long");
@@ -542,6 +707,8 @@ int smem_batch_set_reads(smem_batch_t* b, int n_reads, const uint8_t* const* seq
         o += (uint64_t)len[i];
     }
     b->h_offs.p[n_reads] = o;
+    BatchCall c(b);
+    if (c.rc) return c.rc;
     return upload_reads(b, n_reads);
 }
 
@@ -549,7 +716,6 @@ int smem_batch_set_reads_packed(smem_batch_t* b, int n_reads, const uint8_t* cod
     g_err[0] = 0;
     if (!b || n_reads < 0 || !offsets || (n_reads > 0 && !codes)) return fail(SMEM_E_ARG, "smem_batch_set_reads_packed");
     if (n_reads > b->max_reads) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads_packed: too many reads");
-    HIP_TRY(hipStreamSynchronize(b->st));
     const uint64_t o0 = offsets[0], nb = offsets[n_reads] - o0;
     if (nb > b->max_bases) return fail(SMEM_E_CAPACITY, "smem_batch_set_reads_packed: too many bases");
     for (int i = 0; i < n_reads; ++i) {
@@ -560,6 +726,8 @@ int smem_batch_set_reads_packed(smem_batch_t* b, int n_reads, const uint8_t* cod
     }
     b->h_offs.p[n_reads] = nb;
     if (nb) std::memcpy(b->h_codes.p, codes + o0, nb);
+    BatchCall c(b);
+    if (c.rc) return c.rc;
     return upload_reads(b, n_reads);
 }
 
@@ -587,11 +755,8 @@ static void fill_params(smem_batch_t* b, const smem_opt_t* o, smem::SeedParams& 
     P.dbg = dbg ? atoi(dbg) : 0;
 }
 
-int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
-    g_err[0] = 0;
-    if (!b || !opt) return fail(SMEM_E_ARG, "smem_batch_run");
+static int batch_run_impl(smem_batch_t* b, const smem_opt_t* opt) {
     smem_gpu_t* g = b->g;
-    HIP_TRY(hipSetDevice(g->device));
     const int n = b->n_reads;
     b->fetched = false;
     b->sa_ran = false;
@@ -712,6 +877,7 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     F.flat_calls = b->d_flat_calls.p;
     HIP_TRY(smem_launch_finalize(&F, 1, b->st));
     HIP_TRY(hipEventRecord(b->ev[3], b->st));
+    INJECT(ST_SEED);
     HIP_TRY(hipStreamSynchronize(b->st));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
@@ -730,9 +896,20 @@ int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
     return SMEM_OK;
 }
 
+int smem_batch_run(smem_batch_t* b, const smem_opt_t* opt) {
+    g_err[0] = 0;
+    if (!b || !opt) return fail(SMEM_E_ARG, "smem_batch_run");
+    BatchCall c(b);
+    if (c.rc) return c.rc;
+    return batch_run_impl(b, opt);
+}
+
 // copy the outputs `mask` names (SMEM_FETCH_*) device -> pinned host memory
 static int fetch_impl(smem_batch_t* b, int mask) {
-    HIP_TRY(hipSetDevice(b->g->device));
+    BatchCall call(b);
+    if (call.rc) return call.rc;
+    // views of an earlier fetch end here (its buffers may be regrown below)
+    b->fetched = b->sa_fetched = b->chain_fetched = b->aln_fetched = false;
     const int n = b->n_reads;
     const bool f_intv = mask & SMEM_FETCH_INTV, f_sa = (mask & SMEM_FETCH_SA) && b->sa_ran;
     const bool f_chain = (mask & SMEM_FETCH_CHAINS) && b->chain_ran, f_aln = (mask & SMEM_FETCH_REGS) && b->aln_ran;
@@ -793,6 +970,7 @@ static int fetch_impl(smem_batch_t* b, int mask) {
             HIP_TRY(hipMemcpyAsync(b->h_aln_regs.p, b->d_aln_out.p, sizeof(smem::AlnReg) * b->tot_regs,
                                    hipMemcpyDeviceToHost, b->st));
     }
+    INJECT(ST_FETCH);
     HIP_TRY(hipStreamSynchronize(b->st));
     b->fetched = f_intv;
     b->sa_fetched = f_sa;
@@ -825,10 +1003,14 @@ int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
     if (sa->seq_len != g->L2[4] || sa->n_sa != (sa->seq_len + sa->sa_intv) / sa->sa_intv)
         return fail(SMEM_E_ARG, "smem_gpu_load_sa: SA does not belong to this index (seq_len)");
     if (sa->primary != g->primary) return fail(SMEM_E_ARG, "smem_gpu_load_sa: SA does not belong to this index (primary)");
+    if (int r = gpu_check(g)) return r;
     HIP_TRY(hipSetDevice(g->device));
-    if (g->d_sa) {
-        (void)hipFree(g->d_sa);
-        g->d_sa = nullptr;
+    if (g->d_sa || g->d_sa_raw) {
+        // a reload: no batch may still read the old copy
+        HIP_TRY(hipDeviceSynchronize());
+        if (g->d_sa) (void)hipFree(g->d_sa);
+        if (g->d_sa_raw) (void)hipFree(g->d_sa_raw);
+        g->d_sa = g->d_sa_raw = nullptr;
     }
     // n_sa + 1 words: the zero pad of smem_sa_t (a 16-B load of the last sample stays in bounds)
     hipError_t e = hipMalloc(&g->d_sa, (sa->n_sa + 1) * sizeof(uint64_t));
@@ -854,14 +1036,23 @@ int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
         std::memcpy(S.L2, g->L2, sizeof(S.L2));
         S.sa = g->d_sa;
         S.sa_shift = g->sa_shift;
-        e = smem_launch_sa_densify(&S, dshift, n_dense, dense, nullptr);
-        if (e == hipSuccess) e = hipMemset(dense + n_dense, 0, sizeof(uint64_t));
-        if (e == hipSuccess) e = hipDeviceSynchronize();
+        // in the background, on the device's init stream: the caller goes on
+        // (bwa mem reads its first chunk of reads, the first batches seed)
+        // while the densification runs (~0.7 s at human size); smem_batch_sa
+        // waits for sa_ready on the device, and the uploaded samples are
+        // freed once it has passed
+        if (!g->init_st) e = hipStreamCreateWithFlags(&g->init_st, hipStreamNonBlocking);
+        if (e == hipSuccess && !g->sa_ready) e = hipEventCreateWithFlags(&g->sa_ready, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipMemsetAsync(dense + n_dense, 0, sizeof(uint64_t), g->init_st);
+        if (e == hipSuccess) e = smem_launch_sa_densify(&S, dshift, n_dense, dense, g->init_st);
+        if (e == hipSuccess) e = hipEventRecord(g->sa_ready, g->init_st);
+        if (e == hipSuccess && getenv("SMEM_GPU_SYNC_INIT")) e = hipStreamSynchronize(g->init_st);
         if (e != hipSuccess) {
+            (void)hipDeviceSynchronize();
             (void)hipFree(dense);
             return fail(SMEM_E_DEVICE, "smem_gpu_load_sa: densify", e);
         }
-        (void)hipFree(g->d_sa);
+        g->d_sa_raw = g->d_sa;
         g->d_sa = dense;
         g->n_sa = n_dense;
         g->sa_shift = dshift;
@@ -875,7 +1066,13 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     smem_gpu_t* g = b->g;
     if (!g->d_sa) return fail(SMEM_E_ARG, "smem_batch_sa: no SA loaded (smem_gpu_load_sa)");
     if (max_occ < 0) return fail(SMEM_E_ARG, "smem_batch_sa: max_occ");
-    HIP_TRY(hipSetDevice(g->device));
+    BatchCall call(b);
+    if (call.rc) return call.rc;
+    b->sa_ran = b->chain_ran = b->aln_ran = false;
+    b->sa_fetched = b->chain_fetched = b->aln_fetched = false;
+    // the densified SA may still be in the making (smem_gpu_load_sa runs it
+    // in the background): the walk waits for it on the device
+    if (g->sa_ready) HIP_TRY(hipStreamWaitEvent(b->st, g->sa_ready, 0));
     const uint64_t ni = b->tot_intv;
     if (ni >= (1ull << 31)) return fail(SMEM_E_CAPACITY, "smem_batch_sa: too many intervals");
     HIP_TRY(b->d_occ_n.grow(ni));
@@ -911,6 +1108,7 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     const int grid = std::max(1, (int)std::min<uint64_t>((uint64_t)g->n_cu * 8, (b->tot_occ + 255) / 256));
     HIP_TRY(smem_launch_sa_walk(&S, grid, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    INJECT(ST_SA);
     HIP_TRY(hipStreamSynchronize(b->st));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
@@ -938,7 +1136,10 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     if (!b || !b->sa_ran) return fail(SMEM_E_ARG, "smem_batch_chain: run smem_batch_sa first");
     if (!opt || l_pac < 0 || opt->w < 0) return fail(SMEM_E_ARG, "smem_batch_chain: bad options");
     if (b->tot_occ >= (1ull << 32) - 1) return fail(SMEM_E_CAPACITY, "smem_batch_chain: too many seed occurrences");
-    HIP_TRY(hipSetDevice(b->g->device));
+    BatchCall call(b);
+    if (call.rc) return call.rc;
+    b->chain_ran = b->aln_ran = false;
+    b->chain_fetched = b->aln_fetched = false;
     const int n = b->n_reads;
     const uint64_t no = std::max<uint64_t>(b->tot_occ, 1);
     HIP_TRY(b->d_seed.grow(no));
@@ -1006,11 +1207,6 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.lds_rest = CHAIN_REST_LDS;
     if (const char* v = getenv("SMEM_CHAIN_LDS_REST")) P.lds_rest = (uint32_t)std::max(1024, atoi(v));
     const bool two = !(getenv("SMEM_CHAIN_STREAMS") && atoi(getenv("SMEM_CHAIN_STREAMS")) == 1);
-    if (two && !b->st2) {
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&b->st2, hipStreamNonBlocking, least));
-    }
     if (two && !b->ev_fork) HIP_TRY(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     if (two && !b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
@@ -1030,6 +1226,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.out_seed = b->d_out_seed.p;
     HIP_TRY(smem_launch_chain_write(&P, b->g->n_cu, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    INJECT(ST_CHAIN);
     HIP_TRY(hipStreamSynchronize(b->st));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
@@ -1130,23 +1327,22 @@ int smem_ksw_extend(smem_gpu_t* g, int n, const smem_ksw_task_t* tasks, const ui
     }
     if (kernel_ms) *kernel_ms = 0.0;
     if (n == 0) return SMEM_OK;
-    HIP_TRY(hipSetDevice(g->device));
     DevBuf<smem::KswTask> dt;
     DevBuf<smem::KswResult> dr;
-    DevBuf<uint8_t> dq, dtg;
-    hipStream_t st = nullptr;
+    DevBuf<uint8_t> dq, dtg, dsc;
     hipEvent_t ev[2] = {nullptr, nullptr};
     struct Guard {
         DevBuf<smem::KswTask>& a; DevBuf<smem::KswResult>& b; DevBuf<uint8_t>& c; DevBuf<uint8_t>& d;
-        hipStream_t& s; hipEvent_t* e;
+        DevBuf<uint8_t>& f; hipEvent_t* e;
         ~Guard() {
-            a.release(); b.release(); c.release(); d.release();
+            a.release(); b.release(); c.release(); d.release(); f.release();
             if (e[0]) (void)hipEventDestroy(e[0]);
             if (e[1]) (void)hipEventDestroy(e[1]);
-            if (s) (void)hipStreamDestroy(s);
         }
-    } guard{dt, dr, dq, dtg, st, ev};
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    } guard{dt, dr, dq, dtg, dsc, ev};
+    DeviceCall call(g);  // (declared after the buffers: drained before they are freed)
+    if (call.rc) return call.rc;
+    const hipStream_t st = call.st;
     HIP_TRY(hipEventCreate(&ev[0]));
     HIP_TRY(hipEventCreate(&ev[1]));
     HIP_TRY(dt.ensure(n));
@@ -1171,11 +1367,6 @@ int smem_ksw_extend(smem_gpu_t* g, int n, const smem_ksw_task_t* tasks, const ui
     // SMEM_KSW_LANE=1: one problem per lane (kswl::lane_engine), tiers by query length
     const char* lane_e = getenv("SMEM_KSW_LANE");
     const bool lane = lane_e && atoi(lane_e);
-    DevBuf<uint8_t> dsc;
-    struct FreeSc {
-        DevBuf<uint8_t>& b;
-        ~FreeSc() { b.release(); }
-    } free_sc{dsc};
     if (lane) HIP_TRY(dsc.ensure(smem_ksw_lane_scratch(n)));
     HIP_TRY(hipEventRecord(ev[0], st));
     if (lane) HIP_TRY(smem_launch_ksw_lane(&K, dsc.p, g->n_cu, st));
@@ -1211,23 +1402,22 @@ int smem_ksw_align2(smem_gpu_t* g, int n, const smem_ksw_atask_t* tasks, const u
         if (q[k] > 4) return fail(SMEM_E_ARG, "smem_ksw_align2: query code > 4");
     if (kernel_ms) *kernel_ms = 0.0;
     if (n == 0) return SMEM_OK;
-    HIP_TRY(hipSetDevice(g->device));
     DevBuf<smem::KswATask> dt;
     DevBuf<smem::KswAResult> dr;
     DevBuf<uint8_t> dq, dtg;
-    hipStream_t st = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     struct Guard {
         DevBuf<smem::KswATask>& a; DevBuf<smem::KswAResult>& b; DevBuf<uint8_t>& c; DevBuf<uint8_t>& d;
-        hipStream_t& s; hipEvent_t* e;
+        hipEvent_t* e;
         ~Guard() {
             a.release(); b.release(); c.release(); d.release();
             if (e[0]) (void)hipEventDestroy(e[0]);
             if (e[1]) (void)hipEventDestroy(e[1]);
-            if (s) (void)hipStreamDestroy(s);
         }
-    } guard{dt, dr, dq, dtg, st, ev};
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    } guard{dt, dr, dq, dtg, ev};
+    DeviceCall call(g);  // (declared after the buffers: drained before they are freed)
+    if (call.rc) return call.rc;
+    const hipStream_t st = call.st;
     HIP_TRY(hipEventCreate(&ev[0]));
     HIP_TRY(hipEventCreate(&ev[1]));
     HIP_TRY(dt.ensure(n));
@@ -1300,9 +1490,10 @@ int smem_gpu_load_pac(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
     // under the device lock and after every queued kernel: no batch may be
     // reading the old copy, and a failed upload leaves no half-written one
     std::lock_guard<std::mutex> lk(g->mu);
+    if (int r = gpu_check(g)) return r;
     HIP_TRY(hipSetDevice(g->device));
-    HIP_TRY(hipDeviceSynchronize());
     if (g->d_pac) {
+        HIP_TRY(hipDeviceSynchronize());
         (void)hipFree(g->d_pac);
         g->d_pac = nullptr;
     }
@@ -1374,7 +1565,7 @@ static bool aln_lane_on() {
 // after a run_aln with the guarded walk: fail if any walk tripped its guard.
 // SMEM_ALN_STATS: print the heavy path's counters (regions the chain tasks
 // computed ahead, the walk's regions taken from them / computed serially)
-static int aln_guard_check(const smem::AlnParams& P, hipStream_t st) {
+static int aln_guard_check(const smem::AlnParams& P, hipStream_t st, uint64_t* hs) {
     if (getenv("SMEM_ALN_STATS")) {
         uint32_t c[smem::ALN_CTRS], nt = 0;
         HIP_TRY(hipMemcpyAsync(c, P.ctr, sizeof(c), hipMemcpyDeviceToHost, st));
@@ -1388,18 +1579,21 @@ static int aln_guard_check(const smem::AlnParams& P, hipStream_t st) {
                 nht, c[14]);
     }
     if (!P.walk_guard) return SMEM_OK;
-    uint32_t trips = 0;
-    HIP_TRY(hipMemcpyAsync(&trips, P.ctr + 15, sizeof(trips), hipMemcpyDeviceToHost, st));
+    hs[2] = 0;
+    HIP_TRY(hipMemcpyAsync(&hs[2], P.ctr + 15, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (trips) {
+    if (const uint32_t trips = (uint32_t)hs[2]) {
         snprintf(g_err, sizeof(g_err), "chains -> regions: the inlined heavy-read walk tripped its guard %u times", trips);
         return SMEM_E_INTERNAL;
     }
     return SMEM_OK;
 }
 
+// hs: >= 4 words of pinned host memory for the scalars copied back (never
+// pageable or stack memory: a copy must not outlive the call's frame)
 static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_t n_seeds, bool long_reads,
-                   AlnHeavyBufs& H, hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t ev_join = nullptr) {
+                   AlnHeavyBufs& H, uint64_t* hs, hipStream_t st, hipStream_t st2 = nullptr,
+                   hipEvent_t ev_join = nullptr) {
     const int n = P.n_reads;
     P.heavy_min = aln_heavy_min();
     P.heavy_seeds = aln_heavy_seeds();
@@ -1446,8 +1640,10 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.hscnt.grow(n));
         P.heavy = H.heavy.p, P.hcnt = H.hcnt.p, P.hscnt = H.hscnt.p;
         HIP_TRY(smem_launch_aln_classify(&P, st));
-        HIP_TRY(hipMemcpyAsync(&n_heavy, P.ctr + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        hs[0] = 0;
+        HIP_TRY(hipMemcpyAsync(&hs[0], P.ctr + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        n_heavy = (uint32_t)hs[0];
     }
     smem::CandParams C{};
     if (n_heavy && P.lane_on) {  // the walk's scratch (its chains were prepared by the lane path)
@@ -1465,9 +1661,9 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
             HIP_TRY(H.tmp.grow(tb + 256));
             tb = H.tmp.n;
             HIP_TRY(smem_launch_offsets(H.ccnt.p, H.coff.p, (int)n_heavy, H.tmp.p, &tb, st));
-            uint64_t m = 0;
-            HIP_TRY(hipMemcpyAsync(&m, H.coff.p + n_heavy, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(&hs[1], H.coff.p + n_heavy, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
+            const uint64_t m = hs[1];
             const uint64_t mm = std::max<uint64_t>(m, 1);
             HIP_TRY(H.ckey.grow(mm));
             HIP_TRY(H.ckey2.grow(mm));
@@ -1572,7 +1768,9 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     smem_gpu_t* g = b->g;
     if (!g->d_pac) return fail(SMEM_E_ARG, "smem_batch_chain2aln: no .pac loaded (smem_gpu_load_pac)");
     if (b->max_len > 1024) return fail(SMEM_E_ARG, "smem_batch_chain2aln: reads longer than 1024 bp");
-    HIP_TRY(hipSetDevice(g->device));
+    BatchCall call(b);
+    if (call.rc) return call.rc;
+    b->aln_ran = b->aln_fetched = false;
     const int n = b->n_reads;
     const uint64_t ns = std::max<uint64_t>(b->tot_seeds, 1);
     HIP_TRY(b->d_aln_srt.grow(ns + 1));
@@ -1616,16 +1814,12 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     }
     HIP_TRY(hipMemsetAsync(b->d_aln_ctr.p, 0, smem::ALN_CTRS * sizeof(uint32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
-    if (aln_two_streams() && !b->st2) {
-        int least = 0, greatest = 0;  // the light reads' stream at the lowest priority
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&b->st2, hipStreamNonBlocking, least));
-        HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
-    }
-    if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->st,
+    // the light reads' kernels on the pair's low-priority stream
+    if (aln_two_streams() && !b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->h_tot.p + 8, b->st,
                          aln_two_streams() ? b->st2 : nullptr, b->ev_join))
         return rc;
-    if (int rc = aln_guard_check(P, b->st)) return rc;
+    if (int rc = aln_guard_check(P, b->st, b->h_tot.p + 8)) return rc;
     tmp = b->d_sa_tmp.n;
     HIP_TRY(smem_launch_offsets(b->d_aln_nregs.p, b->d_aln_regoff.p, n, b->d_sa_tmp.p, &tmp, b->st));
     HIP_TRY(hipMemcpyAsync(b->h_tot.p + 5, b->d_aln_regoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, b->st));
@@ -1636,6 +1830,7 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     P.reg_off = b->d_aln_regoff.p, P.out = b->d_aln_out.p;
     HIP_TRY(smem_launch_aln_write(&P, b->st));
     HIP_TRY(hipEventRecord(b->ev[1], b->st));
+    INJECT(ST_ALN);
     HIP_TRY(hipStreamSynchronize(b->st));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
@@ -1725,7 +1920,6 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
         for (size_t k = 1; k < rng.size(); ++k)
             if (rng[k].first < rng[k - 1].second) return fail(SMEM_E_ARG, "smem_chain2aln: chains share seeds");
     }
-    HIP_TRY(hipSetDevice(g->device));
     DevBuf<uint8_t> dcodes, dpac;
     DevBuf<uint64_t> doffs, dchoff, dseedoff, dsrt, dnregs, dregoff;
     DevBuf<smem::OutChain> dch;
@@ -1733,7 +1927,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     DevBuf<smem::AlnReg> draw, dout;
     DevBuf<uint32_t> dctr;
     AlnHeavyBufs heavy;
-    hipStream_t st = nullptr;
+    HostBuf<uint64_t> hs, hnr;  // pinned: the scalars and region counts copied back
     hipEvent_t ev[2] = {nullptr, nullptr};
     struct Guard {
         std::vector<std::function<void()>> f;
@@ -1746,11 +1940,15 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
         dnregs.release(); dregoff.release(); dch.release(); dseeds.release(); draw.release(); dout.release();
         dctr.release();
         heavy.release();
+        hs.release(); hnr.release();
         if (ev[0]) (void)hipEventDestroy(ev[0]);
         if (ev[1]) (void)hipEventDestroy(ev[1]);
-        if (st) (void)hipStreamDestroy(st);
     });
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    DeviceCall call(g);  // (declared after the buffers: drained before they are freed)
+    if (call.rc) return call.rc;
+    const hipStream_t st = call.st;
+    HIP_TRY(hs.ensure(8));
+    HIP_TRY(hnr.ensure((size_t)n_reads));
     HIP_TRY(hipEventCreate(&ev[0]));
     HIP_TRY(hipEventCreate(&ev[1]));
     const uint64_t pac_bytes = (uint64_t)(l_pac + 3) / 4;
@@ -1782,11 +1980,11 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     aln_opt_params(opt, P);
     P.srt = dsrt.p, P.raw = draw.p, P.n_regs = dnregs.p, P.ctr = dctr.p;
     HIP_TRY(hipEventRecord(ev[0], st));
-    if (int rc = run_aln(g, P, n_chains, n_seeds, long_reads, heavy, st)) return rc;
-    if (int rc = aln_guard_check(P, st)) return rc;
+    if (int rc = run_aln(g, P, n_chains, n_seeds, long_reads, heavy, hs.p, st)) return rc;
+    if (int rc = aln_guard_check(P, st, hs.p)) return rc;
     HIP_TRY(hipEventRecord(ev[1], st));
-    std::vector<uint64_t> nr(n_reads);
-    HIP_TRY(hipMemcpyAsync(nr.data(), dnregs.p, 8 * n_reads, hipMemcpyDeviceToHost, st));
+    const uint64_t* nr = hnr.p;
+    HIP_TRY(hipMemcpyAsync(hnr.p, dnregs.p, 8 * n_reads, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     for (int r = 0; r < n_reads; ++r) {
         if (nr[r] > cap[r + 1] - cap[r]) return fail(SMEM_E_INTERNAL, "smem_chain2aln: region count past capacity");
@@ -1975,6 +2173,12 @@ int smem_gpu_seed_stream(smem_gpu_t* g, int64_t n_reads, const uint8_t* codes, c
 // worker slot's, (re)created when too small for this batch of reads
 static int collect_batch(smem_gpu_t* g, int slot, int n_reads, int max_len, uint64_t bases, smem_batch_t** out) {
     smem_batch_t* b = nullptr;
+    std::shared_future<int> res;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        res = g->reserve;
+    }
+    if (res.valid()) res.wait();  // smem_gpu_reserve_slots still sizing the slots
     {
         std::lock_guard<std::mutex> lk(g->mu);
         if (slot >= 0) {
@@ -1999,6 +2203,141 @@ static int collect_batch(smem_gpu_t* g, int slot, int n_reads, int max_len, uint
         b = nb;
     }
     *out = b;
+    return SMEM_OK;
+}
+
+// the later stages' scratch of a slot batch, sized before its first use at
+// per-read estimates above what 150-250 bp reads need on both bench profiles
+// (28 intervals, 4.5-9 seed occurrences and ~3 chains per read): a worker's
+// first batches then do not reallocate (each reallocation frees, and hipFree
+// waits for the whole device).  A batch that needs more grows as before.
+static int batch_prealloc(smem_batch_t* b) {
+    const uint64_t R = (uint64_t)b->max_reads;
+    const uint64_t ni = R * 48, no = R * 24, nc = R * 8, ns = R * 16;
+    HIP_TRY(b->d_flat_intv.ensure(ni));
+    HIP_TRY(b->d_flat_calls.ensure(R * 8));
+    HIP_TRY(b->d_occ_n.grow(ni));
+    HIP_TRY(b->d_occ_off.grow(ni + 1));
+    HIP_TRY(b->d_sa_pos.grow(no));
+    HIP_TRY(b->d_kstart.grow(no + 2));
+    size_t tmp = 0;
+    HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)ni, nullptr, &tmp, nullptr));
+    HIP_TRY(b->d_sa_tmp.grow(tmp + 256));
+    HIP_TRY(b->d_seed.grow(no));
+    HIP_TRY(b->d_next.grow(no));
+    HIP_TRY(b->d_chn.grow(no));
+    HIP_TRY(b->d_ord.grow(no));
+    HIP_TRY(b->d_ord2.grow(no));
+    HIP_TRY(b->d_flt.grow(no));
+    HIP_TRY(b->d_node.grow(no / 7 + 3 * R + 8));
+    HIP_TRY(b->d_n_out.grow(R));
+    HIP_TRY(b->d_ns_out.grow(R));
+    HIP_TRY(b->d_chain_off.grow(R + 1));
+    HIP_TRY(b->d_seed_off.grow(R + 1));
+    HIP_TRY(b->d_heavy.grow(2 * R + 4));
+    HIP_TRY(b->d_out_chain.grow(nc));
+    HIP_TRY(b->d_out_seed.grow(ns));
+    HIP_TRY(b->d_aln_srt.grow(ns + 1));
+    HIP_TRY(b->d_aln_raw.grow(ns + 1));
+    HIP_TRY(b->d_aln_nregs.grow(R));
+    HIP_TRY(b->d_aln_regoff.grow(R + 1));
+    HIP_TRY(b->d_aln_ctr.grow(smem::ALN_CTRS));
+    AlnHeavyBufs& H = b->aln_heavy;
+    HIP_TRY(H.pre.grow(ns));
+    HIP_TRY(H.pre_ok.grow(ns));
+    HIP_TRY(H.span.grow(2 * nc));
+    HIP_TRY(H.sdec.grow(nc));
+    HIP_TRY(H.tasks.grow(nc));
+    HIP_TRY(H.torder.grow(nc));
+    HIP_TRY(H.tfail.grow(nc));
+    HIP_TRY(H.lq.grow(smem::LQ_WORDS));
+    HIP_TRY(H.htasks.grow(ns));
+    HIP_TRY(H.htorder.grow(ns));
+    HIP_TRY(H.htfail.grow(ns));
+    HIP_TRY(H.hlq.grow(smem::LQ_WORDS));
+    HIP_TRY(H.chain_read.grow(nc));
+    HIP_TRY(H.swlist.grow(nc));
+    HIP_TRY(H.short_ok.grow(nc));
+    HIP_TRY(H.pre_short.grow(nc));
+    HIP_TRY(H.heavy.grow(R));
+    HIP_TRY(H.hcnt.grow(R));
+    HIP_TRY(H.hscnt.grow(R));
+    HIP_TRY(b->h_aln_regoff.grow(R + 1));
+    HIP_TRY(b->h_aln_regs.grow(ns));
+    if (!b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    if (!b->ev_fork) HIP_TRY(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    return SMEM_OK;
+}
+
+// one pass of every stage over a few reads cut from the resident .pac on a
+// slot batch: each kernel's code object is loaded on its first launch, and
+// that load should not fall on a worker's first batch
+static int batch_warmup(smem_batch_t* b) {
+    smem_gpu_t* g = b->g;
+    if (!g->d_pac || g->l_pac < 4096) return SMEM_OK;
+    const int nr = std::min(64, b->max_reads), L = std::min(150, b->max_len);
+    std::vector<uint8_t> pk((size_t)(L + 8) / 4 + 2), codes((size_t)nr * L);
+    std::vector<const uint8_t*> seq((size_t)nr);
+    std::vector<int> len((size_t)nr, L);
+    for (int r = 0; r < nr; ++r) {
+        const uint64_t beg = (uint64_t)(g->l_pac - L - 8) / (uint64_t)nr * (uint64_t)r / 4 * 4;
+        HIP_TRY(hipMemcpy(pk.data(), g->d_pac + beg / 4, pk.size(), hipMemcpyDeviceToHost));
+        for (int i = 0; i < L; ++i) codes[(size_t)r * L + i] = pk[(size_t)i >> 2] >> ((~i & 3) << 1) & 3;
+        seq[(size_t)r] = codes.data() + (size_t)r * L;
+    }
+    smem_opt_t so;
+    smem_chain_opt_t co;
+    smem_aln_opt_t ao;
+    smem_opt_default(&so);
+    smem_chain_opt_default(&co);
+    smem_aln_opt_default(&ao);
+    int rc = smem_batch_set_reads(b, nr, seq.data(), len.data());
+    if (!rc) rc = smem_batch_run(b, &so);
+    if (!rc && g->d_sa) rc = smem_batch_sa(b, so.min_seed_len, 10000);
+    if (!rc && g->d_sa) rc = smem_batch_chain(b, g->l_pac, &co);
+    if (!rc && g->d_sa && b->max_len <= 1024) rc = smem_batch_chain2aln(b, &ao);
+    if (!rc && b->aln_ran) rc = smem_batch_fetch_mask(b, SMEM_FETCH_REGS);
+    return rc;
+}
+
+int smem_gpu_set_max_active(smem_gpu_t* g, int n) {
+    g_err[0] = 0;
+    if (!g || n < 0 || n > 256) return fail(SMEM_E_ARG, "smem_gpu_set_max_active: 0..256");
+    std::lock_guard<std::mutex> lk(g->adm_mu);
+    g->max_active = n > 0 ? n : 8;
+    g->adm_cv.notify_all();
+    return SMEM_OK;
+}
+
+int smem_gpu_reserve_slots(smem_gpu_t* g, int n_slots, int reads_per_slot, int max_len) {
+    g_err[0] = 0;
+    if (!g || n_slots <= 0 || n_slots > 4096 || reads_per_slot <= 0 || max_len <= 0 || max_len > (1 << 24) ||
+        (uint64_t)reads_per_slot * (uint64_t)max_len >= (1ull << 32) - 64)
+        return fail(SMEM_E_ARG, "smem_gpu_reserve_slots");
+    if (int r = gpu_check(g)) return r;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->reserve.valid() && g->reserve.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
+        return fail(SMEM_E_ARG, "smem_gpu_reserve_slots: a reservation is still running");
+    g->reserve = std::async(std::launch::async, [g, n_slots, reads_per_slot, max_len]() -> int {
+        g_no_inject = 1;
+        if (hipSetDevice(g->device) != hipSuccess) return SMEM_E_DEVICE;
+        int rc = SMEM_OK;
+        for (int k = 0; k < n_slots && rc == SMEM_OK; ++k) {
+            smem_batch_t* b = nullptr;
+            rc = smem_batch_create(g, reads_per_slot, (uint64_t)reads_per_slot * (uint64_t)max_len, max_len, &b);
+            if (rc == SMEM_OK) rc = batch_prealloc(b);
+            if (rc == SMEM_OK && k == 0) rc = batch_warmup(b);
+            if (rc != SMEM_OK) {
+                smem_batch_destroy(b);
+                break;
+            }
+            std::lock_guard<std::mutex> lk2(g->mu);
+            if (g->slots.size() <= (size_t)k) g->slots.resize((size_t)k + 1, nullptr);
+            if (g->slots[(size_t)k]) smem_batch_destroy(g->slots[(size_t)k]);
+            g->slots[(size_t)k] = b;
+        }
+        return rc;  // a slot left out is created on its first use, as without the reservation
+    }).share();
     return SMEM_OK;
 }
 

@@ -1324,7 +1324,8 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 
 // ------------------------------------------------------------ host launchers
 // The product build instantiates the default kernel (2; 0, 20 and 26 name it too),
-// its stamped diagnostic twin (9) and the k-mer table variant (23).  The other
+// its stamped diagnostic twin (9), the k-mer table variant (23), the claim-ahead
+// variant and its stamped twin (24, 25) and the priority A/B pair (27, 28).  The other
 // A/B variants measured in rounds 1-2 are compiled only with
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
@@ -1339,8 +1340,8 @@ extern "C" int smem_seed_variant_built(int variant) {
 
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
     switch (variant) {
-        // 9: the default with cycle stamps
-        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 9: the default (wave priority included) with cycle stamps
+        case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
         // 23: the default with the k-mer table (P->kt)
         case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
         // 24: the default with the next read claimed and loaded in the uniform section (PFCH); 25: its stamped twin

@@ -34,6 +34,7 @@ EXPORTED = [
     "smem_gpu_seed_stream", "smem_batch_results_packed",
     "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
     "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
+    "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id",
 ]
 
 # smem_batch_fetch_mask bits (include/smem_gpu.h)
@@ -61,6 +62,13 @@ def source_hash() -> str:
 def build_id() -> str:
     """The source hash the loaded libsmemgpu.so was built from."""
     return load().smem_gpu_build_id().decode()
+
+
+def kernel_id() -> str:
+    """Hash of the loaded library's seeding-kernel sources and compile flags only
+    (bwa-mem-harp2_amd/Makefile KERNEL_HASH): seed_kernel counters recorded on
+    another build of the runtime still describe it when this id matches."""
+    return load().smem_gpu_kernel_id().decode()
 
 
 class SmemError(RuntimeError):
@@ -202,6 +210,10 @@ def load() -> C.CDLL:
     lib.smem_strerror.restype = C.c_char_p
     lib.smem_gpu_build_id.argtypes = []
     lib.smem_gpu_build_id.restype = C.c_char_p
+    lib.smem_gpu_kernel_id.argtypes = []
+    lib.smem_gpu_kernel_id.restype = C.c_char_p
+    lib.smem_gpu_reserve_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+    lib.smem_gpu_set_max_active.argtypes = [C.c_void_p, C.c_int]
     _lib = lib
     return lib
 
@@ -437,6 +449,14 @@ class Gpu:
 
     def load_sa(self, sa: "SA") -> None:
         _check(load().smem_gpu_load_sa(self._h, C.byref(sa._raw)), "smem_gpu_load_sa")
+
+    def set_max_active(self, n: int) -> None:
+        """Admission: at most n calls on the device at once (smem_gpu_set_max_active; 0 = default)."""
+        _check(load().smem_gpu_set_max_active(self._h, n), "smem_gpu_set_max_active")
+
+    def reserve_slots(self, n_slots: int, reads_per_slot: int, max_len: int) -> None:
+        """Pre-size collect_ex worker slots in the background (smem_gpu_reserve_slots)."""
+        _check(load().smem_gpu_reserve_slots(self._h, n_slots, reads_per_slot, max_len), "smem_gpu_reserve_slots")
 
     def batch(self, max_reads: int, max_bases: int, max_len: int) -> "Batch":
         return Batch(self, max_reads, max_bases, max_len)

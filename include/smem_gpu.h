@@ -18,6 +18,18 @@
  * SMEM_E_* code; on a negative code the caller may fall back to its own CPU
  * path, mirroring the reference's reject -> CPU semantics
  * (software/bwt.c:686-717).  No entry point silently computes on the CPU.
+ *
+ * Failure contract: every entry point that runs work on a device returns
+ * only once all of that work has finished or been abandoned (its streams
+ * are synchronised on every return path), so no copy of the call lands in
+ * host memory after the caller has resumed, whatever the code.  A HIP
+ * runtime failure (SMEM_E_DEVICE) marks the device faulted: every later
+ * call on it returns SMEM_E_DEVICE at once without enqueuing anything, so a
+ * caller that takes its CPU path on SMEM_E_DEVICE computes exactly what the
+ * reference computes.  Allocation failures are SMEM_E_NOMEM and leave the
+ * device usable.  SMEM_GPU_FAIL=<stage>:<k>[:sticky] (stage: upload, seed,
+ * sa, chain, aln, fetch, any) injects SMEM_E_DEVICE into every k-th call of
+ * the stage after its work is enqueued, to test that contract.
  */
 #ifndef SMEM_GPU_H
 #define SMEM_GPU_H
@@ -77,7 +89,7 @@ typedef struct {
 } smem_opt_t;
 
 typedef struct smem_gpu smem_gpu_t;       /* one device + its resident index */
-typedef struct smem_batch smem_batch_t;   /* one worker's reads/results + HIP stream */
+typedef struct smem_batch smem_batch_t;   /* one worker's reads / results / scratch on one device */
 
 /* defaults of mem_opt_init() (software/bwamem.c:58-65) */
 void smem_opt_default(smem_opt_t *opt);
@@ -141,8 +153,9 @@ int  smem_gpu_parse_devices(const char *spec, int *devices, int max_devices);
 
 /* ------------------------------------------------------------ one shot */
 /* Thread-safe; may be called concurrently from kt_for_batch workers (each
- * calling thread gets its own stream and buffers, created on first use and
- * freed by smem_gpu_shutdown).  seq[i] are nt4 codes (0..3, >3 ambiguous),
+ * calling thread gets its own buffers, created on first use and freed by
+ * smem_gpu_shutdown; the streams come from the device's admission pool, see
+ * smem_gpu_set_max_active).  seq[i] are nt4 codes (0..3, >3 ambiguous),
  * len[i] their lengths; the results stay valid until the same thread calls
  * smem_gpu_collect again.  Read them with smem_batch_read(*batch_out, i, ...). */
 int  smem_gpu_collect(smem_gpu_t *gpu, int n_reads, const uint8_t *const *seq, const int *len,
@@ -159,6 +172,22 @@ int  smem_gpu_collect(smem_gpu_t *gpu, int n_reads, const uint8_t *const *seq, c
 #define SMEM_COLLECT_NO_FETCH 1
 int  smem_gpu_collect_ex(smem_gpu_t *gpu, int slot, int n_reads, const uint8_t *const *seq, const int *len,
                          const smem_opt_t *opt, int flags, smem_batch_t **batch_out);
+/* Pre-size worker slots [0, n_slots) of smem_gpu_collect_ex for batches of up
+ * to reads_per_slot reads of up to max_len bases, with the later stages'
+ * scratch and pinned result buffers sized at generous per-read estimates, and
+ * run one warm-up pass of every stage over a few reads cut from the resident
+ * .pac (a kernel's code object loads on its first launch).  Replaces the
+ * per-worker buffers main_mem allocates before the first chunk
+ * (software/fastmap.c:207-210).  Runs on a background host thread: the call
+ * returns at once, and the first smem_gpu_collect* on the device waits for it.
+ * A batch larger than reserved is re-created on first use, as without it. */
+int  smem_gpu_reserve_slots(smem_gpu_t *gpu, int n_slots, int reads_per_slot, int max_len);
+/* Admission, the HARP manager's role (software/fastmap.c:320-429): at most n
+ * calls run work on the device at once, each on one of n leased stream pairs
+ * (a device carries at most 2n streams however many workers share it); the
+ * others wait for a pair instead of being rejected.  Default 8, or
+ * SMEM_GPU_MAX_ACTIVE at smem_gpu_init; 0 restores the default. */
+int  smem_gpu_set_max_active(smem_gpu_t *gpu, int n);
 
 /* ------------------------------------------------------------ streaming */
 /* bwa mem's chunk loop (software/fastmap.c:213-228, mem_process_seqs ->
@@ -180,7 +209,7 @@ int  smem_gpu_collect_ex(smem_gpu_t *gpu, int slot, int n_reads, const uint8_t *
  * in the callback; SMEM_STREAM_RELEASE -- free the workers' batches when the
  * call returns.  Otherwise the handle keeps at most n_workers of them for
  * the next call (each holds ~1 GB of pinned host memory per 1M-read chunk;
- * a later call with fewer workers shrinks the pool, smem_gpu_destroy frees
+ * a later call with fewer workers shrinks the pool, smem_gpu_shutdown frees
  * it).  fn may be NULL; a non-zero return from fn stops the stream and is
  * returned. */
 typedef int (*smem_chunk_fn)(void *ctx, int64_t chunk, int64_t first_read, int n_reads, const smem_batch_t *b);
@@ -251,7 +280,11 @@ int  smem_batch_results_packed(const smem_batch_t *b, const smem_pintv_t **pintv
  * if it does not belong to the index.  Reads sa->sa[0 .. n_sa-1] only (the
  * reference's bwt->sa array as is).  The device copy is densified to every
  * 4th row by LF walks from these samples (8 B per 4 symbols of HBM); lookups
- * return exactly what bwt_sa does with the .sa's own interval. */
+ * return exactly what bwt_sa does with the .sa's own interval.  The
+ * densification runs in the background (~0.7 s at human size): the call
+ * returns after the upload, and smem_batch_sa waits for it on the device
+ * (SMEM_GPU_SYNC_INIT=1: wait here).  The uploaded samples stay resident
+ * beside the dense copy until smem_gpu_shutdown. */
 int  smem_gpu_load_sa(smem_gpu_t *gpu, const smem_sa_t *sa);
 /* After smem_batch_run: bwt_sa (software/bwt.c:104-114) of every seed
  * occurrence mem_insert_seed() generates from the lists — each interval with
@@ -383,7 +416,9 @@ int  smem_chain2aln(smem_gpu_t *gpu, int n_reads, const uint8_t *codes, const ui
 
 /* Keep the 2-bit forward-strand .pac of the uploaded index resident in HBM
  * (bwa_idx_load's idx->pac, software/bwa.c:325-330); 2 * l_pac must equal the
- * index's seq_len. */
+ * index's seq_len.  Replacing a loaded .pac must not overlap a chains ->
+ * regions call (smem_batch_chain2aln, smem_chain2aln) on the same handle:
+ * such a call may still read the old copy. */
 int  smem_gpu_load_pac(smem_gpu_t *gpu, const uint8_t *pac, int64_t l_pac);
 /* Device-resident twin of smem_chain2aln: after smem_batch_chain (filter = 1,
  * as mem_align1_core_batched filters before extending, software/bwamem.c:1414-1422),
@@ -420,7 +455,7 @@ int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement (the
- * product build has 0 = 2 = 20, 9 and 23; the others need a library built with
+ * product build has 0 = 2 = 20 = 26, 9, 23, 24, 25, 27 and 28; the others need a library built with
  * `make AB=1`, else SMEM_E_ARG):
  * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
  * device at init), per-lane fetch into two register slots with bucket reuse,
@@ -433,7 +468,8 @@ int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
  * 20 = 2; 21 register slots, 7 entries, 4 blocks per CU; 3 reference-layout buckets,
  * cooperative fetch, lists in global memory; 4 reference layout, per-lane
  * fetch; 5 as 2 with 12 list entries in LDS (2 blocks per CU); 6 as 2 with
- * lists in global memory; 9 the default with per-wave cycle stamps
+ * lists in global memory; 9 the default with per-wave cycle stamps; 24 the next read claimed in the
+ * uniform section (25 stamped); 27 wave priority in the extend arithmetic instead; 28 no wave priority
  * (smem_batch_debug); 10 the default on the Occ192 layout (64-B lines of
  * 192 symbols, built on first use: exact, 7 % slower at human size); 22
  * register slots on Occ192; 23 the default reading the bi-interval of every
@@ -454,6 +490,10 @@ const char *smem_strerror(int code);
  * (bwa-mem-harp2_amd/Makefile SRC_HASH): lets a caller prove that the .so it
  * loaded is the build of the sources beside it */
 const char *smem_gpu_build_id(void);
+/* hash of the seeding kernel's own sources and compile flags only
+ * (csrc/smem_kernels.hip / .h): a counter profile of seed_kernel recorded on
+ * another build of the runtime still describes this one when it matches */
+const char *smem_gpu_kernel_id(void);
 
 #ifdef __cplusplus
 }

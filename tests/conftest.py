@@ -5,7 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "bwa-mem-harp2_amd")
-for p in (PKG, ROOT):
+for p in (PKG, ROOT, os.path.join(ROOT, "tests")):  # tests/: shared helpers between test modules
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -36,10 +36,12 @@ def main():
             os.replace(base + ".tmp" + e, base + e)
     m = min(own.reads, reads.n)
     sub = reads.subset(range(m))
+    bodies = {}
     with tempfile.TemporaryDirectory(dir=a.cache) as d:
         fq = os.path.join(d, "r.fq")
         synth.write_fastq(fq, sub)
         batch = max(1024, -(-m // own.threads))
+        print(f"[probe] {m} reads, -t {own.threads} -b {batch}", flush=True)
         for name, cmd in (("gpu", [bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(batch), base, fq]),
                           ("ref", [bench.REF_HARNESS, "mem", base, fq, str(own.threads), "1", "0"])):
             t = time.time()
@@ -52,9 +54,44 @@ def main():
                   f"{nl} lines", flush=True)
             for l in keep[:60]:
                 print("   ", l, flush=True)
+            bodies[name] = body
             if own.out:
+                os.makedirs(own.out, exist_ok=True)
                 with open(os.path.join(own.out, name + ".sam"), "wb") as fh:
                     fh.write(body)
+                with open(os.path.join(own.out, name + ".err"), "w") as fh:
+                    fh.write(err)
+    diff_summary(bodies.get("gpu", b""), bodies.get("ref", b""), batch)
+
+
+def diff_summary(gpu, ref, batch):
+    """Which SAM records differ, and which worker batch (read index // -b) each belongs to."""
+    if gpu == ref:
+        print("== SAM identical", flush=True)
+        return
+    def records(body):
+        rec = {}
+        for l in body.split(b"\n"):
+            if not l or l.startswith(b"@"):
+                continue
+            rec.setdefault(l.split(b"\t", 1)[0], []).append(l)
+        return rec
+    g, r = records(gpu), records(ref)
+    names = list(dict.fromkeys(list(r) + list(g)))
+    order = {n: i for i, n in enumerate(r)}
+    bad = [n for n in names if g.get(n) != r.get(n)]
+    print(f"== SAM differs: {len(bad)} of {len(names)} reads "
+          f"(gpu {sum(map(len, g.values()))} records, ref {sum(map(len, r.values()))})", flush=True)
+    by_batch = {}
+    for n in bad:
+        by_batch.setdefault(order.get(n, -1) // batch if n in order else -1, []).append(n)
+    print("   differing reads by batch:", {k: len(v) for k, v in sorted(by_batch.items())}, flush=True)
+    for n in bad[:6]:
+        print(f"   read {n.decode(errors='replace')} (index {order.get(n)}):", flush=True)
+        for l in r.get(n, []):
+            print("     ref", l[:220].decode(errors="replace"), flush=True)
+        for l in g.get(n, []):
+            print("     gpu", l[:220].decode(errors="replace"), flush=True)
 
 
 if __name__ == "__main__":

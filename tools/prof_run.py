@@ -20,6 +20,7 @@ def main():
     import argparse
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument("--launches", type=int, default=1)
+    p.add_argument("--stats-out", default=None, help="write the launch shape and library ids here (JSON)")
     own, rest = p.parse_known_args()
     import bench
     import smemgpu
@@ -34,6 +35,12 @@ def main():
         t = time.time()
         b.run(opt)
         print(f"launch: kernel {b.stats()['kernel_ms']:.3f} ms, wall {1e3 * (time.time() - t):.1f} ms", flush=True)
+    if own.stats_out:
+        import json
+        st = b.stats()
+        with open(own.stats_out, "w") as fh:
+            json.dump({"grid": st["grid"], "block": st["block"], "build_id": smemgpu.build_id(),
+                       "kernel_id": smemgpu.kernel_id()}, fh)
     b.close()
     gpu.close()
 

@@ -4,7 +4,8 @@ Runs rocprofv3 counter passes (one run per pass, nothing else combined with
 --pmc: MI355X_MICROARCH.md §counters) over tools/prof_run.py on the bench
 workload and writes profiles/traffic.json, which bench.py reports in
 roofline.traffic / request_roofline when its workload AND its library build
-(smem_gpu_build_id) match:
+(smem_gpu_build_id) match -- or its seeding kernel (smem_gpu_kernel_id: the
+kernel's own sources and flags) and launch shape match, for runtime-only changes:
 
   pass 1: TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum  -- L2 fabric read requests
   pass 2: WRITE_SIZE
@@ -29,11 +30,11 @@ sys.path.insert(0, os.path.join(ROOT, "bwa-mem-harp2_amd"))
 sys.path.insert(0, ROOT)
 
 
-def run_pass(counters: list, out_dir: str, rest: list) -> dict:
+def run_pass(counters: list, out_dir: str, rest: list, extra: list = ()) -> dict:
     d = os.path.join(out_dir, "_".join(c.split("_")[0] + str(i) for i, c in enumerate(counters)))
     cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", *counters, "--kernel-include-regex", "seed_kernel",
            "--output-format", "csv", "-d", d, "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_run.py"),
-           "--launches", "1", *rest]
+           "--launches", "1", *extra, *rest]
     subprocess.run(cmd, check=True)
     tot, disp = {}, {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -55,14 +56,19 @@ def main():
     a = bench.parse(rest)
     os.environ.setdefault("TMPDIR", "/tmp")
     r1 = run_pass(["TCC_EA0_RDREQ_sum", "TCC_HIT_sum", "TCC_MISS_sum"], own.tmp, rest)
-    r2 = run_pass(["WRITE_SIZE"], own.tmp, rest)
+    launch_json = os.path.join(own.tmp, "launch.json")
+    r2 = run_pass(["WRITE_SIZE"], own.tmp, rest, ["--stats-out", launch_json])
+    with open(launch_json) as fh:
+        launch = json.load(fh)
     out = {"rdreq_per_launch": r1["TCC_EA0_RDREQ_sum"][0], "tcc_hit_per_launch": r1["TCC_HIT_sum"][0],
            "tcc_miss_per_launch": r1["TCC_MISS_sum"][0], "write_bytes_per_launch": r2["WRITE_SIZE"][0] * 1024.0,
            "dispatches": [r1["TCC_EA0_RDREQ_sum"][1], r2["WRITE_SIZE"][1]],
            "counter": "TCC_EA0_RDREQ_sum (L2 -> fabric read requests), TCC_HIT/MISS_sum, WRITE_SIZE x 1024",
            "workload": {"genome_mbp": a.genome_mbp, "reads": a.reads, "read_len": a.read_len, "seed": a.seed,
                         "sub": a.sub, "genome_profile": a.genome_profile},
-           "build_id": smemgpu.source_hash(),  # == the loaded build (prof_run refuses nothing; bench checks)
+           "build_id": launch["build_id"],  # the library the counted launches ran on
+           "kernel_id": launch["kernel_id"],
+           "launch": {"grid": launch["grid"], "block": launch["block"]},
            "measured": time.strftime("%Y-%m-%d %H:%M:%S")}
     os.makedirs(os.path.dirname(own.out) or ".", exist_ok=True)
     with open(own.out, "w") as fh:
