@@ -434,13 +434,15 @@ def sa_lookup(batch, opt, reps: int = 3) -> dict:
     occurrence of the batch (software/bwamem.c:462-474), on the GPU; reported
     beside the SMEM metric, not part of a step."""
     batch.run(opt)
-    best = None
+    best, all_ms = None, []
     for _ in range(reps):
         batch.sa(opt.min_seed_len, 10000)
         st = batch.stats()
+        all_ms.append(st["sa_ms"])
         if best is None or st["sa_ms"] < best["sa_ms"]:
             best = st
-    return {"ms_per_batch": round(best["sa_ms"], 3), "occurrences": int(best["n_occ"]),
+    return {"ms_per_batch": round(best["sa_ms"], 3), "ms_per_batch_mean": round(float(np.mean(all_ms)), 3),
+            "ms_runs": [round(x, 3) for x in all_ms], "occurrences": int(best["n_occ"]),
             "occurrences_per_s": round(best["n_occ"] / (best["sa_ms"] * 1e-3), 1),
             "what": "bwt_sa of every seed occurrence (seed length >= 19, x2 <= max_occ 10000); "
                     ".sa sa_intv 32, device copy densified to every 4th row at load"}
@@ -452,14 +454,16 @@ def chain_report(batch, opt, l_pac: int, reps: int = 3) -> dict:
     SA positions left in HBM; reported beside the SMEM metric."""
     batch.run(opt)
     batch.sa(opt.min_seed_len, 10000)
-    best = None
+    best, all_ms = None, []
     for _ in range(reps):
         batch.chain(l_pac)
         st = batch.stats()
+        all_ms.append(st["chain_ms"])
         if best is None or st["chain_ms"] < best["chain_ms"]:
             best = st
     n = batch.n_reads
-    return {"ms_per_batch": round(best["chain_ms"], 3), "chains": int(best["n_chains"]),
+    return {"ms_per_batch": round(best["chain_ms"], 3), "ms_per_batch_mean": round(float(np.mean(all_ms)), 3),
+            "ms_runs": [round(x, 3) for x in all_ms], "chains": int(best["n_chains"]),
             "seed_occurrences": int(best["n_occ"]), "reads_per_s": round(n / (best["chain_ms"] * 1e-3), 1),
             "what": "mem_chain (kbtree of chains, test_and_merge) + mem_chain_flt, w 100, max_chain_gap 10000"}
 
@@ -489,21 +493,24 @@ def aln_report(gpu, batch, opt, l_pac: int, pac=None, reads=None, reps: int = 3,
     mem_chain2aln of every filtered chain, software/bwamem.c:1452-1460) on the
     GPU over the chains, seeds, reads and .pac already in HBM
     (smem_batch_chain2aln); reported beside the SMEM metric."""
-    from oracle import oracle
+    import smemgpu
     batch.run(opt)
     batch.sa(opt.min_seed_len, 10000)
     batch.chain(l_pac)
-    best = None
+    best, all_ms = None, []
     for _ in range(reps):
-        batch.chain2aln(oracle.aln_opt(min_seed_len=opt.min_seed_len))
+        batch.chain2aln(smemgpu.aln_opt(min_seed_len=opt.min_seed_len))
         st = batch.stats()
+        all_ms.append(st["aln_ms"])
         if best is None or st["aln_ms"] < best["aln_ms"]:
             best = st
     n = batch.n_reads
     cells = None
     if pac is not None and reads is not None:
-        # the DP cells the stage computes, counted by the restatement on the
-        # first cell_sample reads (same chains), scaled to the batch
+        # the DP cells the stage computes, counted by the restatement (the
+        # checker, not the measured path) on the first cell_sample reads
+        # (same chains), scaled to the batch
+        from oracle import oracle
         res = batch.fetch(mask=4)   # FETCH_CHAINS
         m = min(cell_sample, n)
         aopt = oracle.aln_opt(min_seed_len=opt.min_seed_len)
@@ -519,7 +526,8 @@ def aln_report(gpu, batch, opt, l_pac: int, pac=None, reads=None, reps: int = 3,
                  "extensions_by_qlen": {lab: {"calls": c, "cells": x} for lab, (c, x) in
                                         zip(("<=16", "<=32", "<=64", "<=128", "<=256", ">256"), shapes)},
                  "seed_regions": uses}
-    out = {"ms_per_batch": round(best["aln_ms"], 3), "regions": int(best["n_regs"]), "chains": int(best["n_chains"]),
+    out = {"ms_per_batch": round(best["aln_ms"], 3), "ms_per_batch_mean": round(float(np.mean(all_ms)), 3),
+           "ms_runs": [round(x, 3) for x in all_ms], "regions": int(best["n_regs"]), "chains": int(best["n_chains"]),
            "reads_per_s": round(n / (best["aln_ms"] * 1e-3), 1)}
     if cells:
         out["dp_cells"] = cells
@@ -559,16 +567,18 @@ def sw_report(gpu, genome_codes, n_unique: int = 20000, tile: int = 10, reps: in
     from smemgpu import synth
     kb = synth.make_ksw_tasks(genome_codes, n_unique, seed=771)
     big = synth.KswBatch(np.tile(kb.tasks, tile), kb.q, kb.t, kb.mat)
-    best = float("inf")
+    best, all_ms = float("inf"), []
     for _ in range(reps):
         _, ms = gpu.ksw_extend(big)
+        all_ms.append(ms)
         best = min(best, ms)
     cells = int(np.sum(kb.tasks["qlen"].astype(np.int64) * kb.tasks["tlen"])) * tile
     from oracle import oracle
     oracle.dp_cells(True)
     oracle.ksw(kb)
     band = oracle.dp_cells(True)[0] * tile   # in-band cells ksw_extend2 computes (restatement's count)
-    return {"tasks": int(big.tasks.size), "kernel_ms": round(best, 3), "dp_cells_in_band": band,
+    return {"tasks": int(big.tasks.size), "kernel_ms": round(best, 3),
+            "kernel_ms_mean": round(float(np.mean(all_ms)), 3), "dp_cells_in_band": band,
             "roofline": dp_roofline(band, best),
             "tasks_per_s": round(big.tasks.size / (best * 1e-3), 1),
             "what": "ksw_extend2 (software/ksw.c:379), one wave per problem; synthetic mem_chain2aln-shaped "

@@ -225,10 +225,15 @@ __device__ __forceinline__ void flt_combsort(FltRec* a, size_t n) {
     if (gap != 1) flt_insertsort(a, n);
 }
 
-// ks_introsort(mem_flt) (software/ksort.h:176-224), comparison for comparison
-__device__ __forceinline__ void flt_sort(FltRec* a, size_t n) {
-    size_t sl[64], sr[64];
-    int sd[64];
+// ks_introsort(mem_flt) (software/ksort.h:176-224), comparison for comparison.
+// The pending segments go to stk (3 words each: s, t, depth budget) in the
+// caller's LDS or HBM, not to a private array: a 1.3 KB per-lane stack made
+// every queue that ran the chain kernels allocate scratch for 64 lanes x
+// every wave slot, and with 16 hardware queues the runtime ran out of scratch
+// and aborted queues (failure contract).  The loop pushes only
+// segments of more than 16 records and always the larger half, so at most
+// log2(n / 16) + 1 <= 29 are pending for n < 2^32: 64 entries.
+__device__ __forceinline__ void flt_sort(FltRec* a, uint32_t n, uint32_t* stk) {
     int top = 0, d;
     if (n < 1) return;
     if (n == 2) {
@@ -238,7 +243,7 @@ __device__ __forceinline__ void flt_sort(FltRec* a, size_t n) {
     for (d = 2; (1ull << d) < n; ++d) {
     }
     d <<= 1;
-    size_t s = 0, t = n - 1;
+    uint32_t s = 0, t = n - 1;
     for (;;) {
         if (s < t) {
             if (--d == 0) {
@@ -246,7 +251,7 @@ __device__ __forceinline__ void flt_sort(FltRec* a, size_t n) {
                 t = s;
                 continue;
             }
-            size_t i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            uint32_t i = s, j = t, k = i + ((j - i) >> 1) + 1;
             if (flt_lt(a[k], a[i])) {
                 if (flt_lt(a[k], a[j])) k = j;
             } else {
@@ -265,17 +270,17 @@ __device__ __forceinline__ void flt_sort(FltRec* a, size_t n) {
             flt_swap(a, i, t);
             if (i - s > t - i) {
                 if (i - s > 16) {
-                    sl[top] = s;
-                    sr[top] = i - 1;
-                    sd[top] = d;
+                    stk[3 * top] = s;
+                    stk[3 * top + 1] = i - 1;
+                    stk[3 * top + 2] = (uint32_t)d;
                     ++top;
                 }
                 s = t - i > 16 ? i + 1 : t;
             } else {
                 if (t - i > 16) {
-                    sl[top] = i + 1;
-                    sr[top] = t;
-                    sd[top] = d;
+                    stk[3 * top] = i + 1;
+                    stk[3 * top + 1] = t;
+                    stk[3 * top + 2] = (uint32_t)d;
                     ++top;
                 }
                 t = i - s > 16 ? i - 1 : s;
@@ -286,9 +291,9 @@ __device__ __forceinline__ void flt_sort(FltRec* a, size_t n) {
                 return;
             }
             --top;
-            s = sl[top];
-            t = sr[top];
-            d = sd[top];
+            s = stk[3 * top];
+            t = stk[3 * top + 1];
+            d = (int)stk[3 * top + 2];
         }
     }
 }
@@ -662,15 +667,16 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
 }
 
 // weights + sort + reorder of mem_chain_flt (software/bwamem.c:636-651) by
-// one lane; ord holds the tree order, ord2 receives the sorted order
+// one lane; ord holds the tree order, ord2 receives the sorted order; stk:
+// the sort's 64-entry stack (192 words)
 __device__ __forceinline__ void flt_prepare_serial(const ChainParams& P, uint64_t S, FltRec* a, const uint32_t* ord,
-                                                   uint32_t* ord2, int n) {
+                                                   uint32_t* ord2, int n, uint32_t* stk) {
     const ChainRec* chn = P.chn + S;
     for (int i = 0; i < n; ++i) {
         const ChainRec c = chn[ord[i]];
         a[i] = FltRec{c.first_qbeg, c.last_qbeg + c.last_len, chain_weight(c, P.seed + S, P.next + S), i, -1};
     }
-    flt_sort(a, (size_t)n);
+    flt_sort(a, (uint32_t)n, stk);
     for (int i = 0; i < n; ++i) {
         ord2[i] = ord[a[i].p];
         a[i].p = i;
@@ -1556,11 +1562,13 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
 // (weight, position) keys and a permute.
 // ---------------------------------------------------------------------------
 
-// the serial loop from segment [s, t] with depth budget d, without the
-// closing insertion sort
-__device__ void flt_sort_seg_serial(FltRec* a, size_t s, size_t t, int d) {
-    size_t sl[64], sr[64];
-    int sd[64];
+// the serial loop from segment [s, t] (t < 2^16: flt_sort_wave takes n <
+// 2^16) with depth budget d, without the closing insertion sort; at most
+// log2(2^16 / 16) + 1 = 13 segments are pending (see flt_sort), kept as
+// s | t << 16 and d in 16-entry arrays small enough for registers
+__device__ void flt_sort_seg_serial(FltRec* a, uint32_t s, uint32_t t, int d) {
+    uint32_t sst[16];
+    uint8_t sdd[16];
     int top = 0;
     for (;;) {
         if (s < t) {
@@ -1569,7 +1577,7 @@ __device__ void flt_sort_seg_serial(FltRec* a, size_t s, size_t t, int d) {
                 t = s;
                 continue;
             }
-            size_t i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            uint32_t i = s, j = t, k = i + ((j - i) >> 1) + 1;
             if (flt_lt(a[k], a[i])) {
                 if (flt_lt(a[k], a[j])) k = j;
             } else {
@@ -1588,17 +1596,15 @@ __device__ void flt_sort_seg_serial(FltRec* a, size_t s, size_t t, int d) {
             flt_swap(a, i, t);
             if (i - s > t - i) {
                 if (i - s > 16) {
-                    sl[top] = s;
-                    sr[top] = i - 1;
-                    sd[top] = d;
+                    sst[top] = s | (i - 1) << 16;
+                    sdd[top] = (uint8_t)d;
                     ++top;
                 }
                 s = t - i > 16 ? i + 1 : t;
             } else {
                 if (t - i > 16) {
-                    sl[top] = i + 1;
-                    sr[top] = t;
-                    sd[top] = d;
+                    sst[top] = (i + 1) | t << 16;
+                    sdd[top] = (uint8_t)d;
                     ++top;
                 }
                 t = i - s > 16 ? i - 1 : s;
@@ -1606,9 +1612,9 @@ __device__ void flt_sort_seg_serial(FltRec* a, size_t s, size_t t, int d) {
         } else {
             if (top == 0) return;
             --top;
-            s = sl[top];
-            t = sr[top];
-            d = sd[top];
+            s = sst[top] & 0xffffu;
+            t = sst[top] >> 16;
+            d = sdd[top];
         }
     }
 }
@@ -1778,7 +1784,9 @@ __global__ __launch_bounds__(256) void chain_build_kernel(ChainParams P) {
         for (int i = 0; i < n; ++i) ord2[i] = ord[i];
     } else {
         FltRec* a = P.flt + S;
-        flt_prepare_serial(P, S, a, ord, ord2, n);
+        // the sort's stack in the read's kbtree node pool (>= 3 nodes of 256 B),
+        // free once the chains are listed
+        flt_prepare_serial(P, S, a, ord, ord2, n, reinterpret_cast<uint32_t*>(pool));
         const int m = flt_drop_serial(a, n, P.mask_level, P.drop_ratio, P.min_seed_len);
         n_keep = flt_squeeze_serial(a, m, ord, ord2, n);
     }
@@ -1945,8 +1953,8 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 flt_sort_wave(in_lds ? la : ga, (uint32_t)n, P.sort_lane_max, tl, tl + n, tl + 2 * n,
                               reinterpret_cast<FltRec*>(gs), ord2, s_stk, lane);
             } else if (lane == 0) {
-                if (in_lds) flt_sort(la, (size_t)n);
-                else flt_sort(ga, (size_t)n);
+                if (in_lds) flt_sort(la, (uint32_t)n, s_stk);
+                else flt_sort(ga, (uint32_t)n, s_stk);
             }
             __syncthreads();
             if (dbg && lane == 0) dbg[6] = __builtin_readcyclecounter();

@@ -123,6 +123,23 @@ class ChainOptT(C.Structure):
                 ("chain_drop_ratio", C.c_float), ("filter", C.c_int)]
 
 
+class AlnOptT(C.Structure):
+    """smem_aln_opt_t: the mem_opt_t fields mem_chain2aln reads"""
+    _fields_ = [("mat", C.c_int8 * 25), ("pad", C.c_int8 * 3), ("o_del", C.c_int32), ("e_del", C.c_int32),
+                ("o_ins", C.c_int32), ("e_ins", C.c_int32), ("a", C.c_int32), ("w", C.c_int32), ("zdrop", C.c_int32),
+                ("pen_clip5", C.c_int32), ("pen_clip3", C.c_int32), ("min_seed_len", C.c_int32)]
+
+
+def aln_opt(**kw) -> AlnOptT:
+    """smem_aln_opt_default (mem_opt_init's scoring, software/bwamem.c:47-70)
+    with the named fields overridden (e.g. min_seed_len=19, w=100)."""
+    o = AlnOptT()
+    load().smem_aln_opt_default(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
 SEED_DT = np.dtype([("rbeg", "<i8"), ("qbeg", "<i4"), ("len", "<i4")])          # smem_seed_t = mem_seed_t
 CHAIN_DT = np.dtype([("pos", "<i8"), ("seed_off", "<u8"), ("n", "<i4"), ("pad", "<i4")])  # smem_chain_t
 
