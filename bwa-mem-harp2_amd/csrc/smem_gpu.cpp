@@ -83,7 +83,7 @@ int inject_fault(int stage) {
     if (n % (uint64_t)k) return SMEM_OK;
     snprintf(g_err, sizeof(g_err), "injected failure (SMEM_GPU_FAIL=%s): stage %s, call %llu", e, k_stage_name[stage],
              (unsigned long long)n);
-    if (strstr(c + 1, ":sticky")) g_hip_fault = 1;
+    if (strstr(c + 1, ":sticky")) g_hip_fault = 2;
     return SMEM_E_DEVICE;
 }
 
@@ -392,7 +392,7 @@ struct DeviceCall {
             --g->n_leased;
             g->adm_cv.notify_one();
         }
-        if (g_hip_fault && !g->faulted.exchange(1)) {
+        if (g_hip_fault && !g->faulted.exchange(g_hip_fault)) {
             std::lock_guard<std::mutex> lk(g->adm_mu);
             snprintf(g->fault_msg, sizeof(g->fault_msg), "%s", g_err);
         }
@@ -2298,6 +2298,16 @@ static int batch_warmup(smem_batch_t* b) {
     if (!rc && g->d_sa && b->max_len <= 1024) rc = smem_batch_chain2aln(b, &ao);
     if (!rc && b->aln_ran) rc = smem_batch_fetch_mask(b, SMEM_FETCH_REGS);
     return rc;
+}
+
+int smem_gpu_fault(const smem_gpu_t* g, char* msg, int msg_len) {
+    if (!g) return SMEM_E_ARG;
+    const int f = const_cast<smem_gpu_t*>(g)->faulted.load();
+    if (f && msg && msg_len > 0) {
+        std::lock_guard<std::mutex> lk(const_cast<smem_gpu_t*>(g)->adm_mu);
+        snprintf(msg, (size_t)msg_len, "%s", g->fault_msg);
+    }
+    return f;
 }
 
 int smem_gpu_set_max_active(smem_gpu_t* g, int n) {

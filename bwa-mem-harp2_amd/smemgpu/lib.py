@@ -34,7 +34,7 @@ EXPORTED = [
     "smem_gpu_seed_stream", "smem_batch_results_packed",
     "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
     "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
-    "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id",
+    "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id", "smem_gpu_fault",
 ]
 
 # smem_batch_fetch_mask bits (include/smem_gpu.h)
@@ -231,6 +231,7 @@ def load() -> C.CDLL:
     lib.smem_gpu_kernel_id.restype = C.c_char_p
     lib.smem_gpu_reserve_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
     lib.smem_gpu_set_max_active.argtypes = [C.c_void_p, C.c_int]
+    lib.smem_gpu_fault.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
     _lib = lib
     return lib
 
@@ -470,6 +471,12 @@ class Gpu:
     def set_max_active(self, n: int) -> None:
         """Admission: at most n calls on the device at once (smem_gpu_set_max_active; 0 = default)."""
         _check(load().smem_gpu_set_max_active(self._h, n), "smem_gpu_set_max_active")
+
+    def fault(self) -> tuple:
+        """(0 | 1 runtime fault | 2 injected sticky fault, message) -- smem_gpu_fault"""
+        buf = C.create_string_buffer(512)
+        f = load().smem_gpu_fault(self._h, buf, 512)
+        return f, buf.value.decode(errors="replace")
 
     def reserve_slots(self, n_slots: int, reads_per_slot: int, max_len: int) -> None:
         """Pre-size collect_ex worker slots in the background (smem_gpu_reserve_slots)."""

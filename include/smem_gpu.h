@@ -188,6 +188,11 @@ int  smem_gpu_reserve_slots(smem_gpu_t *gpu, int n_slots, int reads_per_slot, in
  * others wait for a pair instead of being rejected.  Default 8, or
  * SMEM_GPU_MAX_ACTIVE at smem_gpu_init; 0 restores the default. */
 int  smem_gpu_set_max_active(smem_gpu_t *gpu, int n);
+/* 0: the device has not faulted; 1: a HIP runtime failure faulted it (the
+ * HIP runtime may also have printed its own diagnostics -- on a queue abort,
+ * a dump of the queue's packets on stdout); 2: an injected sticky fault
+ * (SMEM_GPU_FAIL).  msg (may be NULL) gets the first failure's text. */
+int  smem_gpu_fault(const smem_gpu_t *gpu, char *msg, int msg_len);
 
 /* ------------------------------------------------------------ streaming */
 /* bwa mem's chunk loop (software/fastmap.c:213-228, mem_process_seqs ->

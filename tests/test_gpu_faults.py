@@ -70,6 +70,7 @@ def test_injected_failure_then_clean_rerun(small, gpu_device, fail_env, stage):
         b.set_reads(r.codes, r.offs)
         b.run()
         assert b.fetch().to_smgo() == small["want"]
+        assert gpu.fault()[0] == 0
         b.close()
     finally:
         fail_env(None)
@@ -89,6 +90,8 @@ def test_sticky_fault_refuses_every_later_call(small, gpu_device, fail_env):
         with pytest.raises(smemgpu.SmemError, match="SMEM_E_DEVICE"):
             b.run()
         fail_env(None)
+        f, msg = gpu.fault()
+        assert f == 2 and "injected" in msg, (f, msg)  # 2: injected (1 would be a real runtime fault)
         for call in (lambda: b.set_reads(r.codes, r.offs), lambda: b.run(),
                      lambda: gpu.batch(10, 1000, 100)):
             with pytest.raises(smemgpu.SmemError, match="faulted earlier"):
