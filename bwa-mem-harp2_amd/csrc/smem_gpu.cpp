@@ -123,6 +123,7 @@ struct DevBuf {
         p = nullptr;
         n = 0;
     }
+    uint64_t bytes() const { return p ? (uint64_t)n * sizeof(T) : 0; }
 };
 
 template <class T>
@@ -150,6 +151,7 @@ struct HostBuf {
         p = nullptr;
         n = 0;
     }
+    uint64_t bytes() const { return p ? (uint64_t)n * sizeof(T) : 0; }
 };
 
 }  // namespace
@@ -214,7 +216,7 @@ struct smem_gpu {
     hipStream_t init_st = nullptr;
     hipEvent_t sa_ready = nullptr;
     uint64_t* d_sa_raw = nullptr;  // the .sa as uploaded, freed once sa_ready has passed
-    std::shared_future<int> reserve;
+    std::vector<std::shared_future<int>> reserve;  // smem_gpu_reserve_slots: one per slot
 };
 
 // scratch of the heavy-read path of chains -> regions
@@ -236,15 +238,16 @@ struct AlnHeavyBufs {
     DevBuf<int64_t> chmax, crb, cre;
     DevBuf<uint8_t> cmade, ctmp;
     DevBuf<uint2> crng;
+    // f(buf) for every buffer (release, sizes)
+    template <class F>
+    void each(F&& f) {
+        f(ckey); f(ckey2); f(coff); f(ccnt); f(cval); f(cval2); f(cq); f(cpos_s); f(cpos_c); f(chord); f(chmax);
+        f(crb); f(cre); f(cmade); f(ctmp); f(crng); f(heavy); f(hcnt); f(hoff); f(hscnt); f(span); f(ht); f(rnext);
+        f(pre); f(pre_short); f(loc); f(short_ok); f(pre_ok); f(tmp); f(tasks); f(torder); f(lq); f(tfail); f(sdec);
+        f(chain_read); f(swlist); f(htasks); f(htorder); f(hlq); f(htfail);
+    }
     void release() {
-        ckey.release(); ckey2.release(); coff.release(); ccnt.release(); cval.release(); cval2.release();
-        cq.release(); cpos_s.release(); cpos_c.release(); chord.release(); chmax.release(); crb.release(); cre.release();
-        cmade.release(); ctmp.release(); crng.release();
-        heavy.release(); hcnt.release(); hoff.release(); hscnt.release(); span.release(); ht.release(); rnext.release();
-        pre.release();
-        pre_short.release(); loc.release(); short_ok.release(); pre_ok.release(); tmp.release();
-        tasks.release(); torder.release(); lq.release(); tfail.release(); sdec.release(); chain_read.release();
-        swlist.release(); htasks.release(); htorder.release(); hlq.release(); htfail.release();
+        each([](auto& x) { x.release(); });
     }
 };
 
@@ -328,6 +331,26 @@ struct smem_batch {
     uint64_t tot_regs = 0;
     smem_batch_stats_t stats{};
 };
+
+// d(buf) for every device buffer of a batch, h(buf) for every pinned host one
+template <class D, class H>
+static void batch_bufs(smem_batch_t* b, D&& d, H&& h) {
+    h(b->h_codes); h(b->h_offs); d(b->d_codes); d(b->d_offs);
+    d(b->d_out_intv); d(b->d_out_call); d(b->d_n_intv); d(b->d_n_calls);
+    d(b->d_ctr); d(b->d_ovf_items); d(b->d_ovf_slot); d(b->d_ovf_items2);
+    d(b->d_scratch); d(b->d_dbg); d(b->d_ovf_intv); d(b->d_ovf_call); d(b->d_ovf_n_intv);
+    d(b->d_ovf_n_calls); d(b->d_sz_intv); d(b->d_sz_calls); d(b->d_intv_off);
+    d(b->d_call_off); d(b->d_scan_tmp); d(b->d_flat_intv); d(b->d_flat_calls);
+    d(b->d_occ_n); d(b->d_occ_off); d(b->d_sa_pos); d(b->d_sa_tmp); d(b->d_kstart); h(b->h_occ_off); h(b->h_sa_pos);
+    d(b->d_seed); d(b->d_out_seed); d(b->d_next); d(b->d_ord); d(b->d_ord2);
+    d(b->d_chn); d(b->d_node); d(b->d_flt); d(b->d_n_out); d(b->d_ns_out);
+    d(b->d_chain_off); d(b->d_seed_off); d(b->d_out_chain); d(b->d_heavy);
+    h(b->h_chain_off); h(b->h_out_chain); h(b->h_out_seed);
+    d(b->d_aln_srt); d(b->d_aln_nregs); d(b->d_aln_regoff); d(b->d_aln_raw);
+    d(b->d_aln_out); d(b->d_aln_ctr); b->aln_heavy.each(d); h(b->h_aln_regoff); h(b->h_aln_regs);
+    h(b->h_ctr); h(b->h_tot); h(b->h_intv); h(b->h_calls);
+    d(b->d_pintv); h(b->h_pintv); h(b->h_intv_off); h(b->h_call_off);
+}
 
 // ---- admission and the drain on the way out of every device call
 static int gpu_check(smem_gpu_t* g) {
@@ -507,7 +530,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
     g_err[0] = 0;
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 28))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
 
     if (!smem_seed_variant_built(variant))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: A/B variant not in this build (make AB=1)");
@@ -569,23 +592,7 @@ void smem_batch_destroy(smem_batch_t* b) {
     // (every call drained its work before returning: nothing of this batch
     // is in flight, and its streams belong to the device's admission pool)
     (void)hipSetDevice(b->g->device);
-    b->h_codes.release(); b->h_offs.release(); b->d_codes.release(); b->d_offs.release();
-    b->d_out_intv.release(); b->d_out_call.release(); b->d_n_intv.release(); b->d_n_calls.release();
-    b->d_ctr.release(); b->d_ovf_items.release(); b->d_ovf_slot.release(); b->d_ovf_items2.release();
-    b->d_scratch.release(); b->d_dbg.release(); b->d_ovf_intv.release(); b->d_ovf_call.release(); b->d_ovf_n_intv.release();
-    b->d_ovf_n_calls.release(); b->d_sz_intv.release(); b->d_sz_calls.release(); b->d_intv_off.release();
-    b->d_call_off.release(); b->d_scan_tmp.release(); b->d_flat_intv.release(); b->d_flat_calls.release();
-    b->d_occ_n.release(); b->d_occ_off.release(); b->d_sa_pos.release(); b->d_sa_tmp.release();
-    b->d_kstart.release(); b->h_occ_off.release(); b->h_sa_pos.release();
-    b->d_seed.release(); b->d_out_seed.release(); b->d_next.release(); b->d_ord.release(); b->d_ord2.release();
-    b->d_chn.release(); b->d_node.release(); b->d_flt.release(); b->d_n_out.release(); b->d_ns_out.release();
-    b->d_chain_off.release(); b->d_seed_off.release(); b->d_out_chain.release(); b->d_heavy.release();
-    b->h_chain_off.release(); b->h_out_chain.release(); b->h_out_seed.release();
-    b->d_aln_srt.release(); b->d_aln_nregs.release(); b->d_aln_regoff.release(); b->d_aln_raw.release();
-    b->d_aln_out.release(); b->d_aln_ctr.release(); b->aln_heavy.release(); b->h_aln_regoff.release(); b->h_aln_regs.release();
-    b->h_ctr.release(); b->h_tot.release(); b->h_intv.release(); b->h_calls.release();
-    b->d_pintv.release(); b->h_pintv.release();
-    b->h_intv_off.release(); b->h_call_off.release();
+    batch_bufs(b, [](auto& x) { x.release(); }, [](auto& x) { x.release(); });
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
@@ -595,7 +602,8 @@ void smem_batch_destroy(smem_batch_t* b) {
 
 void smem_gpu_shutdown(smem_gpu_t* g) {
     if (!g) return;
-    if (g->reserve.valid()) g->reserve.wait();
+    for (auto& f : g->reserve)
+        if (f.valid()) f.wait();
     (void)hipSetDevice(g->device);
     for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
     g->per_thread.clear();
@@ -2176,9 +2184,9 @@ static int collect_batch(smem_gpu_t* g, int slot, int n_reads, int max_len, uint
     std::shared_future<int> res;
     {
         std::lock_guard<std::mutex> lk(g->mu);
-        res = g->reserve;
+        if (slot >= 0 && (size_t)slot < g->reserve.size()) res = g->reserve[(size_t)slot];
     }
-    if (res.valid()) res.wait();  // smem_gpu_reserve_slots still sizing the slots
+    if (res.valid()) res.wait();  // smem_gpu_reserve_slots still sizing this slot
     {
         std::lock_guard<std::mutex> lk(g->mu);
         if (slot >= 0) {
@@ -2300,6 +2308,44 @@ static int batch_warmup(smem_batch_t* b) {
     return rc;
 }
 
+int smem_batch_memory(const smem_batch_t* b, uint64_t* device_bytes, uint64_t* pinned_bytes) {
+    if (!b) return SMEM_E_ARG;
+    uint64_t d = 0, h = 0;
+    batch_bufs(const_cast<smem_batch_t*>(b), [&](auto& x) { d += x.bytes(); }, [&](auto& x) { h += x.bytes(); });
+    if (device_bytes) *device_bytes = d;
+    if (pinned_bytes) *pinned_bytes = h;
+    return SMEM_OK;
+}
+
+int smem_gpu_memory(smem_gpu_t* g, uint64_t* index_bytes, uint64_t* batch_bytes, uint64_t* pinned_bytes, int* n_batches) {
+    if (!g) return SMEM_E_ARG;
+    uint64_t ix = 0, d = 0, h = 0;
+    int nb = 0;
+    const uint64_t n_ref = (g->bwt_size + 15) / 16;
+    ix += (n_ref * 16 + 16) * sizeof(uint32_t);                                   // Occ64
+    if (g->d_bwt) ix += (g->bwt_size + 16) * sizeof(uint32_t);                    // reference layout (A/B builds)
+    if (g->d_occ192) ix += ((2 * n_ref + 2) / 3 * 16 + 16) * sizeof(uint32_t);
+    if (g->d_kt) ix += (((1ull << (2 * (g->kt_k + 1))) - 4) / 3) * 16;
+    if (g->d_sa) ix += (g->n_sa + 1) * sizeof(uint64_t);                          // densified SA
+    if (g->d_sa_raw) ix += ((g->L2[4] >> 5) + 2) * sizeof(uint64_t);              // the uploaded .sa (sa_intv 32)
+    if (g->d_pac) ix += (uint64_t)(g->l_pac + 3) / 4 + 64;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        auto add = [&](const smem_batch_t* b) {
+            uint64_t bd = 0, bh = 0;
+            if (b && smem_batch_memory(b, &bd, &bh) == SMEM_OK) d += bd, h += bh, ++nb;
+        };
+        for (auto& kv : g->per_thread) add(kv.second);
+        for (auto* b : g->slots) add(b);
+        for (auto* b : g->stream_pool) add(b);
+    }
+    if (index_bytes) *index_bytes = ix;
+    if (batch_bytes) *batch_bytes = d;
+    if (pinned_bytes) *pinned_bytes = h;
+    if (n_batches) *n_batches = nb;
+    return SMEM_OK;
+}
+
 int smem_gpu_fault(const smem_gpu_t* g, char* msg, int msg_len) {
     if (!g) return SMEM_E_ARG;
     const int f = const_cast<smem_gpu_t*>(g)->faulted.load();
@@ -2326,28 +2372,40 @@ int smem_gpu_reserve_slots(smem_gpu_t* g, int n_slots, int reads_per_slot, int m
         return fail(SMEM_E_ARG, "smem_gpu_reserve_slots");
     if (int r = gpu_check(g)) return r;
     std::lock_guard<std::mutex> lk(g->mu);
-    if (g->reserve.valid() && g->reserve.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
-        return fail(SMEM_E_ARG, "smem_gpu_reserve_slots: a reservation is still running");
-    g->reserve = std::async(std::launch::async, [g, n_slots, reads_per_slot, max_len]() -> int {
-        g_no_inject = 1;
-        if (hipSetDevice(g->device) != hipSuccess) return SMEM_E_DEVICE;
-        int rc = SMEM_OK;
-        for (int k = 0; k < n_slots && rc == SMEM_OK; ++k) {
+    for (auto& f : g->reserve)
+        if (f.valid() && f.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
+            return fail(SMEM_E_ARG, "smem_gpu_reserve_slots: a reservation is still running");
+    // one host thread per slot (as the workers would each create their own on
+    // first use), slot 0's also runs the warm-up; a worker waits for its own
+    // slot only
+    g->reserve.assign((size_t)n_slots, std::shared_future<int>());
+    for (int k = 0; k < n_slots; ++k)
+        g->reserve[(size_t)k] = std::async(std::launch::async, [g, k, reads_per_slot, max_len]() -> int {
+            g_no_inject = 1;
+            if (hipSetDevice(g->device) != hipSuccess) return SMEM_E_DEVICE;
+            const auto t0 = std::chrono::steady_clock::now();
             smem_batch_t* b = nullptr;
-            rc = smem_batch_create(g, reads_per_slot, (uint64_t)reads_per_slot * (uint64_t)max_len, max_len, &b);
+            int rc = smem_batch_create(g, reads_per_slot, (uint64_t)reads_per_slot * (uint64_t)max_len, max_len, &b);
+            const auto t1 = std::chrono::steady_clock::now();
             if (rc == SMEM_OK) rc = batch_prealloc(b);
+            const auto t2 = std::chrono::steady_clock::now();
             if (rc == SMEM_OK && k == 0) rc = batch_warmup(b);
-            if (rc != SMEM_OK) {
+            if (getenv("SMEM_GPU_TIMES")) {  // diagnostics, as the binding's per-batch times
+                const auto t3 = std::chrono::steady_clock::now();
+                auto sec = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double>(d).count(); };
+                fprintf(stderr, "[M::smem_gpu_reserve_slots] device %d slot %d: create %.4f s, stage scratch %.4f s, "
+                        "warm-up %.4f s (rc %d)\n", g->device, k, sec(t1 - t0), sec(t2 - t1), sec(t3 - t2), rc);
+            }
+            if (rc != SMEM_OK) {  // the slot is created on its first use, as without the reservation
                 smem_batch_destroy(b);
-                break;
+                return rc;
             }
             std::lock_guard<std::mutex> lk2(g->mu);
             if (g->slots.size() <= (size_t)k) g->slots.resize((size_t)k + 1, nullptr);
             if (g->slots[(size_t)k]) smem_batch_destroy(g->slots[(size_t)k]);
             g->slots[(size_t)k] = b;
-        }
-        return rc;  // a slot left out is created on its first use, as without the reservation
-    }).share();
+            return SMEM_OK;
+        }).share();
     return SMEM_OK;
 }
 
@@ -2417,9 +2475,18 @@ int smem_gpu_init_devices(smem_gpu_t** gpus, int n, const int* devices, const ui
     // .sa densification kernels) run side by side
     auto open1 = [&](int i) {
         smem_gpu_t* g = nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         int r = smem_gpu_init(&g, devices ? devices[i] : i, bwt, bwt_size, primary, L2);
+        const auto t1 = std::chrono::steady_clock::now();
         if (!r && sa) r = smem_gpu_load_sa(g, sa);
+        const auto t2 = std::chrono::steady_clock::now();
         if (!r && pac) r = smem_gpu_load_pac(g, pac, l_pac);
+        if (getenv("SMEM_GPU_TIMES")) {
+            auto sec = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double>(d).count(); };
+            fprintf(stderr, "[M::smem_gpu_init_devices] device %d: index upload + Occ64 %.4f s, .sa upload %.4f s, "
+                    ".pac upload %.4f s (rc %d)\n", devices ? devices[i] : i, sec(t1 - t0), sec(t2 - t1),
+                    sec(std::chrono::steady_clock::now() - t2), r);
+        }
         if (r) {
             msg[i] = g_err;
             smem_gpu_shutdown(g);

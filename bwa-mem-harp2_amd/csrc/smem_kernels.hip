@@ -389,7 +389,18 @@ __device__ __forceinline__ void fetch_occ64_issue(const uint32_t* __restrict__ o
 
 // The same slot policy with the two slots in registers (VSLOT): the missing
 // buckets are loaded straight into s0 / s1 (the lanes that hit keep theirs)
-template <bool L192 = false>
+// NT: the bucket loads non-temporal (streamed through L2 without displacing
+// the lanes' list-arena and output lines)
+typedef uint32_t nt_v4u __attribute__((ext_vector_type(4)));
+template <bool L192 = false, bool NT = false>
+__device__ __forceinline__ uint4 ld_bucket16(const uint32_t* a) {
+    if constexpr (NT) {
+        const nt_v4u v = __builtin_nontemporal_load(reinterpret_cast<const nt_v4u*>(a));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *reinterpret_cast<const uint4*>(a);
+}
+template <bool L192 = false, bool NT = false>
 __device__ __forceinline__ void fetch_occ64_issue_regs(const uint32_t* __restrict__ occ, uint64_t kk, uint64_t ll,
                                                        uint32_t& t0, uint32_t& t1, int& ks, int& ls, uint4& s0a,
                                                        uint4& s0b, uint4& s1a, uint4& s1b) {
@@ -407,15 +418,15 @@ __device__ __forceinline__ void fetch_occ64_issue_regs(const uint32_t* __restric
     if (f0) {
         const uint32_t *a0, *a1;
         block_chunks<L192>(occ, b0, a0, a1);
-        s0a = *reinterpret_cast<const uint4*>(a0);
-        s0b = *reinterpret_cast<const uint4*>(a1);
+        s0a = ld_bucket16<L192, NT>(a0);
+        s0b = ld_bucket16<L192, NT>(a1);
         t0 = b0;
     }
     if (f1) {
         const uint32_t *a0, *a1;
         block_chunks<L192>(occ, b1, a0, a1);
-        s1a = *reinterpret_cast<const uint4*>(a0);
-        s1b = *reinterpret_cast<const uint4*>(a1);
+        s1a = ld_bucket16<L192, NT>(a0);
+        s1b = ld_bucket16<L192, NT>(a1);
         t1 = b1;
     }
 }
@@ -440,6 +451,24 @@ __device__ __forceinline__ void next_offsets(const SeedParams& P, int it, uint32
     const uint64_t a = P.offs[rid], b = P.offs[rid + 1];
     o0 = (uint32_t)a;
     len = (int)(b - a);
+}
+
+// a raw output record (Intv 32 B / CallRec 16 B), non-temporal when NT
+template <bool NT, class T>
+__device__ __forceinline__ void put_rec(T* p, const T& v) {
+    static_assert(sizeof(T) % 16 == 0, "16-B records");
+    if constexpr (NT) {
+        const uint4* s = reinterpret_cast<const uint4*>(&v);
+        nt_v4u* d = reinterpret_cast<nt_v4u*>(p);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(T) / 16); ++k) {
+            nt_v4u w;
+            w.x = s[k].x, w.y = s[k].y, w.z = s[k].z, w.w = s[k].w;
+            __builtin_nontemporal_store(w, d + k);
+        }
+    } else {
+        *p = v;
+    }
 }
 
 // chip-wide 100 MHz clock: wave start / end times comparable across XCDs
@@ -483,8 +512,12 @@ __device__ __forceinline__ uint64_t stamp() {
 // iteration (the advance) until its loads are issued, 2: raised for the
 // extend arithmetic after the wait (s_setprio; the SQ's arbitration between
 // the three waves of a SIMD)
+// NTM (A/B, bits): 1 the Occ bucket loads non-temporal; 2 the raw outputs
+// (intervals, list records) stored non-temporal -- finalize_kernel reads them
+// once, later, so they need not occupy L2 beside the list arena
 template <int FETCH, bool STAMP, int WPE, int NLIST, bool SINGLE = true, bool EARLY = false, bool L192 = false,
-          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool PFCH = false, int PRIO = 0>
+          bool FRING = false, bool DUAL = false, bool VSLOT = false, bool KTAB = false, bool PFCH = false, int PRIO = 0,
+          int NTM = 0>
 __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     // backward lists: the first NLIST entries live in LDS
     constexpr int NL = NLIST;
@@ -674,8 +707,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                     if (calls_n >= P.cap_calls) {
                         phase = P_OVF;
                     } else {
-                        P.out_call[(uint64_t)item * P.cap_calls + calls_n++] =
-                            CallRec{m_n, middle ? mem_n : 0u, (uint32_t)ori_start, max_len};
+                        put_rec<(NTM & 2) != 0>(P.out_call + (uint64_t)item * P.cap_calls + calls_n++,
+                                                CallRec{m_n, middle ? mem_n : 0u, (uint32_t)ori_start, max_len});
                         phase = P_NEXT2;
                     }
                 }
@@ -796,7 +829,7 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                                 break;
                             }
                             const uint64_t info = (uint64_t)ikend | ((uint64_t)(i + 1) << 32);
-                            P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] = Intv{ik0, ik1, ik2, info};
+                            put_rec<(NTM & 2) != 0>(P.out_intv + (uint64_t)item * P.cap_intv + raw_n++, Intv{ik0, ik1, ik2, info});
                             // the merge keeps a sub-match if it is at least half the longest
                             // match and ends after the call's start (software/bwamem.c:284-292)
                             keep_n += !middle || (ikend - (uint32_t)(i + 1) >= (max_len >> 1) && ikend > (uint32_t)ori_start);
@@ -932,8 +965,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
                                 phase = P_OVF;
                             } else {
                                 const uint64_t info = (uint64_t)p_end(pn) | ((uint64_t)(i + 1) << 32);
-                                P.out_intv[(uint64_t)item * P.cap_intv + raw_n++] =
-                                    Intv{p_x0(pn), p_x1(pn), p_x2(pn), info};
+                                put_rec<(NTM & 2) != 0>(P.out_intv + (uint64_t)item * P.cap_intv + raw_n++,
+                                                        Intv{p_x0(pn), p_x1(pn), p_x2(pn), info});
                                 keep_n += !middle || (p_end(pn) - (uint32_t)(i + 1) >= (max_len >> 1) &&
                                                       p_end(pn) > (uint32_t)ori_start);
                                 ++mem_n;
@@ -1128,7 +1161,8 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
         }
         if constexpr (VS) {
             if (want && !ktp)
-                fetch_occ64_issue_regs<L192>(L192 ? P.occ192 : P.occ64, kk, ll, tag0, tag1, fks, fls, s0a, s0b, s1a, s1b);
+                fetch_occ64_issue_regs<L192, (NTM & 1) != 0>(L192 ? P.occ192 : P.occ64, kk, ll, tag0, tag1, fks, fls, s0a,
+                                                             s0b, s1a, s1b);
             if constexpr (DU) {
                 if (want2) {
                     ra2 = p_x0(ent2), rb2 = p_x1(ent2), rs2 = p_x2(ent2);
@@ -1331,10 +1365,11 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
 #ifdef SMEM_AB_VARIANTS
-    return variant == 0 || (variant >= 2 && variant <= 28);
+    return variant == 0 || (variant >= 2 && variant <= 31);
 #else
     return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23 || variant == 24 ||
-           variant == 25 || variant == 26 || variant == 27 || variant == 28;
+           variant == 25 || variant == 26 || variant == 27 || variant == 28 || variant == 29 || variant == 30 ||
+           variant == 31;
 #endif
 }
 
@@ -1351,6 +1386,10 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 28: the default without wave priority (round-2 default; 2 % slower, profiles/r03/ab/prio)
         case 28: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 27: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 2>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 29-31: the default with non-temporal bucket loads (29), raw output stores (30), both (31)
+        case 29: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 30: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1, 2>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 31: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1, 3>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

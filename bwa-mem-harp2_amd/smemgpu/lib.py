@@ -35,6 +35,7 @@ EXPORTED = [
     "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
     "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
     "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id", "smem_gpu_fault",
+    "smem_batch_memory", "smem_gpu_memory",
 ]
 
 # smem_batch_fetch_mask bits (include/smem_gpu.h)
@@ -232,6 +233,8 @@ def load() -> C.CDLL:
     lib.smem_gpu_reserve_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
     lib.smem_gpu_set_max_active.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_fault.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+    lib.smem_batch_memory.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
+    lib.smem_gpu_memory.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_int)]
     _lib = lib
     return lib
 
@@ -472,6 +475,13 @@ class Gpu:
         """Admission: at most n calls on the device at once (smem_gpu_set_max_active; 0 = default)."""
         _check(load().smem_gpu_set_max_active(self._h, n), "smem_gpu_set_max_active")
 
+    def memory(self) -> dict:
+        """smem_gpu_memory: bytes of the resident index, of the kept batches (device / pinned)."""
+        ix, d, h, nb = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_int()
+        _check(load().smem_gpu_memory(self._h, C.byref(ix), C.byref(d), C.byref(h), C.byref(nb)), "smem_gpu_memory")
+        return {"index_bytes": ix.value, "batch_device_bytes": d.value, "batch_pinned_bytes": h.value,
+                "batches": nb.value}
+
     def fault(self) -> tuple:
         """(0 | 1 runtime fault | 2 injected sticky fault, message) -- smem_gpu_fault"""
         buf = C.create_string_buffer(512)
@@ -624,6 +634,12 @@ class Batch:
     def run(self, opt: Options = Options()) -> None:
         o = opt.c()
         _check(load().smem_batch_run(self._h, C.byref(o)), "smem_batch_run")
+
+    def memory(self) -> tuple:
+        """(device bytes, pinned host bytes) this batch holds (smem_batch_memory)."""
+        d, h = C.c_uint64(), C.c_uint64()
+        _check(load().smem_batch_memory(self._h, C.byref(d), C.byref(h)), "smem_batch_memory")
+        return d.value, h.value
 
     def stats(self) -> dict:
         s = BatchStats()

@@ -193,6 +193,13 @@ int  smem_gpu_set_max_active(smem_gpu_t *gpu, int n);
  * a dump of the queue's packets on stdout); 2: an injected sticky fault
  * (SMEM_GPU_FAIL).  msg (may be NULL) gets the first failure's text. */
 int  smem_gpu_fault(const smem_gpu_t *gpu, char *msg, int msg_len);
+/* Memory held: a batch's device and pinned host buffers (they grow to the
+ * largest batch seen); a device's resident index (Occ64, densified SA and the
+ * uploaded samples, .pac) and the batches it keeps (worker slots, per-thread
+ * batches, the streaming pool) -- what a maintainer sizes -t / -b against. */
+int  smem_batch_memory(const smem_batch_t *b, uint64_t *device_bytes, uint64_t *pinned_bytes);
+int  smem_gpu_memory(smem_gpu_t *gpu, uint64_t *index_bytes, uint64_t *batch_bytes, uint64_t *pinned_bytes,
+                     int *n_batches);
 
 /* ------------------------------------------------------------ streaming */
 /* bwa mem's chunk loop (software/fastmap.c:213-228, mem_process_seqs ->

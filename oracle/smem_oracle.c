@@ -173,8 +173,19 @@ static void count_extend(const orc_bwt_t *b, const orc_intv_t *ik, int is_back, 
 
 /* SMEMs covering position x (software/bwt.c:776-835). Fills mem in start
  * order, returns the end of the longest exact match starting at x. */
+/* list entries per lane the GPU kernel keeps in LDS (smem_kernels.hip NLIST,
+ * 11 in the product build; ORC_LIST_LDS overrides): the n_*_hi / n_fwd_spill
+ * counters model the kernel's arena traffic (an entry at index >= NL) */
+static int list_lds(void)
+{
+	static int v = -1;
+	if (v < 0) { const char *e = getenv("ORC_LIST_LDS"); v = e ? atoi(e) : 11; }
+	return v;
+}
+
 static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_intv, ivec_t *mem, worker_t *w)
 {
+	const int NL = list_lds();
 	orc_intv_t ik, ok[4];
 	ivec_t *prev = &w->prev, *curr = &w->curr, *t;
 	int i, j, c, ret;
@@ -213,6 +224,7 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 	}
 	if (i == len) iv_push(&w->fwd, &ik);
 	w->st.n_fwd_push += w->fwd.n;
+	if ((int)w->fwd.n > NL) w->st.n_fwd_spill += w->fwd.n - NL;  /* the LDS ring spills its oldest entries */
 	iv_reverse(&w->fwd);                 /* longest match first (software/bwt.c:806) */
 	ret = (int)w->fwd.a[0].info;
 
@@ -225,7 +237,7 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 		had_u1 = has_u1; has_u1 = 0;
 		for (j = 0; j < (int)prev->n; ++j) {
 			orc_intv_t *p = &prev->a[j];
-			if (i < x - 1 && j >= 7) w->st.n_bwd_read_hi++;
+			if (i < x - 1 && j >= NL) w->st.n_bwd_read_hi++;
 			orc_extend(b, p, ok, 1);
 			count_extend(b, p, 1, c >= 0, &w->st);
 			if (c >= 0) { int sl = (int)(uint32_t)p->info - i; w->st.n_ext_len[sl < 32 ? sl : 32]++; }
@@ -243,7 +255,7 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 					iv_push(mem, &e);
 				}
 			} else if (curr->n == 0 || ok[c].x[2] != curr->a[curr->n - 1].x[2]) {
-				if (curr->n >= 7) w->st.n_bwd_push_hi++;
+				if ((int)curr->n >= NL) w->st.n_bwd_push_hi++;
 				ok[c].info = p->info;
 				iv_push(curr, &ok[c]);
 			}
@@ -387,6 +399,7 @@ static void add_stats(orc_stats_t *d, const orc_stats_t *s)
 	d->n_run_u1 += s->n_run_u1; d->n_ext_fwd_k12 += s->n_ext_fwd_k12;
 	{ int k; for (k = 0; k < 33; ++k) d->n_ext_len[k] += s->n_ext_len[k]; }
 	d->n_fwd_push += s->n_fwd_push; d->n_bwd_push_hi += s->n_bwd_push_hi; d->n_bwd_read_hi += s->n_bwd_read_hi;
+	d->n_fwd_spill += s->n_fwd_spill;
 }
 
 int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,

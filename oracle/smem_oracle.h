@@ -59,8 +59,9 @@ typedef struct {
 	uint64_t n_ext_fwd_k12; /* forward extends at depth i - x < 12 with no N before them */
 	uint64_t n_ext_len[33]; /* used extends by the length of the string they produce (32 = 32 or more) */
 	uint64_t n_fwd_push;    /* forward-list pushes (software/bwt.c:798, 801, 804) */
-	uint64_t n_bwd_push_hi; /* backward-list (curr) pushes at index >= 7 */
-	uint64_t n_bwd_read_hi; /* backward-list (prev, steps >= 2) reads at index >= 7 */
+	uint64_t n_bwd_push_hi; /* backward-list (curr) pushes at index >= NL (ORC_LIST_LDS, default 11) */
+	uint64_t n_bwd_read_hi; /* backward-list (prev, steps >= 2) reads at index >= NL */
+	uint64_t n_fwd_spill;   /* forward-list entries beyond NL (the kernel's LDS ring spills them) */
 } orc_stats_t;
 
 orc_bwt_t *orc_bwt_load(const char *fn);

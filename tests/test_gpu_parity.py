@@ -146,7 +146,7 @@ def test_few_lanes_many_reads_per_lane(world, gpu_device):
         gpu.close()
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 6, 9, 10, 11, 12, 13, 16, 19, 20, 21, 22, 24, 25, 27, 28])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 9, 10, 11, 12, 13, 16, 19, 20, 21, 22, 24, 25, 27, 28, 29, 30, 31])
 def test_kernel_variants(world, gpu_device, variant):
     """The A/B builds (reference-layout fetches, stamped, forward-list LDS
     ring) are bit-exact too.  The product library instantiates 9 (stamped)

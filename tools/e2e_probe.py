@@ -48,7 +48,9 @@ def main():
             p2 = subprocess.run(cmd, capture_output=True, env=dict(os.environ, SMEM_GPU_TIMES="1"), timeout=900)
             body = b"\n".join(l for l in p2.stdout.split(b"\n") if not l.startswith(b"@PG"))
             err = p2.stderr.decode(errors="replace")
-            keep = [l for l in err.split("\n") if "mem_batch_gpu" in l or "[W::" in l or "[E::" in l or "rror" in l]
+            keep = [l for l in err.split("\n") if "mem_batch_gpu" in l or "[W::" in l or "[E::" in l or "rror" in l
+                    or "reserve_slots" in l or "mem_process_seqs" in l or "init_devices" in l
+                    or "main_mem" in l or "real sec" in l or "held" in l]
             nl = body.count(b"\n")
             print(f"== {name}: rc {p2.returncode}, {time.time() - t:.1f} s, sha {hashlib.sha256(body).hexdigest()[:16]}, "
                   f"{nl} lines", flush=True)
