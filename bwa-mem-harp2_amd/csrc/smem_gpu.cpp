@@ -217,7 +217,16 @@ struct smem_gpu {
     hipEvent_t sa_ready = nullptr;
     uint64_t* d_sa_raw = nullptr;  // the .sa as uploaded, freed once sa_ready has passed
     std::vector<std::shared_future<int>> reserve;  // smem_gpu_reserve_slots: one per slot
+    // smem_gpu_init_devices_async: the upload running on a host thread; every
+    // entry point that touches the device waits for it (gpu_wait)
+    std::shared_future<int> ready;
 };
+
+// the background upload of smem_gpu_init_devices_async has finished (its
+// failure faulted the device, which gpu_check then reports)
+static void gpu_wait(smem_gpu_t* g) {
+    if (g && g->ready.valid()) g->ready.wait();
+}
 
 // scratch of the heavy-read path of chains -> regions
 struct AlnHeavyBufs {
@@ -374,6 +383,7 @@ struct DeviceCall {
     explicit DeviceCall(smem_gpu_t* g_) : g(g_) {
         g_err[0] = 0;
         g_hip_fault = 0;
+        gpu_wait(g);
         if ((rc = gpu_check(g))) return;
         hipError_t e = hipSetDevice(g->device);
         if (e != hipSuccess) {
@@ -469,6 +479,64 @@ int smem_gpu_device_count(void) {
     return n;
 }
 
+// a handle for `device` and the index's shape; gpu_open does the device work
+static smem_gpu_t* gpu_handle(int device, uint64_t bwt_size, uint64_t primary, const uint64_t L2[5]) {
+    smem_gpu_t* g = new (std::nothrow) smem_gpu_t();
+    if (!g) return nullptr;
+    g->device = device;
+    if (const char* v = getenv("SMEM_GPU_MAX_ACTIVE")) g->max_active = std::max(1, std::min(256, atoi(v)));
+    g->bwt_size = bwt_size;
+    g->primary = primary;
+    std::memcpy(g->L2, L2, sizeof(g->L2));
+    return g;
+}
+
+// the index resident on g's device: upload, Occ64 re-layout (the device
+// pointers stay null on failure)
+static int gpu_open(smem_gpu_t* g, const uint32_t* bwt) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_init: no HIP device");
+    if (g->device < 0 || g->device >= n) return fail(SMEM_E_ARG, "smem_gpu_init: device out of range");
+    HIP_TRY(hipSetDevice(g->device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, g->device));
+    g->n_cu = prop.multiProcessorCount;
+    const uint64_t bwt_size = g->bwt_size;
+    // +16 words: a whole 64-B bucket can be loaded at the very end
+    hipError_t e = hipMalloc(&g->d_bwt, (bwt_size + 16) * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        g->d_bwt = nullptr;
+        return fail(SMEM_E_NOMEM, "smem_gpu_init: hipMalloc(index)", e);
+    }
+    e = hipMemcpy(g->d_bwt, bwt, bwt_size * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(g->d_bwt + bwt_size, 0, 16 * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        (void)hipFree(g->d_bwt);
+        g->d_bwt = nullptr;
+        return fail(SMEM_E_DEVICE, "smem_gpu_init: upload", e);
+    }
+    // the Occ64 re-layout of the same index, built on the device
+    const uint64_t n_ref = (bwt_size + 15) / 16;
+    e = hipMalloc(&g->d_occ64, (n_ref * 16 + 16) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(g->d_occ64 + n_ref * 16, 0, 16 * sizeof(uint32_t));
+    if (e == hipSuccess) e = smem_launch_occ64(g->d_bwt, n_ref, g->d_occ64, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(g->d_bwt);
+        if (g->d_occ64) (void)hipFree(g->d_occ64);
+        g->d_bwt = nullptr;
+        g->d_occ64 = nullptr;
+        return fail(SMEM_E_DEVICE, "smem_gpu_init: Occ64 layout", e);
+    }
+#ifndef SMEM_AB_VARIANTS
+    // only the A/B variants 3 / 4 read the reference layout: 3.1 GB of HBM
+    // back at human size once Occ64 is built
+    (void)hipFree(g->d_bwt);
+    g->d_bwt = nullptr;
+#endif
+    return SMEM_OK;
+}
+
 int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bwt_size, uint64_t primary,
                   const uint64_t L2[5]) {
     g_err[0] = 0;
@@ -480,44 +548,12 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
     if ((bwt_size + 16) * sizeof(uint32_t) > (1ull << 32))
         return fail(SMEM_E_ARG, "smem_gpu_init: index larger than 4 GiB not supported");
     *out = nullptr;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_init: no HIP device");
-    if (device < 0 || device >= n) return fail(SMEM_E_ARG, "smem_gpu_init: device out of range");
-    HIP_TRY(hipSetDevice(device));
-    hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, device));
-    smem_gpu_t* g = new (std::nothrow) smem_gpu_t();
+    smem_gpu_t* g = gpu_handle(device, bwt_size, primary, L2);
     if (!g) return fail(SMEM_E_NOMEM, "smem_gpu_init");
-    g->device = device;
-    g->n_cu = prop.multiProcessorCount;
-    if (const char* v = getenv("SMEM_GPU_MAX_ACTIVE")) g->max_active = std::max(1, std::min(256, atoi(v)));
-    g->bwt_size = bwt_size;
-    g->primary = primary;
-    std::memcpy(g->L2, L2, sizeof(g->L2));
-    // +16 words: a whole 64-B bucket can be loaded at the very end
-    hipError_t e = hipMalloc(&g->d_bwt, (bwt_size + 16) * sizeof(uint32_t));
-    if (e != hipSuccess) { delete g; return fail(SMEM_E_NOMEM, "smem_gpu_init: hipMalloc(index)", e); }
-    e = hipMemcpy(g->d_bwt, bwt, bwt_size * sizeof(uint32_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(g->d_bwt + bwt_size, 0, 16 * sizeof(uint32_t));
-    if (e != hipSuccess) { (void)hipFree(g->d_bwt); delete g; return fail(SMEM_E_DEVICE, "smem_gpu_init: upload", e); }
-    // the Occ64 re-layout of the same index, built on the device
-    const uint64_t n_ref = (bwt_size + 15) / 16;
-    e = hipMalloc(&g->d_occ64, (n_ref * 16 + 16) * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(g->d_occ64 + n_ref * 16, 0, 16 * sizeof(uint32_t));
-    if (e == hipSuccess) e = smem_launch_occ64(g->d_bwt, n_ref, g->d_occ64, nullptr);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-        (void)hipFree(g->d_bwt);
-        if (g->d_occ64) (void)hipFree(g->d_occ64);
+    if (int rc = gpu_open(g, bwt)) {
         delete g;
-        return fail(SMEM_E_DEVICE, "smem_gpu_init: Occ64 layout", e);
+        return rc;
     }
-#ifndef SMEM_AB_VARIANTS
-    // only the A/B variants 3 / 4 read the reference layout: 3.1 GB of HBM
-    // back at human size once Occ64 is built
-    (void)hipFree(g->d_bwt);
-    g->d_bwt = nullptr;
-#endif
     *out = g;
     return SMEM_OK;
 }
@@ -534,6 +570,8 @@ int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
 
     if (!smem_seed_variant_built(variant))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: A/B variant not in this build (make AB=1)");
+    gpu_wait(g);
+    if (int r = gpu_check(g)) return r;
     if ((variant == 10 || variant == 22) && !g->d_occ192) {
         // the Occ192 layout (variant 10 only), built from Occ64 on first use
         std::lock_guard<std::mutex> lk(g->mu);
@@ -557,6 +595,8 @@ int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
 int smem_gpu_set_kmer_table(smem_gpu_t* g, int k) {
     g_err[0] = 0;
     if (!g || k < 0 || k > 15) return fail(SMEM_E_ARG, "smem_gpu_set_kmer_table: k must be 0..15");
+    gpu_wait(g);
+    if (int r = gpu_check(g)) return r;
     std::lock_guard<std::mutex> lk(g->mu);
     HIP_TRY(hipSetDevice(g->device));
     if (g->d_kt) {
@@ -602,6 +642,7 @@ void smem_batch_destroy(smem_batch_t* b) {
 
 void smem_gpu_shutdown(smem_gpu_t* g) {
     if (!g) return;
+    gpu_wait(g);
     for (auto& f : g->reserve)
         if (f.valid()) f.wait();
     (void)hipSetDevice(g->device);
@@ -633,6 +674,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     if (!g || !out || max_reads <= 0 || max_len <= 0 || max_len > (1 << 24)) return fail(SMEM_E_ARG, "smem_batch_create");
     if (max_bases >= (1ull << 32) - 64) return fail(SMEM_E_ARG, "smem_batch_create: >= 2^32 bases per batch");
     *out = nullptr;
+    gpu_wait(g);
     if (int r = gpu_check(g)) return r;
     HIP_TRY(hipSetDevice(g->device));
     smem_batch_t* b = new (std::nothrow) smem_batch_t();
@@ -1004,8 +1046,14 @@ int smem_batch_fetch_mask(smem_batch_t* b, int mask) {
 }
 
 
+static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa);
 int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
     g_err[0] = 0;
+    gpu_wait(g);
+    return load_sa_impl(g, sa);
+}
+
+static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
     if (!g || !sa || !sa->sa || sa->n_sa == 0 || sa->sa_intv == 0 || (sa->sa_intv & (sa->sa_intv - 1)))
         return fail(SMEM_E_ARG, "smem_gpu_load_sa: bad SA");
     if (sa->seq_len != g->L2[4] || sa->n_sa != (sa->seq_len + sa->sa_intv) / sa->sa_intv)
@@ -1491,8 +1539,14 @@ static int aln_opt_ok(const smem_aln_opt_t* opt) {
            opt->w >= 0;
 }
 
+static int load_pac_impl(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac);
 int smem_gpu_load_pac(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
     g_err[0] = 0;
+    gpu_wait(g);
+    return load_pac_impl(g, pac, l_pac);
+}
+
+static int load_pac_impl(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
     if (!g || !pac || l_pac <= 0 || 2 * (uint64_t)l_pac != g->L2[4])
         return fail(SMEM_E_ARG, "smem_gpu_load_pac: pac does not belong to this index (2 l_pac != seq_len)");
     // under the device lock and after every queued kernel: no batch may be
@@ -2319,6 +2373,7 @@ int smem_batch_memory(const smem_batch_t* b, uint64_t* device_bytes, uint64_t* p
 
 int smem_gpu_memory(smem_gpu_t* g, uint64_t* index_bytes, uint64_t* batch_bytes, uint64_t* pinned_bytes, int* n_batches) {
     if (!g) return SMEM_E_ARG;
+    gpu_wait(g);
     uint64_t ix = 0, d = 0, h = 0;
     int nb = 0;
     const uint64_t n_ref = (g->bwt_size + 15) / 16;
@@ -2509,6 +2564,76 @@ int smem_gpu_init_devices(smem_gpu_t** gpus, int n, const int* devices, const ui
         return rc[i];
     }
     return SMEM_OK;
+}
+
+int smem_gpu_init_devices_async(smem_gpu_t** gpus, int n, const int* devices, const uint32_t* bwt, uint64_t bwt_size,
+                                uint64_t primary, const uint64_t L2[5], const smem_sa_t* sa, const uint8_t* pac,
+                                int64_t l_pac) {
+    g_err[0] = 0;
+    if (!gpus || n <= 0 || n > 1024) return fail(SMEM_E_ARG, "smem_gpu_init_devices_async");
+    for (int i = 0; i < n; ++i) gpus[i] = nullptr;
+    // the argument checks of smem_gpu_init / load_sa / load_pac, here, before anything runs
+    if (!bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: bad index");
+    if (L2[4] >= (1ull << 34) - 2) return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: seq_len >= 2^34 not supported");
+    if ((bwt_size + 16) * sizeof(uint32_t) > (1ull << 32))
+        return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: index larger than 4 GiB not supported");
+    if (sa && (!sa->sa || sa->n_sa == 0 || sa->sa_intv == 0 || (sa->sa_intv & (sa->sa_intv - 1)) ||
+               sa->seq_len != L2[4] || sa->n_sa != (sa->seq_len + sa->sa_intv) / sa->sa_intv || sa->primary != primary))
+        return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: SA does not belong to this index");
+    if (pac && (l_pac <= 0 || 2 * (uint64_t)l_pac != L2[4]))
+        return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: pac does not belong to this index");
+    {   // the devices exist (as smem_gpu_init_devices reports it, before anything runs)
+        int nv = 0;
+        if (hipGetDeviceCount(&nv) != hipSuccess || nv <= 0)
+            return fail(SMEM_E_DEVICE, "smem_gpu_init_devices_async: no HIP device");
+        for (int i = 0; i < n; ++i)
+            if ((devices ? devices[i] : i) < 0 || (devices ? devices[i] : i) >= nv) {
+                snprintf(g_err, sizeof(g_err), "smem_gpu_init_devices_async: device %d: smem_gpu_init: device out of range",
+                         devices ? devices[i] : i);
+                return SMEM_E_ARG;
+            }
+    }
+    for (int i = 0; i < n; ++i) {
+        smem_gpu_t* g = gpu_handle(devices ? devices[i] : i, bwt_size, primary, L2);
+        if (!g) {
+            for (int k = 0; k < i; ++k) {
+                smem_gpu_shutdown(gpus[k]);
+                gpus[k] = nullptr;
+            }
+            return fail(SMEM_E_NOMEM, "smem_gpu_init_devices_async");
+        }
+        const smem_sa_t sa_copy = sa ? *sa : smem_sa_t{};  // the caller's struct may go out of scope; its arrays may not
+        const bool has_sa = sa != nullptr;
+        g->ready = std::async(std::launch::async, [g, bwt, sa_copy, has_sa, pac, l_pac]() -> int {
+            const auto t0 = std::chrono::steady_clock::now();
+            int r = gpu_open(g, bwt);
+            const auto t1 = std::chrono::steady_clock::now();
+            if (!r && has_sa) r = load_sa_impl(g, &sa_copy);
+            const auto t2 = std::chrono::steady_clock::now();
+            if (!r && pac) r = load_pac_impl(g, pac, l_pac);
+            if (getenv("SMEM_GPU_TIMES")) {
+                auto sec = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double>(d).count(); };
+                fprintf(stderr, "[M::smem_gpu_init_devices_async] device %d: index upload + Occ64 %.4f s, .sa upload "
+                        "%.4f s, .pac upload %.4f s (rc %d)\n", g->device, sec(t1 - t0), sec(t2 - t1),
+                        sec(std::chrono::steady_clock::now() - t2), r);
+            }
+            if (r) {  // every call on the handle is refused from now on (SMEM_E_DEVICE): the caller's CPU path
+                std::lock_guard<std::mutex> lk(g->adm_mu);
+                snprintf(g->fault_msg, sizeof(g->fault_msg), "initialisation failed: %s", g_err);
+                g->faulted.store(3);
+            }
+            return r;
+        }).share();
+        gpus[i] = g;
+    }
+    return SMEM_OK;
+}
+
+int smem_gpu_wait_ready(smem_gpu_t* g) {
+    g_err[0] = 0;
+    if (!g) return fail(SMEM_E_ARG, "smem_gpu_wait_ready");
+    gpu_wait(g);
+    return gpu_check(g);
 }
 
 }  // extern "C"

@@ -35,7 +35,7 @@ EXPORTED = [
     "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
     "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
     "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id", "smem_gpu_fault",
-    "smem_batch_memory", "smem_gpu_memory",
+    "smem_batch_memory", "smem_gpu_memory", "smem_gpu_init_devices_async", "smem_gpu_wait_ready",
 ]
 
 # smem_batch_fetch_mask bits (include/smem_gpu.h)
@@ -233,6 +233,9 @@ def load() -> C.CDLL:
     lib.smem_gpu_reserve_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
     lib.smem_gpu_set_max_active.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_fault.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+    lib.smem_gpu_init_devices_async.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                                P(C.c_uint64), C.c_void_p, C.c_void_p, C.c_int64]
+    lib.smem_gpu_wait_ready.argtypes = [C.c_void_p]
     lib.smem_batch_memory.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
     lib.smem_gpu_memory.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64), P(C.c_int)]
     _lib = lib
@@ -459,6 +462,32 @@ class Gpu:
         if variant:
             _check(lib.smem_gpu_set_kernel_variant(self._h, variant), "smem_gpu_set_kernel_variant")
         self.device = device
+
+    @classmethod
+    def open_async(cls, index: Index, devices, sa: "SA" = None, pac=None, l_pac: int = 0) -> list:
+        """smem_gpu_init_devices_async: one Gpu per entry of `devices`, whose
+        uploads run in the background (index, sa and pac must outlive them:
+        keep the objects alive until wait_ready() or close())."""
+        lib = load()
+        n = len(devices)
+        hs = (C.c_void_p * n)()
+        devs = (C.c_int * n)(*devices)
+        words = index.words
+        L2 = (C.c_uint64 * 5)(*[int(v) for v in index.L2])
+        pac_p = np.ascontiguousarray(pac, dtype=np.uint8).ctypes.data if pac is not None else None
+        _check(lib.smem_gpu_init_devices_async(hs, n, devs, words.ctypes.data, words.size, index.primary, L2,
+                                               C.byref(sa._raw) if sa is not None else None, pac_p, int(l_pac)),
+               "smem_gpu_init_devices_async")
+        out = []
+        for i in range(n):
+            g = cls.__new__(cls)
+            g._h = C.c_void_p(hs[i])
+            g.device = devices[i]
+            out.append(g)
+        return out
+
+    def wait_ready(self) -> None:
+        _check(load().smem_gpu_wait_ready(self._h), "smem_gpu_wait_ready")
 
     def set_variant(self, variant: int) -> None:
         """Seeding-kernel variant (0 = default; see smem_gpu_set_kernel_variant)."""

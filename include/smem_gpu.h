@@ -146,6 +146,18 @@ void smem_gpu_shutdown(smem_gpu_t *gpu);
 int  smem_gpu_init_devices(smem_gpu_t **gpus, int n, const int *devices, const uint32_t *bwt, uint64_t bwt_size,
                            uint64_t primary, const uint64_t L2[5], const smem_sa_t *sa, const uint8_t *pac,
                            int64_t l_pac);
+/* The same with the device work on one host thread per device: the call
+ * checks its arguments and returns; the uploads (and the .sa densification)
+ * run while the caller goes on (bwa mem reads its first chunk).  Every entry
+ * point that touches a device waits for its upload first; smem_gpu_wait_ready
+ * waits explicitly.  A failed upload faults the handle (smem_gpu_fault 3):
+ * every call on it is refused with SMEM_E_DEVICE, the caller's CPU path.  bwt,
+ * sa->sa and pac must stay valid until the device is ready (the smem_sa_t
+ * itself is copied). */
+int  smem_gpu_init_devices_async(smem_gpu_t **gpus, int n, const int *devices, const uint32_t *bwt, uint64_t bwt_size,
+                                 uint64_t primary, const uint64_t L2[5], const smem_sa_t *sa, const uint8_t *pac,
+                                 int64_t l_pac);
+int  smem_gpu_wait_ready(smem_gpu_t *gpu);
 /* "0,2,5" -> devices[] = {0, 2, 5}; NULL or "" -> every visible device.
  * Returns the count, or a negative code (bad list, more than max_devices,
  * no device for the empty spec). */
@@ -191,7 +203,8 @@ int  smem_gpu_set_max_active(smem_gpu_t *gpu, int n);
 /* 0: the device has not faulted; 1: a HIP runtime failure faulted it (the
  * HIP runtime may also have printed its own diagnostics -- on a queue abort,
  * a dump of the queue's packets on stdout); 2: an injected sticky fault
- * (SMEM_GPU_FAIL).  msg (may be NULL) gets the first failure's text. */
+ * (SMEM_GPU_FAIL); 3: smem_gpu_init_devices_async could not upload the index
+ * (nothing ran on the device).  msg (may be NULL) gets the first failure's text. */
 int  smem_gpu_fault(const smem_gpu_t *gpu, char *msg, int msg_len);
 /* Memory held: a batch's device and pinned host buffers (they grow to the
  * largest batch seen); a device's resident index (Occ64, densified SA and the

@@ -99,7 +99,7 @@ def test_gpu_sam_identical(indexed, gpu_device, g, kind, threads, batch, mode):
     got, err = _run(indexed[g], g, kind, threads, batch, env=GPU_MODES[mode])
     assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
     if mode == "two_ctx":
-        assert "resident on 2 GPU context(s)" in err, err[-2000:]
+        assert "on 2 GPU context(s)" in err, err[-2000:]
     _same(got, _golden(g, kind))
 
 

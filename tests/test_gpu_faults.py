@@ -133,6 +133,26 @@ def test_admission_bound_concurrent_workers(small, gpu_device):
     assert len(ok) == 18 and all(ok)
 
 
+def test_async_init_devices(small, gpu_device):
+    """smem_gpu_init_devices_async: the call returns before the upload; the
+    first device call waits for it and the results are bit-exact (two
+    contexts on the device, as the binding's "0,0"); a device that does not
+    exist is refused before anything runs, as smem_gpu_init_devices does."""
+    import smemgpu
+    with pytest.raises(smemgpu.SmemError, match="out of range"):
+        smemgpu.Gpu.open_async(small["idx"], [gpu_device, 63], sa=small["sa"])
+    gs = smemgpu.Gpu.open_async(small["idx"], [gpu_device, gpu_device], sa=small["sa"])
+    try:
+        r = small["reads"]
+        for g in gs:
+            assert smemgpu.seed(g, r.codes, r.offs).to_smgo() == small["want"]
+            g.wait_ready()
+            assert g.fault()[0] == 0
+    finally:
+        for g in gs:
+            g.close()
+
+
 # every stage, every k-th call; "any:5" spreads over all of them; the sticky
 # case faults the device on the first seeding call, so the rest is refused
 INJECT = ["upload:2", "seed:2", "sa:3", "chain:2", "aln:2", "fetch:3", "any:5", "seed:2:sticky"]
