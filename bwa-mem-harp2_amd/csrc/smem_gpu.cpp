@@ -2270,12 +2270,14 @@ static int collect_batch(smem_gpu_t* g, int slot, int n_reads, int max_len, uint
 
 // the later stages' scratch of a slot batch, sized before its first use at
 // per-read estimates above what 150-250 bp reads need on both bench profiles
-// (28 intervals, 4.5-9 seed occurrences and ~3 chains per read): a worker's
-// first batches then do not reallocate (each reallocation frees, and hipFree
-// waits for the whole device).  A batch that needs more grows as before.
+// (28-35 intervals, 4.5-10 seed occurrences, ~3 chains and regions per read):
+// a worker's first batches then do not reallocate (each reallocation frees,
+// and hipFree waits for the whole device).  A batch that needs more grows as
+// before.  (Generous estimates cost at shutdown: 16 slots of 62.5k reads at
+// 48 / 24 / 8 / 16 per read held 38.6 GB and took 0.43 s to free.)
 static int batch_prealloc(smem_batch_t* b) {
     const uint64_t R = (uint64_t)b->max_reads;
-    const uint64_t ni = R * 48, no = R * 24, nc = R * 8, ns = R * 16;
+    const uint64_t ni = R * 40, no = R * 16, nc = R * 6, ns = R * 12;
     HIP_TRY(b->d_flat_intv.ensure(ni));
     HIP_TRY(b->d_flat_calls.ensure(R * 8));
     HIP_TRY(b->d_occ_n.grow(ni));
@@ -2325,7 +2327,7 @@ static int batch_prealloc(smem_batch_t* b) {
     HIP_TRY(H.hcnt.grow(R));
     HIP_TRY(H.hscnt.grow(R));
     HIP_TRY(b->h_aln_regoff.grow(R + 1));
-    HIP_TRY(b->h_aln_regs.grow(ns));
+    HIP_TRY(b->h_aln_regs.grow(R * 4));  // pinned: the regions fetched (~3 per read)
     if (!b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
     if (!b->ev_fork) HIP_TRY(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     return SMEM_OK;
