@@ -2568,67 +2568,83 @@ int smem_gpu_init_devices(smem_gpu_t** gpus, int n, const int* devices, const ui
     return SMEM_OK;
 }
 
+// the device work of a handle as a chain of background steps: each waits for
+// the one before; a failure faults the handle (3), later steps do nothing
+static void gpu_chain(smem_gpu_t* g, const char* what, std::function<int()> step) {
+    std::shared_future<int> prev = g->ready;
+    g->ready = std::async(std::launch::async, [g, what, prev, step]() -> int {
+        if (prev.valid() && prev.get() != SMEM_OK) return SMEM_E_DEVICE;
+        const auto t0 = std::chrono::steady_clock::now();
+        const int r = step();
+        if (getenv("SMEM_GPU_TIMES"))
+            fprintf(stderr, "[M::smem_gpu_async] device %d: %s %.4f s (rc %d)\n", g->device, what,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), r);
+        if (r) {  // every call on the handle is refused from now on (SMEM_E_DEVICE): the caller's CPU path
+            std::lock_guard<std::mutex> lk(g->adm_mu);
+            snprintf(g->fault_msg, sizeof(g->fault_msg), "initialisation failed: %s", g_err);
+            g->faulted.store(3);
+        }
+        return r;
+    }).share();
+}
+
+int smem_gpu_open_async(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bwt_size, uint64_t primary,
+                        const uint64_t L2[5]) {
+    g_err[0] = 0;
+    if (!out || !bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_open_async: bad index");
+    *out = nullptr;
+    if (L2[4] >= (1ull << 34) - 2) return fail(SMEM_E_ARG, "smem_gpu_open_async: seq_len >= 2^34 not supported");
+    if ((bwt_size + 16) * sizeof(uint32_t) > (1ull << 32))
+        return fail(SMEM_E_ARG, "smem_gpu_open_async: index larger than 4 GiB not supported");
+    int nv = 0;  // the device exists (reported here, before anything runs)
+    if (hipGetDeviceCount(&nv) != hipSuccess || nv <= 0) return fail(SMEM_E_DEVICE, "smem_gpu_open_async: no HIP device");
+    if (device < 0 || device >= nv) return fail(SMEM_E_ARG, "smem_gpu_open_async: device out of range");
+    smem_gpu_t* g = gpu_handle(device, bwt_size, primary, L2);
+    if (!g) return fail(SMEM_E_NOMEM, "smem_gpu_open_async");
+    gpu_chain(g, "index upload + Occ64", [g, bwt]() { return gpu_open(g, bwt); });
+    *out = g;
+    return SMEM_OK;
+}
+
+int smem_gpu_load_sa_async(smem_gpu_t* g, const smem_sa_t* sa) {
+    g_err[0] = 0;
+    if (!g || !sa || !sa->sa || sa->n_sa == 0 || sa->sa_intv == 0 || (sa->sa_intv & (sa->sa_intv - 1)) ||
+        sa->seq_len != g->L2[4] || sa->n_sa != (sa->seq_len + sa->sa_intv) / sa->sa_intv || sa->primary != g->primary)
+        return fail(SMEM_E_ARG, "smem_gpu_load_sa_async: SA does not belong to this index");
+    const smem_sa_t copy = *sa;  // the caller's struct may go out of scope; its array may not
+    gpu_chain(g, ".sa upload (+ densify launched)", [g, copy]() { return load_sa_impl(g, &copy); });
+    return SMEM_OK;
+}
+
+int smem_gpu_load_pac_async(smem_gpu_t* g, const uint8_t* pac, int64_t l_pac) {
+    g_err[0] = 0;
+    if (!g || !pac || l_pac <= 0 || 2 * (uint64_t)l_pac != g->L2[4])
+        return fail(SMEM_E_ARG, "smem_gpu_load_pac_async: pac does not belong to this index");
+    gpu_chain(g, ".pac upload", [g, pac, l_pac]() { return load_pac_impl(g, pac, l_pac); });
+    return SMEM_OK;
+}
+
 int smem_gpu_init_devices_async(smem_gpu_t** gpus, int n, const int* devices, const uint32_t* bwt, uint64_t bwt_size,
                                 uint64_t primary, const uint64_t L2[5], const smem_sa_t* sa, const uint8_t* pac,
                                 int64_t l_pac) {
     g_err[0] = 0;
     if (!gpus || n <= 0 || n > 1024) return fail(SMEM_E_ARG, "smem_gpu_init_devices_async");
     for (int i = 0; i < n; ++i) gpus[i] = nullptr;
-    // the argument checks of smem_gpu_init / load_sa / load_pac, here, before anything runs
-    if (!bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: bad index");
-    if (L2[4] >= (1ull << 34) - 2) return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: seq_len >= 2^34 not supported");
-    if ((bwt_size + 16) * sizeof(uint32_t) > (1ull << 32))
-        return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: index larger than 4 GiB not supported");
-    if (sa && (!sa->sa || sa->n_sa == 0 || sa->sa_intv == 0 || (sa->sa_intv & (sa->sa_intv - 1)) ||
-               sa->seq_len != L2[4] || sa->n_sa != (sa->seq_len + sa->sa_intv) / sa->sa_intv || sa->primary != primary))
-        return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: SA does not belong to this index");
-    if (pac && (l_pac <= 0 || 2 * (uint64_t)l_pac != L2[4]))
-        return fail(SMEM_E_ARG, "smem_gpu_init_devices_async: pac does not belong to this index");
-    {   // the devices exist (as smem_gpu_init_devices reports it, before anything runs)
-        int nv = 0;
-        if (hipGetDeviceCount(&nv) != hipSuccess || nv <= 0)
-            return fail(SMEM_E_DEVICE, "smem_gpu_init_devices_async: no HIP device");
-        for (int i = 0; i < n; ++i)
-            if ((devices ? devices[i] : i) < 0 || (devices ? devices[i] : i) >= nv) {
-                snprintf(g_err, sizeof(g_err), "smem_gpu_init_devices_async: device %d: smem_gpu_init: device out of range",
-                         devices ? devices[i] : i);
-                return SMEM_E_ARG;
-            }
+    int rc = SMEM_OK;
+    for (int i = 0; i < n && rc == SMEM_OK; ++i) {
+        rc = smem_gpu_open_async(&gpus[i], devices ? devices[i] : i, bwt, bwt_size, primary, L2);
+        if (rc == SMEM_OK && sa) rc = smem_gpu_load_sa_async(gpus[i], sa);
+        if (rc == SMEM_OK && pac) rc = smem_gpu_load_pac_async(gpus[i], pac, l_pac);
     }
-    for (int i = 0; i < n; ++i) {
-        smem_gpu_t* g = gpu_handle(devices ? devices[i] : i, bwt_size, primary, L2);
-        if (!g) {
-            for (int k = 0; k < i; ++k) {
-                smem_gpu_shutdown(gpus[k]);
-                gpus[k] = nullptr;
-            }
-            return fail(SMEM_E_NOMEM, "smem_gpu_init_devices_async");
+    if (rc != SMEM_OK) {
+        std::string msg = g_err;
+        for (int k = 0; k < n; ++k) {
+            smem_gpu_shutdown(gpus[k]);
+            gpus[k] = nullptr;
         }
-        const smem_sa_t sa_copy = sa ? *sa : smem_sa_t{};  // the caller's struct may go out of scope; its arrays may not
-        const bool has_sa = sa != nullptr;
-        g->ready = std::async(std::launch::async, [g, bwt, sa_copy, has_sa, pac, l_pac]() -> int {
-            const auto t0 = std::chrono::steady_clock::now();
-            int r = gpu_open(g, bwt);
-            const auto t1 = std::chrono::steady_clock::now();
-            if (!r && has_sa) r = load_sa_impl(g, &sa_copy);
-            const auto t2 = std::chrono::steady_clock::now();
-            if (!r && pac) r = load_pac_impl(g, pac, l_pac);
-            if (getenv("SMEM_GPU_TIMES")) {
-                auto sec = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double>(d).count(); };
-                fprintf(stderr, "[M::smem_gpu_init_devices_async] device %d: index upload + Occ64 %.4f s, .sa upload "
-                        "%.4f s, .pac upload %.4f s (rc %d)\n", g->device, sec(t1 - t0), sec(t2 - t1),
-                        sec(std::chrono::steady_clock::now() - t2), r);
-            }
-            if (r) {  // every call on the handle is refused from now on (SMEM_E_DEVICE): the caller's CPU path
-                std::lock_guard<std::mutex> lk(g->adm_mu);
-                snprintf(g->fault_msg, sizeof(g->fault_msg), "initialisation failed: %s", g_err);
-                g->faulted.store(3);
-            }
-            return r;
-        }).share();
-        gpus[i] = g;
+        snprintf(g_err, sizeof(g_err), "smem_gpu_init_devices_async: %s", msg.c_str());
     }
-    return SMEM_OK;
+    return rc;
 }
 
 int smem_gpu_wait_ready(smem_gpu_t* g) {

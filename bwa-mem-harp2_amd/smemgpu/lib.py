@@ -36,6 +36,7 @@ EXPORTED = [
     "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
     "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id", "smem_gpu_fault",
     "smem_batch_memory", "smem_gpu_memory", "smem_gpu_init_devices_async", "smem_gpu_wait_ready",
+    "smem_gpu_open_async", "smem_gpu_load_sa_async", "smem_gpu_load_pac_async",
 ]
 
 # smem_batch_fetch_mask bits (include/smem_gpu.h)

@@ -158,6 +158,15 @@ int  smem_gpu_init_devices_async(smem_gpu_t **gpus, int n, const int *devices, c
                                  uint64_t primary, const uint64_t L2[5], const smem_sa_t *sa, const uint8_t *pac,
                                  int64_t l_pac);
 int  smem_gpu_wait_ready(smem_gpu_t *gpu);
+/* The steps of smem_gpu_init_devices_async one by one, so that each starts
+ * as soon as its input is in memory (bwa_idx_load reads .bwt, then .sa, then
+ * .pac): open_async checks the device and uploads the index in the
+ * background; load_sa_async / load_pac_async queue behind it.  Same waiting
+ * and fault rules. */
+int  smem_gpu_open_async(smem_gpu_t **gpu, int device, const uint32_t *bwt, uint64_t bwt_size, uint64_t primary,
+                         const uint64_t L2[5]);
+int  smem_gpu_load_sa_async(smem_gpu_t *gpu, const smem_sa_t *sa);
+int  smem_gpu_load_pac_async(smem_gpu_t *gpu, const uint8_t *pac, int64_t l_pac);
 /* "0,2,5" -> devices[] = {0, 2, 5}; NULL or "" -> every visible device.
  * Returns the count, or a negative code (bad list, more than max_devices,
  * no device for the empty spec). */
