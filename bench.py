@@ -108,7 +108,8 @@ def parse(argv=None):
     p.add_argument("--stream-reads", type=int, default=None,
                    help="reads per GPU pushed through the streaming path (default: the config's; 0: the resident "
                         "reads; -1: no streaming leg)")
-    p.add_argument("--stream-chunk", type=int, default=1 << 20)
+    p.add_argument("--stream-chunk", type=int, default=1 << 21,
+                   help="reads per streamed chunk (2M: 0.93 of the resident rate vs 0.86-0.88 at 1M, profiles/r04/stream)")
     p.add_argument("--stream-workers", type=int, default=3)
     p.add_argument("--stream-packed", type=int, default=1, help="1: 16-B wire entries (SMEM_STREAM_PACKED)")
     p.add_argument("--stream-passes", type=int, default=3, help="timed streaming passes; the median is reported")
