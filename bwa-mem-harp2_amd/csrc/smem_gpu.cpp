@@ -47,6 +47,13 @@ thread_local char g_err[512];
 thread_local int g_hip_fault = 0;
 // the library's own warm-up calls are not counted by SMEM_GPU_FAIL
 thread_local int g_no_inject = 0;
+// SMEM_GPU_TIMES diagnostics: this thread's seconds waiting for the device's
+// upload chain (gpu_wait) and for an admitted stream pair
+thread_local double g_t_ready = 0, g_t_admit = 0;
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static const double g_t_lib = now_s();  // the library's load (for a linked binary: its start)
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     if (e != hipSuccess)
@@ -383,7 +390,10 @@ struct DeviceCall {
     explicit DeviceCall(smem_gpu_t* g_) : g(g_) {
         g_err[0] = 0;
         g_hip_fault = 0;
+        const double t0 = now_s();
         gpu_wait(g);
+        const double t1 = now_s();
+        g_t_ready += t1 - t0;
         if ((rc = gpu_check(g))) return;
         hipError_t e = hipSetDevice(g->device);
         if (e != hipSuccess) {
@@ -392,6 +402,7 @@ struct DeviceCall {
         }
         std::unique_lock<std::mutex> lk(g->adm_mu);
         g->adm_cv.wait(lk, [&] { return !g->free_pairs.empty() || (int)g->pairs.size() < g->max_active; });
+        g_t_admit += now_s() - t1;
         if (!g->free_pairs.empty()) {
             pair = g->free_pairs.back();
             g->free_pairs.pop_back();
@@ -1100,8 +1111,27 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
         if (!g->init_st) e = hipStreamCreateWithFlags(&g->init_st, hipStreamNonBlocking);
         if (e == hipSuccess && !g->sa_ready) e = hipEventCreateWithFlags(&g->sa_ready, hipEventDisableTiming);
         if (e == hipSuccess) e = hipMemsetAsync(dense + n_dense, 0, sizeof(uint64_t), g->init_st);
-        if (e == hipSuccess) e = smem_launch_sa_densify(&S, dshift, n_dense, dense, g->init_st);
+        // hop + chase passes (each BWT row stepped over once, ~0.2 s at human
+        // size); SMEM_GPU_DENSIFY=walk: one full walk per dense row (the
+        // round-3 kernel, ~0.7 s), kept for A/B
+        const char* dv = getenv("SMEM_GPU_DENSIFY");
+        if (e == hipSuccess && n_dense < (1ull << 32) && !(dv && !strcmp(dv, "walk"))) {
+            uint64_t* link = nullptr;
+            e = hipMallocAsync((void**)&link, n_dense * sizeof(uint64_t), g->init_st);
+            if (e == hipSuccess) {
+                e = smem_launch_sa_densify2(&S, dshift, n_dense, link, dense, g->init_st);
+                hipError_t f = hipFreeAsync(link, g->init_st);
+                if (e == hipSuccess) e = f;
+            }
+        } else if (e == hipSuccess) {
+            e = smem_launch_sa_densify(&S, dshift, n_dense, dense, g->init_st);
+        }
         if (e == hipSuccess) e = hipEventRecord(g->sa_ready, g->init_st);
+        if (e == hipSuccess && getenv("SMEM_GPU_TIMES"))  // diagnostics: when the device got there
+            e = hipLaunchHostFunc(g->init_st, [](void* d) {
+                fprintf(stderr, "[M::smem_gpu_load_sa] device %d: .sa densified at %.3f s\n", (int)(intptr_t)d,
+                        now_s() - g_t_lib);
+            }, (void*)(intptr_t)g->device);
         if (e == hipSuccess && getenv("SMEM_GPU_SYNC_INIT")) e = hipStreamSynchronize(g->init_st);
         if (e != hipSuccess) {
             (void)hipDeviceSynchronize();
@@ -2450,8 +2480,10 @@ int smem_gpu_reserve_slots(smem_gpu_t* g, int n_slots, int reads_per_slot, int m
             if (getenv("SMEM_GPU_TIMES")) {  // diagnostics, as the binding's per-batch times
                 const auto t3 = std::chrono::steady_clock::now();
                 auto sec = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double>(d).count(); };
-                fprintf(stderr, "[M::smem_gpu_reserve_slots] device %d slot %d: create %.4f s, stage scratch %.4f s, "
-                        "warm-up %.4f s (rc %d)\n", g->device, k, sec(t1 - t0), sec(t2 - t1), sec(t3 - t2), rc);
+                fprintf(stderr, "[M::smem_gpu_reserve_slots] device %d slot %d at %.3f s: create %.4f s, stage scratch "
+                        "%.4f s, warm-up %.4f s (rc %d)\n", g->device, k,
+                        std::chrono::duration<double>(t0.time_since_epoch()).count() - g_t_lib, sec(t1 - t0),
+                        sec(t2 - t1), sec(t3 - t2), rc);
             }
             if (rc != SMEM_OK) {  // the slot is created on its first use, as without the reservation
                 smem_batch_destroy(b);
@@ -2481,10 +2513,19 @@ int smem_gpu_collect_ex(smem_gpu_t* g, int slot, int n_reads, const uint8_t* con
         bases += (uint64_t)len[i];
     }
     smem_batch_t* b = nullptr;
+    static const bool times = getenv("SMEM_GPU_TIMES") != nullptr;
+    const double t0 = times ? now_s() : 0;
+    g_t_ready = g_t_admit = 0;
     int rc = collect_batch(g, slot, n_reads, max_len, bases, &b);
+    const double t1 = times ? now_s() : 0;
     if (!rc) rc = smem_batch_set_reads(b, n_reads, seq, len);
+    const double t2 = times ? now_s() : 0;
     if (!rc) rc = smem_batch_run(b, opt);
     if (!rc && !(flags & SMEM_COLLECT_NO_FETCH)) rc = smem_batch_fetch(b);
+    if (times)  // diagnostics: where a worker's seeding call spent its time
+        fprintf(stderr, "[M::smem_gpu_collect] slot %d at %.3f s: batch %.4f s, reads in %.4f s, seeding %.4f s "
+                "(device-ready waits %.4f s, admission waits %.4f s)\n", slot, t0 - g_t_lib, t1 - t0, t2 - t1,
+                now_s() - t2, g_t_ready, g_t_admit);
     if (!rc) *batch_out = b;
     return rc;
 }
@@ -2577,8 +2618,8 @@ static void gpu_chain(smem_gpu_t* g, const char* what, std::function<int()> step
         const auto t0 = std::chrono::steady_clock::now();
         const int r = step();
         if (getenv("SMEM_GPU_TIMES"))
-            fprintf(stderr, "[M::smem_gpu_async] device %d: %s %.4f s (rc %d)\n", g->device, what,
-                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), r);
+            fprintf(stderr, "[M::smem_gpu_async] device %d: %s %.4f s, done at %.3f s (rc %d)\n", g->device, what,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), now_s() - g_t_lib, r);
         if (r) {  // every call on the handle is refused from now on (SMEM_E_DEVICE): the caller's CPU path
             std::lock_guard<std::mutex> lk(g->adm_mu);
             snprintf(g->fault_msg, sizeof(g->fault_msg), "initialisation failed: %s", g_err);

@@ -1811,7 +1811,102 @@ __global__ __launch_bounds__(256) void sa_densify_kernel(SaParams S, uint32_t ds
     dense[i] = steps + S.sa[k >> S.sa_shift];
 }
 
+// The same dense[] in two passes that share the walks.  The walk from row
+// i * D passes through other multiples of D on its way to a stored sample,
+// and every dense row's walk from there on is that row's own walk, so:
+//   hop pass:   every dense row that is not a stored sample walks only to the
+//               next multiple of D: link[i] = (that row / D) | steps << 32.
+//               The walks end at the first dense row, so together they step
+//               over each BWT row once: seq_len LF steps instead of
+//               n_dense * (sa_intv / D) * ~(D - 1).
+//   chase pass: dense[i] = the steps summed along the links up to a stored
+//               sample + that sample (unsigned, sa[0] = -1 wrapping as in
+//               software/bwt.c:110-113), sa_intv / D links on average, one
+//               8-B load each.
+// Walks and chains differ in length across the lanes of a wave, so both
+// passes deal their rows lane-strided and a lane that finishes takes its
+// next row in the same loop (the sa_walk_kernel scheme).  Link targets need
+// 32 bits: the host uses these passes while n_dense < 2^32.
+__global__ __launch_bounds__(256) void sa_densify_hop_kernel(SaParams S, uint32_t dshift, uint64_t n_dense,
+                                                              uint64_t* __restrict__ link) {
+    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t smask = (1ull << (S.sa_shift - dshift)) - 1;  // dense rows that are stored samples
+    const uint64_t dmask = (1ull << dshift) - 1;
+    const uint4* occ = reinterpret_cast<const uint4*>(S.occ64);
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool live = i < n_dense;
+    uint64_t k = i << dshift, steps = 0;
+    while (__any(live)) {
+        if (live && ((i & smask) == 0 || (steps && (k & dmask) == 0))) {
+            if (i & smask) link[i] = (k >> dshift) | steps << 32;
+            i += lanes;
+            live = i < n_dense;
+            k = i << dshift;
+            steps = 0;
+        } else if (live) {  // bwt_invPsi (software/bwt.c:71-77) on the Occ64 bucket
+            if (k == S.primary) {
+                k = 0;
+            } else {
+                const uint64_t kk = k - (k > S.primary);
+                const uint4 va = occ[(kk >> 6) * 2], vb = occ[(kk >> 6) * 2 + 1];
+                const uint32_t pos = (uint32_t)(kk & 63), sel = pos >> 4;
+                const uint32_t w = sel == 0 ? vb.x : (sel == 1 ? vb.y : (sel == 2 ? vb.z : vb.w));
+                const int c = (int)((w >> ((~pos & 15u) << 1)) & 3u);
+                uint32_t C, G, T;
+                count_cgt4(vb, pos, C, G, T);
+                const uint64_t oc = occ_cgt(va, 0) + C, og = occ_cgt(va, 1) + G, ot = occ_cgt(va, 2) + T;
+                const uint64_t n = c == 0 ? kk + 1 - oc - og - ot : (c == 1 ? oc : (c == 2 ? og : ot));
+                k = sel4(c, S.L2[0], S.L2[1], S.L2[2], S.L2[3]) + n;
+            }
+            ++steps;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void sa_densify_chase_kernel(SaParams S, uint32_t dshift, uint64_t n_dense,
+                                                                const uint64_t* __restrict__ link,
+                                                                uint64_t* __restrict__ dense) {
+    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+    const uint32_t rshift = S.sa_shift - dshift;
+    const uint64_t smask = (1ull << rshift) - 1;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool live = i < n_dense;
+    uint64_t j = i, acc = 0;
+    while (__any(live)) {
+        if (live && (j & smask) == 0) {
+            dense[i] = acc + S.sa[j >> rshift];
+            i += lanes;
+            live = i < n_dense;
+            j = i;
+            acc = 0;
+        } else if (live) {
+            const uint64_t l = link[j];
+            acc += l >> 32;
+            j = (uint32_t)l;
+        }
+    }
+}
+
 }  // namespace smem
+
+// lane-strided passes: enough waves to fill the chip several times over
+static unsigned densify_grid(uint64_t n) {
+    const uint64_t want = (n + 255) / 256;
+    return (unsigned)(want < 256 * 64 ? (want ? want : 1) : 256 * 64);
+}
+
+extern "C" hipError_t smem_launch_sa_densify2(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense,
+                                              uint64_t* link, uint64_t* dense, hipStream_t st) {
+    if (n_dense == 0) return hipSuccess;
+    if (n_dense >= (1ull << 32) || dshift >= S->sa_shift) return hipErrorInvalidValue;
+    const unsigned grid = densify_grid(n_dense);
+    hipLaunchKernelGGL(smem::sa_densify_hop_kernel, dim3(grid), dim3(256), 0, st, *S, dshift, n_dense, link);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(smem::sa_densify_chase_kernel, dim3(grid), dim3(256), 0, st, *S, dshift, n_dense,
+                       (const uint64_t*)link, dense);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t smem_launch_sa_densify(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense,
                                              uint64_t* dense, hipStream_t st) {

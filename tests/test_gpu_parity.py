@@ -338,9 +338,12 @@ def test_sa_golden_fixture(gpu_device, tmp_path):
         gpu.close()
 
 
+@pytest.mark.parametrize("densify", ["hop", "walk"])
 @pytest.mark.parametrize("max_occ", [1, 20, 10000])
-def test_sa_vs_oracle(gpu_device, max_occ):
-    """Random genome with repeats, mixed reads: GPU positions == restated bwt_sa."""
+def test_sa_vs_oracle(gpu_device, max_occ, densify, monkeypatch):
+    """Random genome with repeats, mixed reads: GPU positions == restated bwt_sa
+    (the device SA densified by hop + chase passes, or by one walk per row)."""
+    monkeypatch.setenv("SMEM_GPU_DENSIFY", densify)
     import smemgpu
     from smemgpu import synth
     g = synth.make_genome(300_000, seed=41)
@@ -366,8 +369,10 @@ def test_sa_vs_oracle(gpu_device, max_occ):
         oidx.close()
 
 
-def test_sa_intervals_and_errors(gpu_device):
+@pytest.mark.parametrize("densify", ["hop", "walk"])
+def test_sa_intervals_and_errors(gpu_device, densify, monkeypatch):
     """Other sampling intervals; SA of another index rejected; sa before run rejected."""
+    monkeypatch.setenv("SMEM_GPU_DENSIFY", densify)
     import smemgpu
     from smemgpu import synth
     g = synth.make_genome(50_000, seed=45)

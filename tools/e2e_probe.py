@@ -1,7 +1,10 @@
 """Run the product path (bwa-gpu mem) on the bench's human-size index and reads
 with the stderr kept: per-batch GPU timings, refusals and their error text.
 
-    python tools/e2e_probe.py [--reads 200000] [--threads 16] [bench args]  (env passes through)
+    python tools/e2e_probe.py [--reads 200000] [--threads 16] [--legs gpu/ref] [bench args]  (env passes through)
+
+--legs: "gpu", "ref", or "gpu+VAR=v+VAR2=w" (a gpu leg with extra environment,
+e.g. gpu+SMEM_GPU_DENSIFY=walk); the SAM of every leg is compared with the first.
 """
 import argparse
 import hashlib
@@ -21,6 +24,7 @@ def main():
     p.add_argument("--reads", type=int, default=200_000)
     p.add_argument("--threads", type=int, default=16)
     p.add_argument("--out", default=None)
+    p.add_argument("--legs", default="gpu/ref")
     own, rest = p.parse_known_args()
     import torch
     torch.cuda.device_count()
@@ -42,19 +46,25 @@ def main():
         synth.write_fastq(fq, sub)
         batch = max(1024, -(-m // own.threads))
         print(f"[probe] {m} reads, -t {own.threads} -b {batch}", flush=True)
-        for name, cmd in (("gpu", [bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(batch), base, fq]),
-                          ("ref", [bench.REF_HARNESS, "mem", base, fq, str(own.threads), "1", "0"])):
+        legs = []
+        for leg in own.legs.split("/"):
+            name, *kv = leg.split("+")
+            env = dict(os.environ, SMEM_GPU_TIMES="1", **dict(x.split("=", 1) for x in kv))
+            cmd = ([bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(batch), base, fq] if name == "gpu" else
+                   [bench.REF_HARNESS, "mem", base, fq, str(own.threads), "1", "0"])
+            legs.append((leg, cmd, env))
+        for name, cmd, env in legs:
             t = time.time()
-            p2 = subprocess.run(cmd, capture_output=True, env=dict(os.environ, SMEM_GPU_TIMES="1"), timeout=900)
+            p2 = subprocess.run(cmd, capture_output=True, env=env, timeout=900)
             body = b"\n".join(l for l in p2.stdout.split(b"\n") if not l.startswith(b"@PG"))
             err = p2.stderr.decode(errors="replace")
             keep = [l for l in err.split("\n") if "mem_batch_gpu" in l or "[W::" in l or "[E::" in l or "rror" in l
-                    or "reserve_slots" in l or "mem_process_seqs" in l or "init_devices" in l
-                    or "main_mem" in l or "real sec" in l or "held" in l]
+                    or "smem_gpu" in l or "mem_process_seqs" in l or "main_mem" in l or "real sec" in l
+                    or "held" in l]
             nl = body.count(b"\n")
             print(f"== {name}: rc {p2.returncode}, {time.time() - t:.1f} s, sha {hashlib.sha256(body).hexdigest()[:16]}, "
                   f"{nl} lines", flush=True)
-            for l in keep[:60]:
+            for l in keep[:120]:
                 print("   ", l, flush=True)
             bodies[name] = body
             if own.out:
@@ -63,7 +73,10 @@ def main():
                     fh.write(body)
                 with open(os.path.join(own.out, name + ".err"), "w") as fh:
                     fh.write(err)
-    diff_summary(bodies.get("gpu", b""), bodies.get("ref", b""), batch)
+    first = legs[0][0]
+    for name, _, _ in legs[1:]:
+        print(f"== {first} vs {name}", flush=True)
+        diff_summary(bodies[first], bodies[name], batch)
 
 
 def diff_summary(gpu, ref, batch):
