@@ -657,12 +657,26 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     for (auto& f : g->reserve)
         if (f.valid()) f.wait();
     (void)hipSetDevice(g->device);
-    for (auto& kv : g->per_thread) smem_batch_destroy(kv.second);
+    const double t0 = now_s();
+    // the worker batches' device and pinned buffers, released on a few host
+    // threads (unpinning host pages dominates)
+    std::vector<smem_batch_t*> all;
+    for (auto& kv : g->per_thread) all.push_back(kv.second);
+    for (auto* b : g->slots) all.push_back(b);
+    for (auto* b : g->stream_pool) all.push_back(b);
     g->per_thread.clear();
-    for (auto* b : g->slots) smem_batch_destroy(b);
     g->slots.clear();
-    for (auto* b : g->stream_pool) smem_batch_destroy(b);
     g->stream_pool.clear();
+    {
+        const size_t nt = std::min<size_t>(all.size(), 8);
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < nt; ++t)
+            th.emplace_back([&all, t, nt]() {
+                for (size_t k = t; k < all.size(); k += nt) smem_batch_destroy(all[k]);
+            });
+        for (auto& x : th) x.join();
+    }
+    const double t1 = now_s();
     if (g->d_bwt) (void)hipFree(g->d_bwt);
     if (g->d_occ64) (void)hipFree(g->d_occ64);
     if (g->d_occ192) (void)hipFree(g->d_occ192);
@@ -677,6 +691,9 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     }
     if (g->sa_ready) (void)hipEventDestroy(g->sa_ready);
     if (g->init_st) (void)hipStreamDestroy(g->init_st);
+    if (getenv("SMEM_GPU_TIMES"))
+        fprintf(stderr, "[M::smem_gpu_shutdown] device %d: %zu batches released in %.4f s, index and streams in %.4f s\n",
+                g->device, all.size(), t1 - t0, now_s() - t1);
     delete g;
 }
 

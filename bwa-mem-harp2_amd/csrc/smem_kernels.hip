@@ -1821,8 +1821,9 @@ __global__ __launch_bounds__(256) void sa_densify_kernel(SaParams S, uint32_t ds
 //               n_dense * (sa_intv / D) * ~(D - 1).
 //   chase pass: dense[i] = the steps summed along the links up to a stored
 //               sample + that sample (unsigned, sa[0] = -1 wrapping as in
-//               software/bwt.c:110-113), sa_intv / D links on average, one
-//               8-B load each.
+//               software/bwt.c:110-113), one 8-B load per link; a finished
+//               row's link is replaced by its total (path compression), so
+//               chains that reach it later stop there.
 // Walks and chains differ in length across the lanes of a wave, so both
 // passes deal their rows lane-strided and a lane that finishes takes its
 // next row in the same loop (the sa_walk_kernel scheme).  Link targets need
@@ -1864,8 +1865,7 @@ __global__ __launch_bounds__(256) void sa_densify_hop_kernel(SaParams S, uint32_
 }
 
 __global__ __launch_bounds__(256) void sa_densify_chase_kernel(SaParams S, uint32_t dshift, uint64_t n_dense,
-                                                                const uint64_t* __restrict__ link,
-                                                                uint64_t* __restrict__ dense) {
+                                                                uint64_t* link, uint64_t* __restrict__ dense) {
     const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t rshift = S.sa_shift - dshift;
     const uint64_t smask = (1ull << rshift) - 1;
@@ -1875,6 +1875,11 @@ __global__ __launch_bounds__(256) void sa_densify_chase_kernel(SaParams S, uint3
     while (__any(live)) {
         if (live && (j & smask) == 0) {
             dense[i] = acc + S.sa[j >> rshift];
+            // path compression: a later chain through row i jumps straight to
+            // the sample (its link still says "acc steps to row j", the same
+            // walk).  Other lanes may read link[i] before or after this store
+            // (an aligned 8-B store, never torn), and either value is right.
+            if (acc) link[i] = j | acc << 32;
             i += lanes;
             live = i < n_dense;
             j = i;
@@ -1903,8 +1908,8 @@ extern "C" hipError_t smem_launch_sa_densify2(const smem::SaParams* S, uint32_t 
     hipLaunchKernelGGL(smem::sa_densify_hop_kernel, dim3(grid), dim3(256), 0, st, *S, dshift, n_dense, link);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(smem::sa_densify_chase_kernel, dim3(grid), dim3(256), 0, st, *S, dshift, n_dense,
-                       (const uint64_t*)link, dense);
+    hipLaunchKernelGGL(smem::sa_densify_chase_kernel, dim3(grid), dim3(256), 0, st, *S, dshift, n_dense, link,
+                       dense);
     return hipGetLastError();
 }
 

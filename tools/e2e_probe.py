@@ -4,7 +4,8 @@ with the stderr kept: per-batch GPU timings, refusals and their error text.
     python tools/e2e_probe.py [--reads 200000] [--threads 16] [--legs gpu/ref] [bench args]  (env passes through)
 
 --legs: "gpu", "ref", or "gpu+VAR=v+VAR2=w" (a gpu leg with extra environment,
-e.g. gpu+SMEM_GPU_DENSIFY=walk); the SAM of every leg is compared with the first.
+e.g. gpu+SMEM_GPU_DENSIFY=walk; gpu+B=<n> sets that leg's -b); the SAM of every
+leg is compared with the first.
 """
 import argparse
 import hashlib
@@ -25,6 +26,7 @@ def main():
     p.add_argument("--threads", type=int, default=16)
     p.add_argument("--out", default=None)
     p.add_argument("--legs", default="gpu/ref")
+    p.add_argument("--batch", type=int, default=0, help="bwa -b (default: reads / threads)")
     own, rest = p.parse_known_args()
     import torch
     torch.cuda.device_count()
@@ -44,13 +46,14 @@ def main():
     with tempfile.TemporaryDirectory(dir=a.cache) as d:
         fq = os.path.join(d, "r.fq")
         synth.write_fastq(fq, sub)
-        batch = max(1024, -(-m // own.threads))
+        batch = own.batch or max(1024, -(-m // own.threads))
         print(f"[probe] {m} reads, -t {own.threads} -b {batch}", flush=True)
         legs = []
         for leg in own.legs.split("/"):
             name, *kv = leg.split("+")
             env = dict(os.environ, SMEM_GPU_TIMES="1", **dict(x.split("=", 1) for x in kv))
-            cmd = ([bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(batch), base, fq] if name == "gpu" else
+            b = env.pop("B", batch)  # gpu+B=<n>: this leg's bwa -b
+            cmd = ([bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(b), base, fq] if name == "gpu" else
                    [bench.REF_HARNESS, "mem", base, fq, str(own.threads), "1", "0"])
             legs.append((leg, cmd, env))
         for name, cmd, env in legs:
