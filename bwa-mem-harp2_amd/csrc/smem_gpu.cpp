@@ -54,6 +54,8 @@ static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 static const double g_t_lib = now_s();  // the library's load (for a linked binary: its start)
+// SMEM_GPU_TIMES: time spent releasing batch buffers (device / pinned host) and their counts
+static std::atomic<int64_t> g_rel_dev_ns{0}, g_rel_host_ns{0}, g_rel_dev_n{0}, g_rel_host_n{0};
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     if (e != hipSuccess)
@@ -643,7 +645,15 @@ void smem_batch_destroy(smem_batch_t* b) {
     // (every call drained its work before returning: nothing of this batch
     // is in flight, and its streams belong to the device's admission pool)
     (void)hipSetDevice(b->g->device);
-    batch_bufs(b, [](auto& x) { x.release(); }, [](auto& x) { x.release(); });
+    const double t0 = now_s();
+    int nd = 0, nh = 0;
+    batch_bufs(b, [&nd](auto& x) { nd += x.p != nullptr; x.release(); }, [](auto&) {});
+    const double t1 = now_s();
+    batch_bufs(b, [](auto&) {}, [&nh](auto& x) { nh += x.p != nullptr; x.release(); });
+    g_rel_dev_ns += (int64_t)((t1 - t0) * 1e9);
+    g_rel_host_ns += (int64_t)((now_s() - t1) * 1e9);
+    g_rel_dev_n += nd;
+    g_rel_host_n += nh;
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
@@ -692,8 +702,10 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     if (g->sa_ready) (void)hipEventDestroy(g->sa_ready);
     if (g->init_st) (void)hipStreamDestroy(g->init_st);
     if (getenv("SMEM_GPU_TIMES"))
-        fprintf(stderr, "[M::smem_gpu_shutdown] device %d: %zu batches released in %.4f s, index and streams in %.4f s\n",
-                g->device, all.size(), t1 - t0, now_s() - t1);
+        fprintf(stderr, "[M::smem_gpu_shutdown] device %d: %zu batches released in %.4f s (thread-seconds: %lld device "
+                "buffers %.4f, %lld pinned %.4f), index and streams in %.4f s\n", g->device, all.size(), t1 - t0,
+                (long long)g_rel_dev_n.load(), g_rel_dev_ns.load() * 1e-9, (long long)g_rel_host_n.load(),
+                g_rel_host_ns.load() * 1e-9, now_s() - t1);
     delete g;
 }
 
