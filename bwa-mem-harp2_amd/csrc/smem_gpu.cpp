@@ -107,17 +107,47 @@ int inject_fault(int stage) {
         if (_e != hipSuccess) return fail(SMEM_E_DEVICE, #expr, _e);    \
     } while (0)
 
+// A worker slot's buffers carved from two blocks (device, pinned host)
+// instead of ~80 separate allocations: each hipFree / hipHostFree is a
+// driver round trip (~1 ms and ~3 ms each, profiles/r04/e2e), so releasing 16
+// slots one buffer at a time took 0.3 s of `bwa mem`'s exit.  Used by
+// smem_gpu_reserve_slots (the sizes are known there: a measuring pass
+// records them, then the blocks are allocated and the same calls carve);
+// buffers that grow later get their own allocation, as without.
+struct Arena {
+    bool measure = false;
+    char* base = nullptr;
+    size_t cap = 0, used = 0;
+    void* take(size_t bytes) {
+        const size_t at = (used + 255) & ~(size_t)255;
+        if (measure) {
+            used = at + bytes;
+            return reinterpret_cast<void*>((uintptr_t)256);  // never dereferenced, never freed
+        }
+        if (!base || at + bytes > cap) return nullptr;
+        used = at + bytes;
+        return base + at;
+    }
+};
+thread_local Arena* t_dev_arena = nullptr;
+thread_local Arena* t_host_arena = nullptr;
+
 template <class T>
 struct DevBuf {
     T* p = nullptr;
     size_t n = 0;
+    bool own = true;  // false: carved from the slot's block
     hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
-        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        release();
+        const size_t m = std::max<size_t>(want, 1);
+        if (t_dev_arena)
+            if (void* a = t_dev_arena->take(m * sizeof(T))) {
+                p = static_cast<T*>(a), n = m, own = false;
+                return hipSuccess;
+            }
+        hipError_t e = hipMalloc(&p, m * sizeof(T));
+        if (e == hipSuccess) n = m, own = true;
         return e;
     }
     // ensure() with 25 % headroom when it must reallocate: for scratch whose
@@ -128,9 +158,10 @@ struct DevBuf {
         return ensure(want + want / 4);
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && own) (void)hipFree(p);
         p = nullptr;
         n = 0;
+        own = true;
     }
     uint64_t bytes() const { return p ? (uint64_t)n * sizeof(T) : 0; }
 };
@@ -139,6 +170,7 @@ template <class T>
 struct HostBuf {
     T* p = nullptr;
     size_t n = 0;
+    bool own = true;
     // a pinned result buffer of at least `want` elements, grown with 25 %
     // headroom: batches of a worker vary in size, and re-pinning on every
     // slightly larger one costs more than the copy
@@ -148,17 +180,22 @@ struct HostBuf {
     }
     hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        n = 0;
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
-        if (e == hipSuccess) n = std::max<size_t>(want, 1);
+        release();
+        const size_t m = std::max<size_t>(want, 1);
+        if (t_host_arena)
+            if (void* a = t_host_arena->take(m * sizeof(T))) {
+                p = static_cast<T*>(a), n = m, own = false;
+                return hipSuccess;
+            }
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), m * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = m, own = true;
         return e;
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p && own) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
+        own = true;
     }
     uint64_t bytes() const { return p ? (uint64_t)n * sizeof(T) : 0; }
 };
@@ -271,6 +308,8 @@ struct AlnHeavyBufs {
 
 struct smem_batch {
     smem_gpu_t* g = nullptr;
+    char* arena_dev = nullptr;   // the blocks a reserved slot's buffers are carved from (Arena)
+    char* arena_host = nullptr;
     hipStream_t st = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // chains -> regions: the light reads' kernel runs on st2 beside the heavy
@@ -647,9 +686,11 @@ void smem_batch_destroy(smem_batch_t* b) {
     (void)hipSetDevice(b->g->device);
     const double t0 = now_s();
     int nd = 0, nh = 0;
-    batch_bufs(b, [&nd](auto& x) { nd += x.p != nullptr; x.release(); }, [](auto&) {});
+    batch_bufs(b, [&nd](auto& x) { nd += x.p && x.own; x.release(); }, [](auto&) {});
     const double t1 = now_s();
-    batch_bufs(b, [](auto&) {}, [&nh](auto& x) { nh += x.p != nullptr; x.release(); });
+    batch_bufs(b, [](auto&) {}, [&nh](auto& x) { nh += x.p && x.own; x.release(); });
+    if (b->arena_dev) (void)hipFree(b->arena_dev), ++nd;
+    if (b->arena_host) (void)hipHostFree(b->arena_host), ++nh;
     g_rel_dev_ns += (int64_t)((t1 - t0) * 1e9);
     g_rel_host_ns += (int64_t)((now_s() - t1) * 1e9);
     g_rel_dev_n += nd;
@@ -2385,6 +2426,10 @@ static int batch_prealloc(smem_batch_t* b) {
     HIP_TRY(H.heavy.grow(R));
     HIP_TRY(H.hcnt.grow(R));
     HIP_TRY(H.hscnt.grow(R));
+    HIP_TRY(H.hoff.grow(R + 1));
+    HIP_TRY(H.rnext.grow(ns));
+    HIP_TRY(H.ht.grow((size_t)b->g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+    HIP_TRY(b->d_aln_out.grow(R * 4));
     HIP_TRY(b->h_aln_regoff.grow(R + 1));
     HIP_TRY(b->h_aln_regs.grow(R * 4));  // pinned: the regions fetched (~3 per read)
     if (!b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
@@ -2500,10 +2545,37 @@ int smem_gpu_reserve_slots(smem_gpu_t* g, int n_slots, int reads_per_slot, int m
             g_no_inject = 1;
             if (hipSetDevice(g->device) != hipSuccess) return SMEM_E_DEVICE;
             const auto t0 = std::chrono::steady_clock::now();
+            const uint64_t bases = (uint64_t)reads_per_slot * (uint64_t)max_len;
+            // the slot's buffers from two blocks (Arena): the same calls once
+            // to measure, then to carve (SMEM_GPU_ARENA=0: one allocation each)
+            Arena ad, ah;
+            const char* av = getenv("SMEM_GPU_ARENA");
+            if (!(av && atoi(av) == 0)) {
+                Arena md, mh;
+                md.measure = mh.measure = true;
+                t_dev_arena = &md, t_host_arena = &mh;
+                smem_batch_t* m = nullptr;
+                int r = smem_batch_create(g, reads_per_slot, bases, max_len, &m);
+                if (r == SMEM_OK) r = batch_prealloc(m);
+                t_dev_arena = t_host_arena = nullptr;
+                if (m) smem_batch_destroy(m);
+                if (r == SMEM_OK && hipMalloc(&ad.base, md.used) == hipSuccess) ad.cap = md.used;
+                if (r == SMEM_OK && hipHostMalloc(reinterpret_cast<void**>(&ah.base), mh.used, hipHostMallocDefault) ==
+                                        hipSuccess)
+                    ah.cap = mh.used;
+                t_dev_arena = ad.base ? &ad : nullptr, t_host_arena = ah.base ? &ah : nullptr;
+            }
             smem_batch_t* b = nullptr;
-            int rc = smem_batch_create(g, reads_per_slot, (uint64_t)reads_per_slot * (uint64_t)max_len, max_len, &b);
+            int rc = smem_batch_create(g, reads_per_slot, bases, max_len, &b);
             const auto t1 = std::chrono::steady_clock::now();
             if (rc == SMEM_OK) rc = batch_prealloc(b);
+            t_dev_arena = t_host_arena = nullptr;
+            if (b) {
+                b->arena_dev = ad.base, b->arena_host = ah.base;
+            } else {  // smem_batch_create failed and released what it carved
+                if (ad.base) (void)hipFree(ad.base);
+                if (ah.base) (void)hipHostFree(ah.base);
+            }
             const auto t2 = std::chrono::steady_clock::now();
             if (rc == SMEM_OK && k == 0) rc = batch_warmup(b);
             if (getenv("SMEM_GPU_TIMES")) {  // diagnostics, as the binding's per-batch times
