@@ -965,6 +965,8 @@ def main():
     d = Dist()
     rank, world = d.rank, d.world
     barrier = d.barrier
+    if world > 1:  # the CPU baseline is an N=1 record (rank 0); N>1 lines carry null
+        args.cpu_seconds = 0.0
 
     idx, idx_path, sa, genome_codes = get_index(args, rank, barrier, d.gpu)
     reads = make_reads(args, rank, genome_codes, world)
