@@ -1,6 +1,6 @@
 """End-to-end parity of the reference-side binding (integration/): the
 reference's own `bwa` CLI with the maintainer's patch applied
-(integration/patches: main.c, bwa.c, fastmap.c, bwamem.c) and linked to
+(integration/patches: main.c, bwa.c, fastmap.c, bwamem.c, bwtindex.c) and linked to
 libsmemgpu.so, built by integration/Makefile into oracle/_ref/bwa-gpu.
 
 Golden: tests/golden/sam/*.sam.gz, the unpatched reference pipeline's SAM
@@ -50,9 +50,53 @@ def indexed(tmp_path_factory, built):
         fa = d / f"{g}.fa"
         with gzip.open(os.path.join(GOLD, f"{g}.fa.gz"), "rb") as src, open(fa, "wb") as dst:
             shutil.copyfileobj(src, dst)
-        subprocess.run([BWA, "index", "-a", "is", str(fa)], check=True, capture_output=True, cwd=d)
+        # the reference's CPU steps (the GPU build of `bwa index` is tested
+        # against them below)
+        subprocess.run([BWA, "index", "-a", "is", str(fa)], check=True, capture_output=True, cwd=d,
+                       env=dict(os.environ, SMEM_GPU_INDEX="0"))
         out[g] = str(fa)
     return out
+
+
+INDEX_FILES = (".bwt", ".sa", ".pac", ".ann", ".amb")
+
+
+def _index_files(tmp, g, name, algo, env):
+    """`bwa-gpu index [-a algo] -p <name>` of golden genome g in tmp -> (stderr, {suffix: bytes})."""
+    fa = tmp / f"{g}.fa"
+    if not fa.exists():
+        with gzip.open(os.path.join(GOLD, f"{g}.fa.gz"), "rb") as src, open(fa, "wb") as dst:
+            shutil.copyfileobj(src, dst)
+    args = [BWA, "index"] + (["-a", algo] if algo else []) + ["-p", str(tmp / name), str(fa)]
+    p = subprocess.run(args, capture_output=True, text=True, cwd=tmp, env=dict(os.environ, **env), timeout=900)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return p.stderr, {x: open(tmp / (name + x), "rb").read() for x in INDEX_FILES}
+
+
+def test_index_without_gpu_runs_the_reference_steps(tmp_path, built):
+    """`bwa index` with no usable device (device 63: refused): the reference's
+    CPU steps, announced, and the same files as with SMEM_GPU_INDEX=0."""
+    _need_bwa()
+    err, files = _index_files(tmp_path, "g1", "cpu", "is", {"SMEM_GPU_DEVICES": "63"})
+    assert "the CPU builds the BWT and the SA" in err and "Update BWT" in err, err[-2000:]
+    err0, ref = _index_files(tmp_path, "g1", "ref", "is", {"SMEM_GPU_INDEX": "0"})
+    assert "Construct BWT and SA on GPU" not in err0
+    assert files == ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("g", ["g1", "g2"])
+@pytest.mark.parametrize("algo", ["is", None])
+def test_gpu_index_files_identical(tmp_path, gpu_device, built, g, algo):
+    """`bwa index` on the MI355X (smem_bwt_build_gpu_sa in place of the BWT
+    construction, bwt_bwtupdate_core and bwt_cal_sa): all five index files
+    byte-identical to the reference's CPU steps."""
+    _need_bwa()
+    err, got = _index_files(tmp_path, g, "gpu", algo, {})
+    assert "Construct BWT and SA on GPU" in err and "Update BWT" not in err, err[-2000:]
+    _, want = _index_files(tmp_path, g, "cpu", algo, {"SMEM_GPU_INDEX": "0"})
+    for x in INDEX_FILES:
+        assert got[x] == want[x], x
 
 
 def _golden(g, kind) -> list:

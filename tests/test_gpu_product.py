@@ -224,3 +224,88 @@ def test_init_devices_two_contexts(world):
     rc = lib.smem_gpu_init_devices(hs, 2, bad, words.ctypes.data, words.size, idx.primary, L2, None, None, 0)
     assert rc != 0 and not hs[0] and not hs[1]
     assert b"device 4095" in lib.smem_strerror(rc)
+
+
+def _slot_run(lib, gpu, t, reads, lo, hi):
+    """One worker batch through every stage on slot t, as mem_batch_gpu runs it:
+    (seeding lists as SMGO, the regions' bytes, their per-read offsets)."""
+    import smemgpu
+    from smemgpu.lib import _results_of
+    rc, bh, keep = _collect(lib, gpu._h, t, reads, lo, hi, flags=smemgpu.lib.COLLECT_NO_FETCH)
+    assert rc == 0, smemgpu.lib.ERRORS.get(rc, rc)
+    assert lib.smem_batch_sa(bh, 19, 500) == 0
+    co = smemgpu.lib.ChainOptT(100, 10000, 0.5, 0.5, 1)
+    assert lib.smem_batch_chain(bh, int(gpu._l_pac), C.byref(co)) == 0
+    opt = smemgpu.aln_opt()
+    assert lib.smem_batch_chain2aln(bh, C.byref(opt)) == 0
+    assert lib.smem_batch_fetch(bh) == 0
+    smgo = _results_of(lib, bh, hi - lo).to_smgo()
+    rg, ro, nr = C.c_void_p(), C.POINTER(C.c_uint64)(), C.c_uint64()
+    assert lib.smem_batch_aln_results(bh, C.byref(rg), C.byref(ro), C.byref(nr)) == 0
+    n = int(nr.value)
+    regs = np.frombuffer((C.c_char * (max(n, 1) * 64)).from_address(rg.value), dtype=np.uint8)[:n * 64].copy()
+    return smgo, regs, np.ctypeslib.as_array(ro, shape=(hi - lo + 1,)).copy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arena", ["1", "0"])
+def test_reserved_slots_every_stage(world, monkeypatch, arena):
+    """smem_gpu_reserve_slots (what the patched main_mem calls for -t / -b):
+    every slot's buffers carved from one device and one pinned block
+    (SMEM_GPU_ARENA=1, the default) or allocated one by one (0), slot 0's
+    warm-up over reads cut from the resident .pac.  Four threads then run
+    worker batches on their slots through every stage, some larger than the
+    reservation (such a slot's batch is re-created at its size): seeding lists
+    equal the oracle's, regions equal those of an unreserved handle's batches."""
+    import smemgpu
+    from smemgpu import synth
+    monkeypatch.setenv("SMEM_GPU_ARENA", arena)
+    lib = _lib()
+    g, reads = world["g"], world["reads"]
+    pac = _pack(g.codes)
+
+    def open_gpu():
+        gpu = smemgpu.Gpu(world["idx"], device=0)
+        gpu.load_sa(world["sa"])
+        gpu.load_pac(pac, g.codes.size)
+        gpu._l_pac = g.codes.size
+        return gpu
+
+    bounds, a, k = [], 0, 0
+    while a < reads.n:  # 350- and 450-read batches: the larger outgrow the 400-read slots
+        b = min(a + (350, 450)[k % 2], reads.n)
+        bounds.append((a, b))
+        a, k = b, k + 1
+    ref = open_gpu()  # no reservation: every slot created on first use
+    try:
+        want = {lo: _slot_run(lib, ref, 0, reads, lo, hi) for lo, hi in bounds}
+    finally:
+        ref.close()
+    gpu = open_gpu()
+    try:
+        gpu.reserve_slots(4, 400, 300)
+        got, errs = {}, []
+
+        def worker(t):
+            try:
+                for k in range(t, len(bounds), 4):
+                    lo, hi = bounds[k]
+                    got[lo] = _slot_run(lib, gpu, t, reads, lo, hi)
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs[0]
+        recs = []
+        for lo, hi in bounds:
+            recs.extend(synth.read_smgo(got[lo][0]))
+            assert np.array_equal(got[lo][1], want[lo][1]) and np.array_equal(got[lo][2], want[lo][2]), lo
+        _same_reads(recs, synth.read_smgo(world["want"]))
+        m = gpu.memory()
+        assert m["batches"] == 4 and m["batch_device_bytes"] > 0 and m["batch_pinned_bytes"] > 0, m
+    finally:
+        gpu.close()
