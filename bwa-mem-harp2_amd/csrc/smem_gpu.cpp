@@ -2375,6 +2375,8 @@ static int collect_batch(smem_gpu_t* g, int slot, int n_reads, int max_len, uint
 // and hipFree waits for the whole device).  A batch that needs more grows as
 // before.  (Generous estimates cost at shutdown: 16 slots of 62.5k reads at
 // 48 / 24 / 8 / 16 per read held 38.6 GB and took 0.43 s to free.)
+// (no device work here or in smem_batch_create: smem_gpu_reserve_slots runs
+// both once with a measuring Arena, whose buffers are placeholders)
 static int batch_prealloc(smem_batch_t* b) {
     const uint64_t R = (uint64_t)b->max_reads;
     const uint64_t ni = R * 40, no = R * 16, nc = R * 6, ns = R * 12;
