@@ -203,3 +203,61 @@ def test_bwa_prefix_from_smem_index_matches_bwa_index(tmp_path, built):
     synth.write_bwa_bns(mine, g.codes, n_contigs=5)
     for ext in (".bwt", ".sa", ".pac", ".ann", ".amb"):
         assert open(mine + ext, "rb").read() == open(str(fa) + ext, "rb").read(), ext
+
+
+@pytest.fixture(scope="module")
+def two_chunks(indexed, tmp_path_factory):
+    """75k x 150 bp reads of g1 (11.25 M bases: two `bwa mem -t 1` chunks of
+    10 M bases) and the compiled reference's SAM of them (ref_harness mem,
+    the reference's sequential chunk loop)."""
+    import numpy as np
+    from smemgpu import synth
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(ref):
+        pytest.fail("oracle/_ref/ref_harness missing (built by __graft_entry__.build() where /root/reference exists)")
+    fa = indexed["g1"]
+    seq = []
+    with open(fa, "rb") as fh:
+        for line in fh:
+            if not line.startswith(b">"):
+                seq.append(line.strip())
+    codes = synth.NT4[np.frombuffer(b"".join(seq), dtype=np.uint8)]
+    r = synth.make_reads(codes, 75_000, 150, seed=77, sub_rate=0.02, n_rate=0.001, random_frac=0.02)
+    fq = tmp_path_factory.mktemp("chunks") / "r.fq"
+    acgtn = np.frombuffer(b"ACGTN", dtype=np.uint8)
+    with open(fq, "wb") as fh:
+        for i in range(r.n):
+            s = acgtn[np.minimum(r.read(i), 4)].tobytes()
+            fh.write(b"@c%d\n" % i + s + b"\n+\n" + b"I" * len(s) + b"\n")
+    p = subprocess.run([ref, "mem", fa, str(fq), "1", "1", "0"], capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return fa, str(fq), [l for l in p.stdout.split("\n") if l and not l.startswith("@PG")]
+
+
+def _run_chunks(fa, fq, env):
+    q = subprocess.run([BWA, "mem", "-t", "1", fa, fq], capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, **env))
+    assert q.returncode == 0, q.stderr[-2000:]
+    assert q.stderr.count("[M::main_mem] read ") == 2, q.stderr[-2000:]
+    return [l for l in q.stdout.split("\n") if l and not l.startswith("@PG")], q.stderr
+
+
+def test_pipelined_chunks_sam_identical(two_chunks):
+    """The patched main_mem's chunk pipeline (a reader thread parsing chunk
+    k+1, a writer printing chunk k-1 while chunk k is processed) on the CPU
+    path: SAM equal to the reference's sequential loop over two chunks."""
+    fa, fq, want = two_chunks
+    got, _ = _run_chunks(fa, fq, {"SMEM_GPU_DEVICES": "63"})
+    _same(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_pipelined_chunks_sam_identical(two_chunks, gpu_device):
+    """The same two chunks with the GPU stages (and the SE SAM beside them)
+    under the chunk pipeline, and with SMEM_GPU_PIPELINE=0: both equal the
+    reference's SAM."""
+    fa, fq, want = two_chunks
+    for env in ({}, {"SMEM_GPU_PIPELINE": "0"}):
+        got, err = _run_chunks(fa, fq, env)
+        assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
+        _same(got, want)
