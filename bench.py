@@ -124,6 +124,8 @@ def parse(argv=None):
     p.add_argument("--e2e-pairs", type=int, default=250_000,
                    help="e2e: also this many interleaved pairs through bwa-gpu mem -p vs the reference (0: skip)")
     p.add_argument("--e2e-batch", type=int, default=0, help="-b of bwa-gpu mem (0: reads / threads)")
+    p.add_argument("--e2e-chunk-reads", type=int, default=3_200_000,
+                   help="e2e.multi_chunk: this many SE reads (several bwa mem chunks of 10 Mbp x threads; 0: off)")
     p.add_argument("--human-like", type=int, default=1,
                    help="1: also measure the seeding step on the human-like genome profile (N=1 only)")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
@@ -713,6 +715,33 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
     return out
 
 
+def e2e_chunks_report(args, base: str, reads, threads: int, gpu: int) -> dict:
+    """The product path over several `bwa mem` chunks (10 Mbp x threads each,
+    software/fastmap.c:213): steady-state throughput with the patched chunk
+    pipeline (the next chunk parsed and the last one printed while a chunk is
+    processed), against the reference's sequential loop on the same reads."""
+    from smemgpu import synth
+    m = reads.n
+    batch = args.e2e_batch or 62500
+    out = {"reads": m, "read_len": args.read_len, "threads": threads, "batch": batch,
+           "what": "bwa-gpu mem vs the unpatched reference pipeline over several chunks of 10 Mbp x threads: "
+                   "wall clock, and the reference's mem_process_seqs real time summed over the chunks"}
+    with tempfile.TemporaryDirectory(dir=args.cache) as d:
+        fq = os.path.join(d, "c.fq")
+        synth.write_fastq(fq, reads, prefix="c")
+        env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu), SMEM_GPU_TIMES="1")
+        legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq], {}),
+                ("reference", [REF_HARNESS, "mem", base, fq, str(threads), "1", "0"], {})]
+        runs = _e2e_legs(d, legs, env_base, m, tag="chunks ")
+        if runs is None:
+            return dict(out, error="a leg failed (see the bench log)")
+        out.update(runs)
+        out["sam_identical"] = runs["gpu"]["sam_sha256"] == runs["reference"]["sam_sha256"]
+        out.update(_e2e_speedups(runs))
+        out["reads_per_s_wall"] = {k: round(m / runs[k]["wall_s"], 1) for k in ("gpu", "reference")}
+    return out
+
+
 def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | None:
     """Run each (name, argv, env) leg with its SAM into d; wall clock, the
     reference's own mem_process_seqs real time, SAM digest (minus @PG)."""
@@ -1073,6 +1102,10 @@ def main():
     if rank == 0 and world == 1:
         if args.e2e_reads > 0:
             out["e2e"] = e2e_report(args, genome_key(args), genome_codes, reads, cores, d.gpu)
+            if out["e2e"] is not None and args.e2e_chunk_reads > 0:
+                creads = make_reads(args, 0, genome_codes, 1, args.e2e_chunk_reads, salt=2)
+                out["e2e"]["multi_chunk"] = e2e_chunks_report(args, genome_key(args), creads, cores, d.gpu)
+                del creads
         if args.human_like and args.genome_profile == "uniform":
             del idx, sa
             out["human_like"] = human_like_report(args, d, cores)
