@@ -84,6 +84,20 @@ def test_index_without_gpu_runs_the_reference_steps(tmp_path, built):
     assert files == ref
 
 
+@pytest.mark.parametrize("g", ["g1", "g2"])
+def test_index_host_builder_glue(tmp_path, built, g):
+    """The patched `bwa index` glue (the forward strand read back from the
+    .pac, the .bwt / .sa written in the reference's formats) run with the
+    library's host builder (SMEM_GPU_INDEX=host): five files identical to the
+    reference's CPU steps'."""
+    _need_bwa()
+    err, got = _index_files(tmp_path, g, "host", "is", {"SMEM_GPU_INDEX": "host"})
+    assert "host builder" in err and "Update BWT" not in err, err[-2000:]
+    _, want = _index_files(tmp_path, g, "cpu", "is", {"SMEM_GPU_INDEX": "0"})
+    for x in INDEX_FILES:
+        assert got[x] == want[x], x
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("g", ["g1", "g2"])
 @pytest.mark.parametrize("algo", ["is", None])
