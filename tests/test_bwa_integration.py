@@ -275,3 +275,27 @@ def test_gpu_pipelined_chunks_sam_identical(two_chunks, gpu_device):
         got, err = _run_chunks(fa, fq, env)
         assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
         _same(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("g", ["g1", "g2"])
+def test_gpu_pe_given_insert_sam_identical(indexed, gpu_device, g):
+    """`bwa mem -p -I 500,50`: with the insert size given, the PE SAM of each
+    pair is computed as soon as both mates' regions are back (no mem_pestat
+    over the chunk); SAM equal to the same binary's reference CPU path and to
+    its two-pass GPU run (SMEM_GPU_OVERLAP=0)."""
+    _need_bwa()
+    args = [BWA, "mem", "-t", "4", "-b", "256", "-p", "-I", "500,50", indexed[g],
+            os.path.join(GOLD, "sam", f"{g}_pe.fq.gz")]
+
+    def run(env):
+        p = subprocess.run(args, capture_output=True, text=True, env=dict(os.environ, **env), timeout=600)
+        assert p.returncode == 0, p.stderr[-2000:]
+        return [l for l in p.stdout.split("\n") if l and not l.startswith("@PG")], p.stderr
+
+    want, err = run({"SMEM_GPU_DEVICES": "63"})
+    assert "seeding on the CPU" in err
+    for env in ({}, {"SMEM_GPU_OVERLAP": "0"}):
+        got, err = run(env)
+        assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
+        _same(got, want)
