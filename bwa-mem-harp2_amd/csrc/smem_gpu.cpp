@@ -2794,8 +2794,20 @@ int smem_gpu_init_devices_async(smem_gpu_t** gpus, int n, const int* devices, co
 int smem_gpu_wait_ready(smem_gpu_t* g) {
     g_err[0] = 0;
     if (!g) return fail(SMEM_E_ARG, "smem_gpu_wait_ready");
-    gpu_wait(g);
-    return gpu_check(g);
+    gpu_wait(g);  // the upload chain
+    std::vector<std::shared_future<int>> res;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        res = g->reserve;
+    }
+    for (auto& f : res)  // the worker slots being sized (smem_gpu_reserve_slots)
+        if (f.valid()) f.wait();
+    if (int r = gpu_check(g)) return r;
+    if (g->sa_ready) {  // the .sa densification on the init stream
+        HIP_TRY(hipSetDevice(g->device));
+        HIP_TRY(hipEventSynchronize(g->sa_ready));
+    }
+    return SMEM_OK;
 }
 
 }  // extern "C"

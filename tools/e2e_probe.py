@@ -33,6 +33,7 @@ def main():
     import bench
     from smemgpu import synth
     a = bench.parse(rest)
+    a.reads = max(a.reads, own.reads)  # --reads past the bench's 1M: more chunks
     idx, _, sa, codes = bench.get_index(a, 0, lambda: None, 0)
     reads = bench.make_reads(a, 0, codes, 1)
     base = bench.genome_key(a)
