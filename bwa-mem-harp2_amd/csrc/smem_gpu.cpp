@@ -261,7 +261,8 @@ struct smem_gpu {
     // worker slots' pre-sized batches (a host thread)
     hipStream_t init_st = nullptr;
     hipEvent_t sa_ready = nullptr;
-    uint64_t* d_sa_raw = nullptr;  // the .sa as uploaded, freed once sa_ready has passed
+    uint64_t* d_sa_raw = nullptr;  // the .sa as uploaded (kept: the lookups use it until sa_ready has passed)
+    uint32_t sa_shift_raw = 0;
     std::vector<std::shared_future<int>> reserve;  // smem_gpu_reserve_slots: one per slot
     // smem_gpu_init_devices_async: the upload running on a host thread; every
     // entry point that touches the device waits for it (gpu_wait)
@@ -1175,9 +1176,8 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
         S.sa_shift = g->sa_shift;
         // in the background, on the device's init stream: the caller goes on
         // (bwa mem reads its first chunk of reads, the first batches seed)
-        // while the densification runs (~0.7 s at human size); smem_batch_sa
-        // waits for sa_ready on the device, and the uploaded samples are
-        // freed once it has passed
+        // while the densification runs; until sa_ready has passed,
+        // smem_batch_sa walks to the uploaded samples (kept until shutdown)
         if (!g->init_st) e = hipStreamCreateWithFlags(&g->init_st, hipStreamNonBlocking);
         if (e == hipSuccess && !g->sa_ready) e = hipEventCreateWithFlags(&g->sa_ready, hipEventDisableTiming);
         if (e == hipSuccess) e = hipMemsetAsync(dense + n_dense, 0, sizeof(uint64_t), g->init_st);
@@ -1209,6 +1209,7 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
             return fail(SMEM_E_DEVICE, "smem_gpu_load_sa: densify", e);
         }
         g->d_sa_raw = g->d_sa;
+        g->sa_shift_raw = g->sa_shift;
         g->d_sa = dense;
         g->n_sa = n_dense;
         g->sa_shift = dshift;
@@ -1227,8 +1228,22 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     b->sa_ran = b->chain_ran = b->aln_ran = false;
     b->sa_fetched = b->chain_fetched = b->aln_fetched = false;
     // the densified SA may still be in the making (smem_gpu_load_sa runs it
-    // in the background): the walk waits for it on the device
-    if (g->sa_ready) HIP_TRY(hipStreamWaitEvent(b->st, g->sa_ready, 0));
+    // in the background): until its event has passed, the walk goes to the
+    // stored samples instead (the same positions, sa_intv / D times the LF
+    // steps), so no batch waits for it.  SMEM_GPU_SA_RAW=1: always the
+    // stored samples (tests).
+    const uint64_t* sa_rows = g->d_sa;
+    uint32_t sa_shift = g->sa_shift;
+    if (g->d_sa_raw) {
+        const char* rv = getenv("SMEM_GPU_SA_RAW");
+        hipError_t q = (rv && atoi(rv)) ? hipErrorNotReady : hipEventQuery(g->sa_ready);
+        if (q == hipErrorNotReady) {
+            sa_rows = g->d_sa_raw;
+            sa_shift = g->sa_shift_raw;
+        } else if (q != hipSuccess) {
+            return fail(SMEM_E_DEVICE, "smem_batch_sa: densification", q);
+        }
+    }
     const uint64_t ni = b->tot_intv;
     if (ni >= (1ull << 31)) return fail(SMEM_E_CAPACITY, "smem_batch_sa: too many intervals");
     HIP_TRY(b->d_occ_n.grow(ni));
@@ -1241,8 +1256,8 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
     S.occ64 = g->d_occ64;
     S.primary = g->primary;
     std::memcpy(S.L2, g->L2, sizeof(S.L2));
-    S.sa = g->d_sa;
-    S.sa_shift = g->sa_shift;
+    S.sa = sa_rows;
+    S.sa_shift = sa_shift;
     S.intv = b->d_flat_intv.p;
     S.n_intv = ni;
     S.min_seed_len = min_seed_len;
@@ -2802,12 +2817,9 @@ int smem_gpu_wait_ready(smem_gpu_t* g) {
     }
     for (auto& f : res)  // the worker slots being sized (smem_gpu_reserve_slots)
         if (f.valid()) f.wait();
-    if (int r = gpu_check(g)) return r;
-    if (g->sa_ready) {  // the .sa densification on the init stream
-        HIP_TRY(hipSetDevice(g->device));
-        HIP_TRY(hipEventSynchronize(g->sa_ready));
-    }
-    return SMEM_OK;
+    // (the .sa densification may still run: smem_batch_sa uses the stored
+    // samples until it has finished)
+    return gpu_check(g);
 }
 
 }  // extern "C"

@@ -157,8 +157,9 @@ int  smem_gpu_init_devices(smem_gpu_t **gpus, int n, const int *devices, const u
 int  smem_gpu_init_devices_async(smem_gpu_t **gpus, int n, const int *devices, const uint32_t *bwt, uint64_t bwt_size,
                                  uint64_t primary, const uint64_t L2[5], const smem_sa_t *sa, const uint8_t *pac,
                                  int64_t l_pac);
-/* Waits until the device is ready for worker batches: the upload chain, the
- * .sa densification and any smem_gpu_reserve_slots sizing have finished. */
+/* Waits until the device is ready for worker batches: the upload chain and
+ * any smem_gpu_reserve_slots sizing have finished (the .sa densification may
+ * still be running: the SA lookups use the stored samples until it is done). */
 int  smem_gpu_wait_ready(smem_gpu_t *gpu);
 /* The steps of smem_gpu_init_devices_async one by one, so that each starts
  * as soon as its input is in memory (bwa_idx_load reads .bwt, then .sa, then
@@ -317,10 +318,12 @@ int  smem_batch_results_packed(const smem_batch_t *b, const smem_pintv_t **pintv
  * reference's bwt->sa array as is).  The device copy is densified to every
  * 4th row by LF walks from these samples (8 B per 4 symbols of HBM); lookups
  * return exactly what bwt_sa does with the .sa's own interval.  The
- * densification runs in the background (~0.7 s at human size): the call
- * returns after the upload, and smem_batch_sa waits for it on the device
- * (SMEM_GPU_SYNC_INIT=1: wait here).  The uploaded samples stay resident
- * beside the dense copy until smem_gpu_shutdown. */
+ * densification runs in the background (~0.3 s at human size): the call
+ * returns after the upload, and until the densification has finished
+ * smem_batch_sa walks to the uploaded samples instead (the same positions,
+ * more LF steps), so no batch waits for it (SMEM_GPU_SYNC_INIT=1: wait here;
+ * SMEM_GPU_SA_RAW=1: always the uploaded samples).  The uploaded samples stay
+ * resident beside the dense copy until smem_gpu_shutdown. */
 int  smem_gpu_load_sa(smem_gpu_t *gpu, const smem_sa_t *sa);
 /* After smem_batch_run: bwt_sa (software/bwt.c:104-114) of every seed
  * occurrence mem_insert_seed() generates from the lists — each interval with

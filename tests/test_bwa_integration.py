@@ -145,6 +145,7 @@ GPU_MODES = {
     "regions": {},                             # default: seeding -> regions on the GPU
     "chains": {"SMEM_GPU_STAGES": "1"},        # seeding -> chains on the GPU (round-2 binding)
     "two_ctx": {"SMEM_GPU_DEVICES": "0,0"},    # two device contexts, workers dealt tid % 2
+    "sa_raw": {"SMEM_GPU_SA_RAW": "1"},        # SA lookups to the uploaded samples (as before the densification ends)
 }
 
 

@@ -338,12 +338,17 @@ def test_sa_golden_fixture(gpu_device, tmp_path):
         gpu.close()
 
 
-@pytest.mark.parametrize("densify", ["hop", "walk"])
+@pytest.mark.parametrize("densify", ["hop", "walk", "raw"])
 @pytest.mark.parametrize("max_occ", [1, 20, 10000])
 def test_sa_vs_oracle(gpu_device, max_occ, densify, monkeypatch):
     """Random genome with repeats, mixed reads: GPU positions == restated bwt_sa
-    (the device SA densified by hop + chase passes, or by one walk per row)."""
-    monkeypatch.setenv("SMEM_GPU_DENSIFY", densify)
+    (the device SA densified by hop + chase passes, or by one walk per row, or
+    the walk to the uploaded samples -- what the lookups use while the
+    densification still runs)."""
+    if densify == "raw":
+        monkeypatch.setenv("SMEM_GPU_SA_RAW", "1")
+    else:
+        monkeypatch.setenv("SMEM_GPU_DENSIFY", densify)
     import smemgpu
     from smemgpu import synth
     g = synth.make_genome(300_000, seed=41)
@@ -369,10 +374,13 @@ def test_sa_vs_oracle(gpu_device, max_occ, densify, monkeypatch):
         oidx.close()
 
 
-@pytest.mark.parametrize("densify", ["hop", "walk"])
+@pytest.mark.parametrize("densify", ["hop", "walk", "raw"])
 def test_sa_intervals_and_errors(gpu_device, densify, monkeypatch):
     """Other sampling intervals; SA of another index rejected; sa before run rejected."""
-    monkeypatch.setenv("SMEM_GPU_DENSIFY", densify)
+    if densify == "raw":
+        monkeypatch.setenv("SMEM_GPU_SA_RAW", "1")
+    else:
+        monkeypatch.setenv("SMEM_GPU_DENSIFY", densify)
     import smemgpu
     from smemgpu import synth
     g = synth.make_genome(50_000, seed=45)
