@@ -1712,9 +1712,11 @@ static uint32_t aln_heavy_min() {
     const char* e = getenv("SMEM_ALN_HEAVY_MIN");
     return e ? (uint32_t)atoi(e) : 17u;
 }
+// (seeds: 16 since round 4 -- human-like 71.8 -> 70.5 ms per 1M reads,
+// uniform 29.0 -> 28.9; 8-48 swept, profiles/r04/aln/heavy_seeds_sweep.txt)
 static uint32_t aln_heavy_seeds() {
     const char* e = getenv("SMEM_ALN_HEAVY_SEEDS");
-    return e ? (uint32_t)atoi(e) : 48u;
+    return e ? (uint32_t)atoi(e) : 16u;
 }
 // SMEM_ALN_CAND=0: the heavy walk without the candidate index (the bin hash
 // of the regions made so far, as before it)
