@@ -1678,3 +1678,9 @@ extern "C" hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_
     hipLaunchKernelGGL(smem::aln_write_kernel, dim3((P->n_reads + 255) / 256), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
+
+// this file's code object loaded on the current device (see smem_preload_seed)
+extern "C" hipError_t smem_preload_aln(void) {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&smem::aln_classify_kernel));
+}

@@ -2136,3 +2136,9 @@ extern "C" hipError_t smem_launch_chain_write(const smem::ChainParams* P, int n_
     hipLaunchKernelGGL(smem::chain_write_heavy_kernel, dim3(n_cu * 4), dim3(64), 0, st, *P);
     return hipGetLastError();
 }
+
+// this file's code object loaded on the current device (see smem_preload_seed)
+extern "C" hipError_t smem_preload_chain(void) {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&smem::chain_write_kernel));
+}

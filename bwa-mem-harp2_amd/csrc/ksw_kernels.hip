@@ -263,3 +263,9 @@ extern "C" hipError_t smem_launch_ksw(const smem::KswParams* K, int n_cu, hipStr
     hipLaunchKernelGGL(smem::ksw_extend_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, *K);
     return hipGetLastError();
 }
+
+// this file's code object loaded on the current device (see smem_preload_seed)
+extern "C" hipError_t smem_preload_ksw(void) {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&smem::ksw_extend_kernel));
+}

@@ -1189,7 +1189,12 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
             uint64_t* link = nullptr;
             e = hipMallocAsync((void**)&link, n_dense * sizeof(uint64_t), g->init_st);
             if (e == hipSuccess) {
-                e = smem_launch_sa_densify2(&S, dshift, n_dense, link, dense, g->init_st);
+                // in the background: a quarter of the chip's block slots (4
+                // per CU), so the first batches' kernels find CUs beside it
+                // (their lookups use the uploaded samples until it is done);
+                // synchronous (SMEM_GPU_SYNC_INIT): the whole chip
+                const unsigned cap = getenv("SMEM_GPU_SYNC_INIT") ? 0u : (unsigned)g->n_cu * 4u;
+                e = smem_launch_sa_densify2(&S, dshift, n_dense, link, dense, cap, g->init_st);
                 hipError_t f = hipFreeAsync(link, g->init_st);
                 if (e == hipSuccess) e = f;
             }
@@ -2459,8 +2464,25 @@ static int batch_prealloc(smem_batch_t* b) {
 // one pass of every stage over a few reads cut from the resident .pac on a
 // slot batch: each kernel's code object is loaded on its first launch, and
 // that load should not fall on a worker's first batch
+extern "C" hipError_t smem_preload_seed(void);
+extern "C" hipError_t smem_preload_chain(void);
+extern "C" hipError_t smem_preload_ksw(void);
+extern "C" hipError_t smem_preload_aln(void);
+
 static int batch_warmup(smem_batch_t* b) {
     smem_gpu_t* g = b->g;
+    // default: each kernel file's code object loaded by a query, no device
+    // work -- a pass of the stages would queue behind the .sa densification
+    // (SMEM_GPU_WARMUP=full: that pass, over reads cut from the .pac)
+    const char* wv = getenv("SMEM_GPU_WARMUP");
+    if (!(wv && !strcmp(wv, "full"))) {
+        HIP_TRY(hipSetDevice(g->device));
+        HIP_TRY(smem_preload_seed());
+        HIP_TRY(smem_preload_chain());
+        HIP_TRY(smem_preload_ksw());
+        HIP_TRY(smem_preload_aln());
+        return SMEM_OK;
+    }
     if (!g->d_pac || g->l_pac < 4096) return SMEM_OK;
     const int nr = std::min(64, b->max_reads), L = std::min(150, b->max_len);
     std::vector<uint8_t> pk((size_t)(L + 8) / 4 + 2), codes((size_t)nr * L);

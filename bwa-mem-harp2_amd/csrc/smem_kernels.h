@@ -113,9 +113,10 @@ hipError_t smem_launch_ovf_slot(const int32_t* items, int n_ovf, int32_t* ovf_sl
 hipError_t smem_launch_sa_count(const smem::SaParams* S, hipStream_t st);
 hipError_t smem_launch_sa_densify(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense, uint64_t* dense,
                                   hipStream_t st);
-// the same dense[] by hop + chase passes (link: n_dense words of scratch; n_dense < 2^32)
+// the same dense[] by hop + chase passes (link: n_dense words of scratch; n_dense < 2^32;
+// max_blocks != 0 caps the lane-strided grids, leaving CUs to other work)
 hipError_t smem_launch_sa_densify2(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense, uint64_t* link,
-                                   uint64_t* dense, hipStream_t st);
+                                   uint64_t* dense, unsigned max_blocks, hipStream_t st);
 hipError_t smem_launch_sa_walk(const smem::SaParams* S, int grid, hipStream_t st);
 hipError_t smem_launch_offsets(const uint64_t* in, uint64_t* out, int n, void* temp, size_t* temp_bytes,
                                hipStream_t st);

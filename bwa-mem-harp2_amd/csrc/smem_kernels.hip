@@ -1901,10 +1901,11 @@ static unsigned densify_grid(uint64_t n) {
 }
 
 extern "C" hipError_t smem_launch_sa_densify2(const smem::SaParams* S, uint32_t dshift, uint64_t n_dense,
-                                              uint64_t* link, uint64_t* dense, hipStream_t st) {
+                                              uint64_t* link, uint64_t* dense, unsigned max_blocks, hipStream_t st) {
     if (n_dense == 0) return hipSuccess;
     if (n_dense >= (1ull << 32) || dshift >= S->sa_shift) return hipErrorInvalidValue;
-    const unsigned grid = densify_grid(n_dense);
+    unsigned grid = densify_grid(n_dense);
+    if (max_blocks && grid > max_blocks) grid = max_blocks;
     hipLaunchKernelGGL(smem::sa_densify_hop_kernel, dim3(grid), dim3(256), 0, st, *S, dshift, n_dense, link);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1932,4 +1933,11 @@ extern "C" hipError_t smem_launch_sa_walk(const smem::SaParams* S, int grid, hip
     hipLaunchKernelGGL(smem::sa_fill_kernel, dim3((unsigned)((S->n_intv + 255) / 256)), dim3(256), 0, st, *S);
     hipLaunchKernelGGL(smem::sa_walk_kernel, dim3(grid), dim3(256), 0, st, *S);
     return hipGetLastError();
+}
+
+// this file's code object loaded on the current device without running
+// anything (smem_gpu_reserve_slots: the first batch does not pay the load)
+extern "C" hipError_t smem_preload_seed(void) {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&smem::sa_count_kernel));
 }
