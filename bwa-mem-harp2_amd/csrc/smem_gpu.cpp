@@ -202,6 +202,11 @@ struct HostBuf {
 
 }  // namespace
 
+extern "C" hipError_t smem_preload_seed(void);
+extern "C" hipError_t smem_preload_chain(void);
+extern "C" hipError_t smem_preload_ksw(void);
+extern "C" hipError_t smem_preload_aln(void);
+
 // device SA sampling interval = 2^SA_DENSE_SHIFT (see smem_gpu_load_sa)
 constexpr uint32_t SA_DENSE_SHIFT = 2;
 // chaining: reads with more seed occurrences than this get a wave each
@@ -587,6 +592,14 @@ static int gpu_open(smem_gpu_t* g, const uint32_t* bwt) {
     (void)hipFree(g->d_bwt);
     g->d_bwt = nullptr;
 #endif
+    // every kernel file's code object loaded now (~0.1 s, once per process
+    // and device), beside bwa_idx_load's reading the .sa, not when the first
+    // batch launches its kernels
+    e = smem_preload_seed();
+    if (e == hipSuccess) e = smem_preload_chain();
+    if (e == hipSuccess) e = smem_preload_ksw();
+    if (e == hipSuccess) e = smem_preload_aln();
+    if (e != hipSuccess) return fail(SMEM_E_DEVICE, "smem_gpu_init: code objects", e);
     return SMEM_OK;
 }
 
@@ -1189,12 +1202,10 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
             uint64_t* link = nullptr;
             e = hipMallocAsync((void**)&link, n_dense * sizeof(uint64_t), g->init_st);
             if (e == hipSuccess) {
-                // in the background: a quarter of the chip's block slots (4
-                // per CU), so the first batches' kernels find CUs beside it
-                // (their lookups use the uploaded samples until it is done);
-                // synchronous (SMEM_GPU_SYNC_INIT): the whole chip
-                const unsigned cap = getenv("SMEM_GPU_SYNC_INIT") ? 0u : (unsigned)g->n_cu * 4u;
-                e = smem_launch_sa_densify2(&S, dshift, n_dense, link, dense, cap, g->init_st);
+                // the whole chip (capped at 4 blocks per CU so that the first
+                // batches ran beside it, it finished later and they were no
+                // faster: profiles/r04/e2e/probe_preload_densify_cap.log)
+                e = smem_launch_sa_densify2(&S, dshift, n_dense, link, dense, 0u, g->init_st);
                 hipError_t f = hipFreeAsync(link, g->init_st);
                 if (e == hipSuccess) e = f;
             }
@@ -2464,16 +2475,12 @@ static int batch_prealloc(smem_batch_t* b) {
 // one pass of every stage over a few reads cut from the resident .pac on a
 // slot batch: each kernel's code object is loaded on its first launch, and
 // that load should not fall on a worker's first batch
-extern "C" hipError_t smem_preload_seed(void);
-extern "C" hipError_t smem_preload_chain(void);
-extern "C" hipError_t smem_preload_ksw(void);
-extern "C" hipError_t smem_preload_aln(void);
-
 static int batch_warmup(smem_batch_t* b) {
     smem_gpu_t* g = b->g;
     // default: each kernel file's code object loaded by a query, no device
-    // work -- a pass of the stages would queue behind the .sa densification
-    // (SMEM_GPU_WARMUP=full: that pass, over reads cut from the .pac)
+    // work (gpu_open has already done it; a pass of the stages would queue
+    // behind the .sa densification) -- SMEM_GPU_WARMUP=full: that pass, over
+    // reads cut from the .pac
     const char* wv = getenv("SMEM_GPU_WARMUP");
     if (!(wv && !strcmp(wv, "full"))) {
         HIP_TRY(hipSetDevice(g->device));
