@@ -272,12 +272,19 @@ struct smem_gpu {
     // smem_gpu_init_devices_async: the upload running on a host thread; every
     // entry point that touches the device waits for it (gpu_wait)
     std::shared_future<int> ready;
+    std::mutex ready_mu;  // ready is extended (gpu_chain) while other threads may wait on it
 };
 
 // the background upload of smem_gpu_init_devices_async has finished (its
 // failure faulted the device, which gpu_check then reports)
 static void gpu_wait(smem_gpu_t* g) {
-    if (g && g->ready.valid()) g->ready.wait();
+    if (!g) return;
+    std::shared_future<int> f;
+    {
+        std::lock_guard<std::mutex> lk(g->ready_mu);
+        f = g->ready;
+    }
+    if (f.valid()) f.wait();
 }
 
 // scratch of the heavy-read path of chains -> regions
@@ -2761,6 +2768,7 @@ int smem_gpu_init_devices(smem_gpu_t** gpus, int n, const int* devices, const ui
 // the device work of a handle as a chain of background steps: each waits for
 // the one before; a failure faults the handle (3), later steps do nothing
 static void gpu_chain(smem_gpu_t* g, const char* what, std::function<int()> step) {
+    std::lock_guard<std::mutex> lk(g->ready_mu);
     std::shared_future<int> prev = g->ready;
     g->ready = std::async(std::launch::async, [g, what, prev, step]() -> int {
         if (prev.valid() && prev.get() != SMEM_OK) return SMEM_E_DEVICE;
