@@ -2856,9 +2856,12 @@ int smem_gpu_wait_ready(smem_gpu_t* g) {
     }
     for (auto& f : res)  // the worker slots being sized (smem_gpu_reserve_slots)
         if (f.valid()) f.wait();
-    // (the .sa densification may still run: smem_batch_sa uses the stored
-    // samples until it has finished)
-    return gpu_check(g);
+    if (int r = gpu_check(g)) return r;
+    if (g->sa_ready) {  // the .sa densification on the init stream (batches do not
+        HIP_TRY(hipSetDevice(g->device));  // need it: their lookups use the uploaded
+        HIP_TRY(hipEventSynchronize(g->sa_ready));  // samples until it is done)
+    }
+    return SMEM_OK;
 }
 
 }  // extern "C"

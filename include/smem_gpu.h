@@ -157,9 +157,10 @@ int  smem_gpu_init_devices(smem_gpu_t **gpus, int n, const int *devices, const u
 int  smem_gpu_init_devices_async(smem_gpu_t **gpus, int n, const int *devices, const uint32_t *bwt, uint64_t bwt_size,
                                  uint64_t primary, const uint64_t L2[5], const smem_sa_t *sa, const uint8_t *pac,
                                  int64_t l_pac);
-/* Waits until the device is ready for worker batches: the upload chain and
- * any smem_gpu_reserve_slots sizing have finished (the .sa densification may
- * still be running: the SA lookups use the stored samples until it is done). */
+/* Waits until everything the device does in the background has finished:
+ * the upload chain, the .sa densification and any smem_gpu_reserve_slots
+ * sizing (batches need not wait: their SA lookups use the uploaded samples
+ * until the densification is done). */
 int  smem_gpu_wait_ready(smem_gpu_t *gpu);
 /* The steps of smem_gpu_init_devices_async one by one, so that each starts
  * as soon as its input is in memory (bwa_idx_load reads .bwt, then .sa, then
