@@ -53,8 +53,9 @@ def main():
         for leg in own.legs.split("/"):
             name, *kv = leg.split("+")
             env = dict(os.environ, SMEM_GPU_TIMES="1", **dict(x.split("=", 1) for x in kv))
-            b = env.pop("B", batch)  # gpu+B=<n>: this leg's bwa -b
-            cmd = ([bench.BWA_GPU, "mem", "-t", str(own.threads), "-b", str(b), base, fq] if name == "gpu" else
+            b = env.pop("B", batch)  # gpu+B=<n>: this leg's bwa -b (B=auto: no -b)
+            bopt = [] if str(b) == "auto" else ["-b", str(b)]
+            cmd = ([bench.BWA_GPU, "mem", "-t", str(own.threads)] + bopt + [base, fq] if name == "gpu" else
                    [bench.REF_HARNESS, "mem", base, fq, str(own.threads), "1", "0"])
             legs.append((leg, cmd, env))
         for name, cmd, env in legs:
