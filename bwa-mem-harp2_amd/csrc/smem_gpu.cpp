@@ -550,6 +550,12 @@ static smem_gpu_t* gpu_handle(int device, uint64_t bwt_size, uint64_t primary, c
     if (!g) return nullptr;
     g->device = device;
     if (const char* v = getenv("SMEM_GPU_MAX_ACTIVE")) g->max_active = std::max(1, std::min(256, atoi(v)));
+    // the default seeding kernel for this handle (A/B: the same runs with another kernel);
+    // a variant this build does not have is ignored
+    if (const char* v = getenv("SMEM_GPU_SEED_VARIANT")) {
+        const int sv = atoi(v);
+        if (sv > 0 && smem_seed_variant_built(sv) && sv != 9 && sv != 23 && sv != 25) g->variant = sv;
+    }
     g->bwt_size = bwt_size;
     g->primary = primary;
     std::memcpy(g->L2, L2, sizeof(g->L2));
@@ -639,7 +645,8 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
     g_err[0] = 0;
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31))) return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31) || (variant >= 40 && variant <= 43)))
+        return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
 
     if (!smem_seed_variant_built(variant))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant: A/B variant not in this build (make AB=1)");

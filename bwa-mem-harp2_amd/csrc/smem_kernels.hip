@@ -105,6 +105,8 @@ enum Phase : int {
     P_NEXT2,        // start of one smem_next2 call      (software/bwamem.c:247-258)
     P_SMEM_BEGIN,   // start of one bwt_smem1            (software/bwt.c:782-789)
     P_FETCH,        // next read from the work counter
+    P_BWD_WAIT,     // seed_wp_kernel: the wave is extending the step's entries
+    P_BWD_DONE,     // seed_wp_kernel: every entry of the step extended
     P_EXIT
 };
 
@@ -1277,6 +1279,476 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
     }
 }
 
+// ======================================================================
+// seed_wp_kernel: the same loop with the backward phase wave-parallel over
+// list entries (variants 40-43).
+//
+// A backward step at position i extends every interval of `prev` with the
+// same base q[i], and the extends are independent (software/bwt.c:812-826).
+// prev is nested (prev[0] is the longest match, each entry's SA interval
+// contains the one before it), so the extended sizes are non-decreasing in
+// the entry index: the entries that fail (size < min_intv) are a prefix,
+// only entry 0 can become a SMEM (the fail branch needs curr->n == 0 and, for
+// a second failure, mem's last start is already i + 1), and the survivors
+// keep the first of each run of equal sizes (:823).  So a step is one ballot
+// of "survives", one of "kept", and a prefix rank of the kept entries -- no
+// entry depends on another's result.
+//
+// Lanes 0 .. OWN-1 of a wave own reads (the smem_next2 / bwt_smem1 state
+// machine, as seed_kernel's lanes); every lane of the wave executes one
+// bwt_extend per iteration:
+//  * an owner in a forward extension (software/bwt.c:791-805: a serial chain)
+//    extends its own interval;
+//  * every other lane (owners waiting on a backward step, lanes >= OWN, idle
+//    owners) takes the next entry of some owner's backward step: the owners'
+//    remaining entry counts are prefix-summed across the wave (DPP), owner o
+//    gets the free lanes of ranks [excl_o, excl_o + take_o), and each worker
+//    finds its owner from the start marks (one LDS scatter + one ballot);
+//  * the worker extends the entry, and the kept results are written straight
+//    into the owner's curr list (in place over prev: curr[k] is written after
+//    prev[>= k] was read, software/bwt.c:828) at the rank the kept ballot gives.
+// An owner's step therefore takes one iteration when enough lanes are free,
+// instead of one per entry, and the per-entry advance (seed_kernel's
+// BWD_RES block) is gone; the lists live in LDS (NL entries per owner, OWN
+// owners per wave: twice seed_kernel's entries per list in the same LDS),
+// entries beyond NL in the owner's arena.
+// ======================================================================
+template <int OWN, int NL>
+struct WpWave {
+    uint4 e[NL][OWN];     // owners' lists: index k < NL at slot (lr - k) mod NL
+    uint4 d0[OWN];        // step descriptors: j, curr_n, prev_off, c | lr << 2 | last_x2 bits 32-33 << 8
+    uint4 d1[OWN];        // min_intv, last_x2 low word
+    uint4 q[OWN];         // query windows (LDS-DMA landing slots)
+    uint64_t res[64];     // extend result sizes by lane
+    uint32_t tabS[64];    // owner whose segment starts at task position p (0xFF: none)
+    uint32_t tabP[64];    // free-lane rank -> lane
+};
+
+// inclusive prefix sum over the 64 lanes (the row_shr / row_bcast pattern of
+// ksw_device.h's scan_max)
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// set bits of m below this lane
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ int hibit64(uint64_t m) { return 63 - __builtin_clzll(m); }
+
+// LDS accesses of one wave execute in order; this keeps the compiler from
+// moving them across the point where another lane's write must be seen
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int OWN, int NL, int PRIO>
+__global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
+    static_assert(OWN >= 1 && OWN <= 64 && NL >= 2 && NL < 32, "owners per wave / list entries");
+    __shared__ WpWave<OWN, NL> wlds[4];
+    WpWave<OWN, NL>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    const int me = (int)(threadIdx.x & 63);
+    const uint64_t wave_g = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);  // lane 0's global index
+    const uint32_t cap = P.cap_list;
+    // an owner's arena: [0, cap) the forward list beyond the ring, [cap, 2 cap) curr / prev beyond NL
+    PIntv* __restrict__ bp = reinterpret_cast<PIntv*>(P.scratch + (wave_g + (uint64_t)me) * 2ull * cap);
+
+    int phase = me < OWN ? P_FETCH : P_EXIT;  // lanes >= OWN only execute extends
+    int item = -1, len = 0;
+    int nitem = 0, nlen = -2;  // next read: -2 nothing claimed, -1 claimed, >= 0 offsets loaded
+    int rid = 0, nrid = 0;
+    uint32_t keep_n = 0;
+    uint32_t o0 = 0, no0 = 0;
+    uint32_t qb = ~0u, qwant = ~0u;
+    uint4 qv = {0, 0, 0, 0};
+    uint32_t raw_n = 0, calls_n = 0;
+    int start = 0, ori_start = 0;
+    int x = 0, min_intv = 1, middle = 0, i = 0, ret = 0, cur_c = 0;
+    uint32_t j = 0;
+    uint64_t ik0 = 0, ik1 = 0, ik2 = 0;
+    uint32_t ikend = 0;
+    uint32_t fwd_n = 0, prev_off = 0, prev_n = 0, curr_n = 0;
+    uint32_t lr = 0;           // forward: the ring position; backward: the slot of list index 0
+    uint32_t fail0 = 0;        // entry 0 of the current step failed (its SMEM candidate)
+    uint64_t last_x2 = 0;      // size of the last entry kept in curr (dedup across chunks of a step)
+    uint32_t mem_n = 0, mem_last_start = 0, m_n = 0;
+    uint32_t max_len = 0, max_x2 = 0, max_mid = 0;
+    uint4 head = {0, 0, 0, 0};  // prev[0] of the current step
+    uint64_t na = 0, nb = 0, ns = 0;
+    if (P.tspan && me == 0) atomicMax(reinterpret_cast<unsigned long long*>(P.tspan), ~(unsigned long long)rtstamp());
+
+#define QBLK(pos) ((o0 + (uint32_t)(pos)) & ~15u)
+#define WSLOT(r_, k_) ((r_) >= (k_) ? (r_) - (k_) : (r_) + (uint32_t)NL - (k_))
+// a SMEM of the current call: the raw log entry, the merge's keep count and
+// the longest match (software/bwt.c:817-819, software/bwamem.c:266-270, 284-292)
+#define WP_EMIT(e_)                                                                                          \
+    {                                                                                                        \
+        const uint4 me_ = (e_);                                                                              \
+        if (raw_n >= P.cap_intv) {                                                                           \
+            phase = P_OVF;                                                                                   \
+        } else {                                                                                             \
+            const uint32_t b_ = (uint32_t)(i + 1), en_ = p_end(me_);                                         \
+            put_rec<false>(P.out_intv + (uint64_t)item * P.cap_intv + raw_n++,                               \
+                           Intv{p_x0(me_), p_x1(me_), p_x2(me_), (uint64_t)en_ | ((uint64_t)b_ << 32)});    \
+            keep_n += !middle || (en_ - b_ >= (max_len >> 1) && en_ > (uint32_t)ori_start);                 \
+            ++mem_n;                                                                                         \
+            mem_last_start = b_;                                                                             \
+            if (!middle && en_ - b_ >= max_len) {                                                            \
+                max_len = en_ - b_;                                                                          \
+                max_x2 = p_x2(me_) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)p_x2(me_);                      \
+                max_mid = (en_ + b_) >> 1;                                                                   \
+            }                                                                                                \
+        }                                                                                                    \
+    }
+
+    for (;;) {
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(2);
+        if (phase == P_FETCH) {
+            if (nlen == -2) {  // claim the next read
+                nitem = atomicAdd(P.head, 1);
+                nlen = -1;
+            } else if (nlen == -1) {  // its offsets (the claim returned last iteration)
+                next_offsets(P, nitem, no0, nlen, nrid);
+            }
+        }
+        // ---- owners: advance the state machine one pass (seed_kernel's
+        // blocks, without the per-entry backward block) ----
+        bool out = false;
+        if (phase != P_EXIT) {
+            if (phase == P_SMEM_END) {
+                if (!middle) {  // software/bwamem.c:261-272
+                    start = ret;
+                    m_n = mem_n;
+                    const int split_len = P.split_len_init < len ? P.split_len_init : len;
+                    if (m_n > 0 && split_len > 0 && (int)max_len >= split_len &&
+                        (uint64_t)max_x2 <= (uint64_t)(int64_t)P.split_width) {
+                        x = (int)max_mid;  // re-seed from the middle (software/bwamem.c:272-278)
+                        min_intv = (int)(max_x2 + 1);
+                        middle = 1;
+                        phase = P_SMEM_BEGIN;
+                    }
+                }
+                if (phase == P_SMEM_END) {
+                    if (calls_n >= P.cap_calls) {
+                        phase = P_OVF;
+                    } else {
+                        put_rec<false>(P.out_call + (uint64_t)item * P.cap_calls + calls_n++,
+                                       CallRec{m_n, middle ? mem_n : 0u, (uint32_t)ori_start, max_len});
+                        phase = P_NEXT2;
+                    }
+                }
+            }
+            if (phase == P_OVF) {
+                P.n_intv[item] = SMEM_OVERFLOW;
+                P.n_calls[item] = 0;
+                const int slot = atomicAdd(P.ovf_count, 1);
+                P.ovf_items[slot] = item;
+                phase = P_FETCH;
+            }
+            if (phase == P_FETCH) {
+                if (nlen < 0) {
+                    out = true;
+                } else if (nitem >= P.n_items) {
+                    phase = P_EXIT;
+                } else {
+                    item = nitem;
+                    rid = nrid;
+                    keep_n = 0;
+                    o0 = no0;
+                    len = nlen;
+                    nlen = -2;
+                    raw_n = 0;
+                    calls_n = 0;
+                    start = 0;
+                    if (len < P.min_seed_len) {  // mem_chain's guard (software/bwamem.c:600)
+                        P.n_intv[item] = 0;
+                        P.n_calls[item] = 0;
+                        P.s_intv[rid] = 0;
+                        P.s_calls[rid] = 0;
+                        out = true;
+                    } else {
+                        phase = P_NEXT2;
+                    }
+                }
+            }
+            if (phase == P_NEXT2) {  // software/bwamem.c:247-261
+                bool wait_q = false;
+                if (start < len && start >= 0) {
+                    for (;;) {
+                        if (start >= len) break;
+                        if (QBLK(start) != qb) { wait_q = true; break; }
+                        if (qsel(o0, start, qv) <= 3) break;
+                        ++start;
+                    }
+                }
+                if (wait_q) {
+                    qwant = QBLK(start);
+                    out = true;
+                } else if (start >= len || start < 0) {
+                    P.n_intv[item] = raw_n;
+                    P.n_calls[item] = calls_n;
+                    P.s_intv[rid] = keep_n;
+                    P.s_calls[rid] = calls_n;
+                    phase = P_FETCH;
+                } else {
+                    ori_start = start;
+                    x = ori_start;
+                    min_intv = P.start_width;
+                    middle = 0;
+                    max_len = 0;
+                    phase = P_SMEM_BEGIN;
+                }
+            }
+            if (phase == P_SMEM_BEGIN) {  // software/bwt.c:782-789
+                if (QBLK(x) != qb) {
+                    qwant = QBLK(x);
+                    out = true;
+                } else {
+                    mem_n = 0;
+                    const int qx = qsel(o0, x, qv);
+                    if (qx > 3) {
+                        ret = x + 1;
+                        phase = P_SMEM_END;
+                    } else {
+                        if (min_intv < 1) min_intv = 1;
+                        const uint64_t lq = sel4(qx, P.L2[0], P.L2[1], P.L2[2], P.L2[3]);
+                        const uint64_t lq1 = sel4(qx, P.L2[1], P.L2[2], P.L2[3], P.L2[4]);
+                        ik0 = lq + 1;
+                        ik2 = lq1 - lq;
+                        ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
+                        ikend = (uint32_t)(x + 1);
+                        fwd_n = 0;
+                        lr = 0;
+                        i = x + 1;
+                        phase = P_FWD;
+                    }
+                }
+            }
+            if (phase == P_BWD_DONE) {  // every entry of step i extended (software/bwt.c:815-828)
+                if (fail0 && (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start)) WP_EMIT(head);
+                if (phase == P_BWD_DONE) {
+                    if (curr_n == 0) {  // software/bwt.c:827
+                        phase = P_SMEM_END;
+                    } else {            // :828 swap, next position
+                        prev_n = curr_n;
+                        prev_off = cap;
+                        head = L->e[lr][me];  // curr[0]: index 0 sits in slot lr
+                        --i;
+                        phase = P_BWD_STEP;
+                    }
+                }
+            }
+            if (phase == P_FWD_RES) {  // software/bwt.c:795-799; na = x[1], nb = x[0]
+                bool stop = false;
+                if (ns != ik2) {
+                    const uint4 fe = pack_p(ik0, ik1, ik2, ikend);
+                    if (fwd_n >= (uint32_t)NL) *reinterpret_cast<uint4*>(bp + cap - 1 - (fwd_n - NL)) = L->e[lr][me];
+                    L->e[lr][me] = fe;
+                    lr = lr + 1 == (uint32_t)NL ? 0u : lr + 1;
+                    ++fwd_n;
+                    stop = ns < (uint64_t)min_intv;
+                }
+                if (stop) {
+                    phase = P_FWD_DONE;
+                } else {
+                    ik0 = nb; ik1 = na; ik2 = ns;
+                    ikend = (uint32_t)(i + 1);
+                    ++i;
+                    phase = P_FWD;
+                }
+            }
+            if (phase == P_FWD) {  // software/bwt.c:791-803
+                bool push = true;
+                if (i < len) {
+                    if (QBLK(i) != qb) {
+                        qwant = QBLK(i);
+                        out = true;
+                        push = false;
+                    } else {
+                        const int qi = qsel(o0, i, qv);
+                        if (qi < 4) {
+                            cur_c = 3 - qi;
+                            if (i + 1 < len) qwant = QBLK(i + 1);
+                            phase = P_FWD_RES;  // -> extend (forward), on this lane
+                            out = true;
+                            push = false;
+                        }
+                    }
+                }
+                if (push) {  // ambiguous base, or end of query: push ik and stop
+                    const uint4 fe = pack_p(ik0, ik1, ik2, ikend);
+                    if (fwd_n >= (uint32_t)NL) *reinterpret_cast<uint4*>(bp + cap - 1 - (fwd_n - NL)) = L->e[lr][me];
+                    L->e[lr][me] = fe;
+                    lr = lr + 1 == (uint32_t)NL ? 0u : lr + 1;
+                    ++fwd_n;
+                    phase = P_FWD_DONE;
+                }
+            }
+            if (phase == P_FWD_DONE) {  // software/bwt.c:805-808 (the ring read backwards is the reversal)
+                head = pack_p(ik0, ik1, ik2, ikend);  // the last push: prev[0]
+                ret = (int)ikend;
+                prev_off = cap - fwd_n;
+                prev_n = fwd_n;
+                lr = lr == 0 ? (uint32_t)NL - 1 : lr - 1;  // slot of the last push
+                i = x - 1;
+                phase = P_BWD_STEP;
+            }
+            if (phase == P_BWD_STEP) {  // software/bwt.c:810-812
+                if (i >= 0 && QBLK(i) != qb) {
+                    qwant = QBLK(i);
+                    out = true;
+                } else {
+                    cur_c = i < 0 ? -1 : qsel(o0, i, qv);
+                    if (cur_c > 3) cur_c = -1;
+                    if (cur_c >= 0) {
+                        j = 0;
+                        curr_n = 0;
+                        fail0 = 0;
+                        if (i > 0) qwant = QBLK(i - 1);  // the next step's base
+                        phase = P_BWD_WAIT;               // -> the wave extends the step's entries
+                    } else {
+                        // nothing extends: prev[0] is the only candidate (software/bwt.c:816-819)
+                        phase = P_SMEM_END;
+                        if (mem_n == 0 || (uint32_t)(i + 1) < mem_last_start) WP_EMIT(head);
+                    }
+                }
+            }
+        }
+        // ---- uniform section ----
+        if (!__any(phase != P_EXIT)) break;
+        const bool fwdreq = out && phase == P_FWD_RES;
+        const uint32_t rem = phase == P_BWD_WAIT ? prev_n - j : 0u;
+        if (rem) {  // what a worker needs of this owner's step
+            L->d0[me] = make_uint4(j, curr_n, prev_off,
+                                   (uint32_t)cur_c | lr << 2 | (uint32_t)(last_x2 >> 32) << 8);
+            L->d1[me] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, 0u, 0u);
+        }
+        // the owners' remaining entries laid out in lane order over the free lanes
+        const uint32_t incl = wave_scan_add(rem);
+        const uint32_t excl = incl - rem;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint64_t fmask = ~(uint64_t)__ballot(fwdreq);
+        const uint32_t nfree = (uint32_t)__popcll(fmask);
+        const uint32_t ntask = total < nfree ? total : nfree;
+        const uint32_t take = (rem && excl < nfree) ? min(rem, nfree - excl) : 0u;
+        const bool freel = (fmask >> me) & 1;
+        const uint32_t rank = mbcnt64(fmask);
+        L->tabS[me] = 0xFFu;
+        wave_lds_fence();
+        if (take) L->tabS[excl] = (uint32_t)me;
+        if (freel) L->tabP[rank] = (uint32_t)me;
+        wave_lds_fence();
+        const uint64_t marks = __ballot(L->tabS[me] != 0xFFu);
+        const bool worker = freel && rank < ntask;
+        uint32_t s = 0, o = 0, jj = 0, lro = 0;
+        uint4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0}, ent = {0, 0, 0, 0};
+        if (worker) {
+            s = (uint32_t)hibit64(marks & ((2ull << rank) - 1ull));  // the segment holding task `rank`
+            o = L->tabS[s];
+            w0 = L->d0[o];
+            w1 = L->d1[o];
+            jj = w0.x + (rank - s);
+            lro = (w0.w >> 2) & 31u;
+            if (jj < (uint32_t)NL) {
+                ent = L->e[WSLOT(lro, jj)][o];
+            } else {  // beyond the LDS list: the owner's arena (the bound only guards a broken list)
+                const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                const uint32_t at = w0.z + jj;
+                ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+            }
+        }
+        // the query window for owners that want one
+        const bool ld_q = qwant != qb && qwant != ~0u;
+        if (ld_q) __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&L->q[0]), 16, 0, 0);
+        // the extend: forward owners their own ik (a = x[1]), workers an entry backward (a = x[0])
+        const bool task = worker || fwdreq;
+        const uint64_t ra = fwdreq ? ik1 : p_x0(ent), rb = fwdreq ? ik0 : p_x1(ent), rs = fwdreq ? ik2 : p_x2(ent);
+        const int rc = fwdreq ? cur_c : (int)(w0.w & 3u);
+        const uint64_t k = ra - 1, l = k + rs;
+        uint64_t kk = k - (k >= P.primary), ll = l - (l >= P.primary);
+        // rows past the BWT only come from a broken entry: keep the loads inside the index
+        // (the results then differ from the oracle instead of faulting the device)
+        if (kk >= P.L2[4]) kk = 0;
+        if (ll >= P.L2[4]) ll = 0;
+        const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
+        uint4 k0 = {0, 0, 0, 0}, k1 = {0, 0, 0, 0}, l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
+        if (task) {
+            const uint32_t *a0, *a1;
+            block_chunks<false>(P.occ64, bk, a0, a1);
+            k0 = *reinterpret_cast<const uint4*>(a0);
+            k1 = *reinterpret_cast<const uint4*>(a1);
+            if (bl != bk) {
+                block_chunks<false>(P.occ64, bl, a0, a1);
+                l0 = *reinterpret_cast<const uint4*>(a0);
+                l1 = *reinterpret_cast<const uint4*>(a1);
+            }
+        }
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ld_q) {
+            qv = L->q[me];
+            qb = qwant;
+        }
+        if (task) {
+            const Bucket32 wk{k0, k1};
+            const Bucket32 wl = bl != bk ? Bucket32{l0, l1} : wk;
+            extend_counts64<false>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
+        }
+        // ---- the backward results: survive, dedup, rank, write into curr ----
+        const bool surv = worker && ns >= (uint64_t)w1.x;
+        const uint64_t smask = __ballot(surv);
+        L->res[me] = ns;
+        wave_lds_fence();
+        bool keep = false;
+        if (surv) {
+            if (rank == s) {  // first entry of this chunk: against the last entry kept before it
+                const uint64_t lx = (uint64_t)((w0.w >> 8) & 3u) << 32 | w1.y;
+                keep = w0.y == 0 || ns != lx;
+            } else {          // against the previous entry (the previous free lane)
+                const int pp = hibit64(fmask & ((1ull << me) - 1ull));
+                keep = !((smask >> pp) & 1) || ns != L->res[pp];
+            }
+        }
+        const uint64_t kmask = __ballot(keep);
+        if (keep) {
+            const uint32_t pf = L->tabP[s];
+            const uint32_t kr = (uint32_t)__popcll(kmask & ((1ull << me) - 1ull) & ~((1ull << pf) - 1ull));
+            const uint32_t idx = w0.y + kr;
+            const uint4 e = pack_p(na, nb, ns, p_end(ent));
+            if (idx < (uint32_t)NL) {
+                L->e[WSLOT(lro, idx)][o] = e;
+            } else if (idx < cap) {
+                PIntv* obp = reinterpret_cast<PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                *reinterpret_cast<uint4*>(obp + cap + idx) = e;
+            }
+        }
+        // ---- owners whose entries ran: the chunk's outcome ----
+        if (take) {
+            const uint32_t pf = L->tabP[excl], pl = L->tabP[excl + take - 1];
+            const uint64_t seg = ((2ull << pl) - 1ull) & ~((1ull << pf) - 1ull);
+            const uint64_t km = kmask & seg;
+            if (j == 0) fail0 = !((smask >> pf) & 1);
+            if (km) last_x2 = L->res[hibit64(km)];
+            curr_n += (uint32_t)__popcll(km);
+            j += take;
+            if (j == prev_n) phase = P_BWD_DONE;
+        }
+        wave_lds_fence();  // this iteration's LDS reads before the next one's writes
+    }
+#undef WP_EMIT
+#undef WSLOT
+#undef QBLK
+    if (P.tspan && me == 0) atomicMax(reinterpret_cast<unsigned long long*>(P.tspan) + 1, (unsigned long long)rtstamp());
+}
+
 // Raw logs -> the lists smem_next2 returns: reverse each bwt_smem1 output
 // (software/bwt.c:830) and merge matches with sub-matches keyed by
 // (start, len - end), keeping a sub-match only if it is at least half the
@@ -1364,6 +1836,7 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
+    if (variant >= 40 && variant <= 43) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
     return variant == 0 || (variant >= 2 && variant <= 31);
 #else
@@ -1390,6 +1863,12 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 29: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1, 1>), dim3(grid), dim3(block), 0, st, *P); break;
         case 30: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1, 2>), dim3(grid), dim3(block), 0, st, *P); break;
         case 31: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1, 3>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 40-43: the backward phase wave-parallel over list entries (seed_wp_kernel<owners per wave,
+        // LDS list entries per owner, wave priority>)
+        case 40: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 41: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 16, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 42: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 24, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 43: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 0>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

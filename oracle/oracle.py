@@ -38,10 +38,11 @@ class Stats(C.Structure):
                                           "n_bkt_ref", "n_bases", "n_bkt64", "n_ext_fwd",
                                           "n_ext_u1_fwd", "n_ext_u1_bwd", "n_run_u1", "n_ext_fwd_k12")] + [
         ("n_ext_len", C.c_uint64 * 33), ("n_fwd_push", C.c_uint64), ("n_bwd_push_hi", C.c_uint64),
-        ("n_bwd_read_hi", C.c_uint64), ("n_fwd_spill", C.c_uint64)]
+        ("n_bwd_read_hi", C.c_uint64), ("n_fwd_spill", C.c_uint64),
+        ("n_bwd_step", C.c_uint64), ("n_step_hist", C.c_uint64 * 17), ("n_bwd_task_hi", C.c_uint64)]
 
     def as_dict(self) -> dict:
-        return {k: (list(getattr(self, k)) if k == "n_ext_len" else int(getattr(self, k))) for k, _ in self._fields_}
+        return {k: (list(getattr(self, k)) if k in ("n_ext_len", "n_step_hist") else int(getattr(self, k))) for k, _ in self._fields_}
 
 
 class ChainOptT(C.Structure):

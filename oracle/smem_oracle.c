@@ -235,9 +235,14 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 		c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
 		curr->n = 0;
 		had_u1 = has_u1; has_u1 = 0;
+		if (c >= 0) {
+			w->st.n_bwd_step++;
+			w->st.n_step_hist[prev->n < 16 ? prev->n : 16]++;
+		}
 		for (j = 0; j < (int)prev->n; ++j) {
 			orc_intv_t *p = &prev->a[j];
 			if (i < x - 1 && j >= NL) w->st.n_bwd_read_hi++;
+			if (c >= 0 && j >= NL) w->st.n_bwd_task_hi++;
 			orc_extend(b, p, ok, 1);
 			count_extend(b, p, 1, c >= 0, &w->st);
 			if (c >= 0) { int sl = (int)(uint32_t)p->info - i; w->st.n_ext_len[sl < 32 ? sl : 32]++; }
@@ -400,6 +405,8 @@ static void add_stats(orc_stats_t *d, const orc_stats_t *s)
 	{ int k; for (k = 0; k < 33; ++k) d->n_ext_len[k] += s->n_ext_len[k]; }
 	d->n_fwd_push += s->n_fwd_push; d->n_bwd_push_hi += s->n_bwd_push_hi; d->n_bwd_read_hi += s->n_bwd_read_hi;
 	d->n_fwd_spill += s->n_fwd_spill;
+	d->n_bwd_step += s->n_bwd_step; d->n_bwd_task_hi += s->n_bwd_task_hi;
+	{ int k; for (k = 0; k < 17; ++k) d->n_step_hist[k] += s->n_step_hist[k]; }
 }
 
 int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,

@@ -62,6 +62,9 @@ typedef struct {
 	uint64_t n_bwd_push_hi; /* backward-list (curr) pushes at index >= NL (ORC_LIST_LDS, default 11) */
 	uint64_t n_bwd_read_hi; /* backward-list (prev, steps >= 2) reads at index >= NL */
 	uint64_t n_fwd_spill;   /* forward-list entries beyond NL (the kernel's LDS ring spills them) */
+	uint64_t n_bwd_step;    /* backward steps with a base to extend by (c >= 0, software/bwt.c:812) */
+	uint64_t n_step_hist[17]; /* those steps by prev->n: 1..15, 16 = 16 or more */
+	uint64_t n_bwd_task_hi; /* backward extends (c >= 0, any step) of prev[j], j >= NL */
 } orc_stats_t;
 
 orc_bwt_t *orc_bwt_load(const char *fn);

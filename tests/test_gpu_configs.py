@@ -153,6 +153,25 @@ def test_human_kmer_table(human, gpu_device):
 
 
 @pytest.mark.timeout(900)
+@pytest.mark.parametrize("variant", [40, 41])
+def test_human_wp_kernel(human, variant):
+    """seed_wp_kernel at human size: forward lists longer than the LDS lists
+    (entries in the owner's arena, both list regions), 34-bit coordinates."""
+    from smemgpu import synth
+    gpu = human["gpu"]
+    gpu.set_variant(variant)
+    try:
+        reads = synth.make_reads(human["codes"], 10_000, 150, seed=12, sub_rate=0.02, n_rate=0.001)
+        res, _ = _seed_and_compare(gpu, human["oidx"], reads, {})
+        assert _high_bits(res) > 500
+        reads = synth.make_reads(human["codes"], 2_000, 250, seed=13, sub_rate=0.05, n_rate=0.001)
+        for opt in ({}, dict(start_width=2), dict(split_factor=1.0, split_width=500)):
+            _seed_and_compare(gpu, human["oidx"], reads, opt)
+    finally:
+        gpu.set_variant(0)
+
+
+@pytest.mark.timeout(900)
 def test_human_sa_lookup(human):
     """bwt_sa of every seed occurrence at human size (positions past 2^32)."""
     from smemgpu import synth

@@ -165,6 +165,62 @@ def test_kernel_variants(world, gpu_device, variant):
         gpu.close()
 
 
+WP_VARIANTS = [40, 41, 42, 43]
+
+
+def _edge_reads(g):
+    from smemgpu import synth
+    parts = []
+    for L in [0, 1, 2, 18, 19, 20, 28, 29, 30, 31]:
+        parts.append(synth.Reads(np.array([L], np.int32), g[1000:1000 + L].copy(), np.array([0, L], np.int64)))
+    for arr in (np.full(60, 4, np.uint8), np.concatenate([[4], g[5000:5100], [4]]).astype(np.uint8),
+                np.where(np.arange(120) % 7 == 0, 4, g[9000:9120]).astype(np.uint8), np.zeros(150, np.uint8)):
+        parts.append(synth.Reads(np.array([arr.size], np.int32), arr, np.array([0, arr.size], np.int64)))
+    return synth.concat_reads(parts)
+
+
+@pytest.mark.parametrize("variant", WP_VARIANTS)
+def test_wp_kernel_parity(world, gpu_device, variant):
+    """seed_wp_kernel (variants 40-43: owners per wave x LDS list entries x
+    wave priority): the backward steps' entries extended by the whole wave,
+    pruned by ballots (software/bwt.c:812-826) -- bit-exact against the
+    oracle on every read kind and option set, the edge cases, the overflow
+    pass and a grid with fewer lanes than reads."""
+    import smemgpu
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant)
+    try:
+        g = world["genome"].codes
+        for kind in ("150bp", "mixed", "250bp5"):
+            reads = _reads(world["genome"], kind, seed=300 + variant)
+            for opt in OPTS.values():
+                want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4, **opt)
+                got = smemgpu.seed(gpu, reads.codes, reads.offs, smemgpu.Options(**opt)).to_smgo()
+                assert got == want, (kind, opt)
+        edge = _edge_reads(g)
+        for opt in OPTS.values():
+            want, _, _ = oracle.seed(world["ref"], edge.codes, edge.offs, threads=4, **opt)
+            assert smemgpu.seed(gpu, edge.codes, edge.offs, smemgpu.Options(**opt)).to_smgo() == want, opt
+    finally:
+        gpu.close()
+    reads = _reads(world["genome"], "mixed", seed=7)
+    want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4)
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant, intv_cap=2)
+    try:  # the overflow pass
+        b = gpu.batch(reads.n, reads.codes.size, int(reads.lens.max()))
+        b.set_reads(reads.codes, reads.offs)
+        b.run()
+        assert b.stats()["n_overflow"] > 0
+        assert b.fetch().to_smgo() == want
+        b.close()
+    finally:
+        gpu.close()
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant, lanes_per_cu=64)
+    try:  # many reads per owner
+        assert smemgpu.seed(gpu, reads.codes, reads.offs).to_smgo() == want
+    finally:
+        gpu.close()
+
+
 @pytest.mark.parametrize("k", [1, 2, 7, 10, 12])
 def test_kmer_table_variant(world, gpu_device, k):
     """Variant 23: extends whose result has <= k bases read the k-mer table;
