@@ -6,10 +6,14 @@
 Workload (BASELINE.json configs[1], the default --config c2): an FM index
 resident in HBM and 1M x 150 bp single-end reads per GPU (2% substitutions,
 0.1% N, both strands).  human_g1k_v37 is not available offline, so the index
-is built from a seeded synthetic genome of its size (smemgpu/synth.py:
-random sequence with repeat families, exact and tandem repeats; or, with
---genome-profile human, a human-like ~46 % interspersed-repeat profile) by
-this repo's own `bwa index -a is`-identical builder; its size is in `config`.
+is built from a seeded synthetic genome of its size by this repo's own
+`bwa index -a is`-identical builder; its size is in `config`.  The headline
+(--genome-profile human, the default since round 5) uses the human-like
+profile of smemgpu/synth.py -- ~46 % interspersed repeats shaped like
+RepeatMasker's classes plus 3 % satellites, the closer stand-in -- and the
+line carries the same step on the uniform profile (random sequence with 2 %
+repeat families, exact and tandem repeats: rounds 1-4's headline) beside it
+(`uniform`).
 
 A step = one pass of the seeding hot path (mem_insert_seed's smem_next2 loop
 for every read, software/bwamem.c:453-460) over the resident batch: the
@@ -29,7 +33,7 @@ target sizes (12.5M pairs = one GPU's shard of C3's 100M pairs, 10M x 250 bp,
 10M x 150 bp at 5 %; c2 streams 4M); `value` stays the device-resident rate
 on a 1M-read batch of the same reads.
 
-roofline: dominant kernel = seed_kernel.  achieved = algorithmic bytes per
+roofline: dominant kernel = seed_wp_kernel (seed_kernel for variants < 40).  achieved = algorithmic bytes per
 launch (64 B x distinct Occ buckets per extend + read length
 + 32 B x intervals out, counted by the CPU oracle on a sample of the same
 reads) / the kernel's HIP-event duration measured here; frac_occ64 does the
@@ -37,7 +41,9 @@ same with the 32-B buckets this build actually reads.  The kernel is bound by
 random-request rate, not bytes: request_roofline compares its L2 fabric read
 requests per second (rocprofv3 TCC_EA0_RDREQ recorded by tools/traffic.py for
 this build and workload) with the random-gather ceiling measured on this GPU
-(tools/gather_ceiling.hip, profiles/gather_ceiling.json).
+(tools/gather_ceiling.hip, profiles/gather_ceiling.json); sq_counters gives
+the same kernel's VALU / SALU instructions per extend and its issue / wait
+shares (SQ_* counters of the same tools/traffic.py run).
 
 cpu_baseline: the reference's own C (oracle/_ref/ref_harness, compiled from
 the reference sources) when present, else the C restatement, timed on this
@@ -97,8 +103,9 @@ def parse(argv=None):
     p.add_argument("--sub", type=float, default=None)
     p.add_argument("--genome-mbp", type=float, default=HUMAN_MBP,
                    help="synthetic genome size; default = human_g1k_v37 l_pac (6.2 G symbols with its reverse complement)")
-    p.add_argument("--genome-profile", choices=["uniform", "human"], default="uniform",
-                   help="uniform: random + 2 %% repeat families; human: ~46 %% interspersed repeats + satellites")
+    p.add_argument("--genome-profile", choices=["uniform", "human"], default="human",
+                   help="human (the headline): ~46 %% interspersed repeats + satellites, the closer stand-in for "
+                        "human_g1k_v37; uniform: random + 2 %% repeat families")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu", help="index construction (same bytes)")
     p.add_argument("--lanes-per-cu", type=int, default=0)
@@ -126,11 +133,13 @@ def parse(argv=None):
     p.add_argument("--e2e-batch", type=int, default=0, help="-b of bwa-gpu mem (0: reads / threads)")
     p.add_argument("--e2e-chunk-reads", type=int, default=3_200_000,
                    help="e2e.multi_chunk: this many SE reads (several bwa mem chunks of 10 Mbp x threads; 0: off)")
-    p.add_argument("--human-like", type=int, default=1,
-                   help="1: also measure the seeding step on the human-like genome profile (N=1 only)")
+    p.add_argument("--other-profile", "--human-like", dest="other_profile", type=int, default=1,
+                   help="1: also measure the seeding step on the other genome profile (uniform beside the human-like "
+                        "headline; N=1 only)")
     p.add_argument("--cache", default=os.path.join(tempfile.gettempdir(), "smem_bench_cache"))
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                   help="per-launch TCC_EA0_RDREQ / FETCH_SIZE recorded by tools/traffic.py for this build + workload")
+    p.add_argument("--traffic-json", default=None,
+                   help="per-launch counters recorded by tools/traffic.py for this build + workload (default: "
+                        "profiles/traffic.json, or profiles/traffic_human.json for the human-like profile)")
     p.add_argument("--ceiling-json", default=os.path.join(ROOT, "profiles", "gather_ceiling.json"))
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
@@ -140,7 +149,17 @@ def parse(argv=None):
     a.pairs = cfg["pairs"]
     if a.stream_reads is None:
         a.stream_reads = cfg["stream_reads"]
+    if a.traffic_json is None:
+        a.traffic_json = traffic_path(a.genome_profile)
     return a
+
+
+def traffic_path(profile: str) -> str:
+    return os.path.join(ROOT, "profiles", "traffic_human.json" if profile == "human" else "traffic.json")
+
+
+def kernel_name(variant: int) -> str:
+    return "seed_wp_kernel" if variant >= 40 else "seed_kernel"
 
 
 def genome_key(args) -> str:
@@ -324,10 +343,14 @@ def traffic_for(args, path: str, build_id: str, kernel_id: str | None = None, la
             "sub": args.sub, "genome_profile": args.genome_profile}
     if any(w.get(k) != v for k, v in want.items()):
         return None
+    # the counted launches ran the kernel variant this line ran (files before round 5: variant 2)
+    if launch is None or t.get("variant", 2) != launch.get("variant"):
+        return None
     if t.get("build_id") == build_id:
-        return dict(t, matched_on="build_id")
-    if kernel_id and t.get("kernel_id") == kernel_id and launch and t.get("launch") == launch:
-        return dict(t, matched_on="kernel_id + launch shape")
+        return dict(t, matched_on="build_id + variant")
+    shape = {"grid": launch.get("grid"), "block": launch.get("block")}
+    if kernel_id and t.get("kernel_id") == kernel_id and t.get("launch") == shape:
+        return dict(t, matched_on="kernel_id + variant + launch shape")
     return None
 
 
@@ -821,7 +844,7 @@ def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": None,
-        "kernel": "seed_kernel",
+        "kernel": kernel_name((launch or {}).get("variant", 2)),
         "kernel_busy_ms": round(busy_ms, 3),
         "kernel_busy_ms_source": "time the GPU spent in seed_kernel over the timed region (union of every launch's "
                                  "first-wave-start .. last-wave-end on the chip's 100 MHz clock, s_memrealtime) / "
@@ -862,6 +885,22 @@ def roofline(args, bpr, bpr64, ostats, n_counted, reads_n, k_ms, a_ms, build_id,
                 "requests_per_launch": int(rq), "achieved_Greq_per_s": round(rate / 1e9, 2),
                 "ceiling_Greq_per_s": c["occ64_3p1gb_Greq_per_s"], "frac": round(rate / 1e9 / c["occ64_3p1gb_Greq_per_s"], 3),
                 "ceiling_source": c["source"]}
+        if "write_bytes_per_launch" in t:
+            out["write_bytes_per_launch"] = t["write_bytes_per_launch"]
+        sq = t.get("sq")
+        if sq:  # issue-side counters of the same kernel, build and workload (tools/traffic.py pass 3)
+            n_ext = ostats["n_ext"] / max(n_counted, 1) * reads_n
+            wc = max(sq.get("SQ_WAVE_CYCLES", 0.0), 1.0)
+            out["sq_counters"] = {
+                "valu_per_extend": round(sq["SQ_INSTS_VALU"] / n_ext, 2),
+                "salu_per_extend": round(sq["SQ_INSTS_SALU"] / n_ext, 2),
+                "valu_salu_per_extend": round((sq["SQ_INSTS_VALU"] + sq["SQ_INSTS_SALU"]) / n_ext, 2),
+                "active_inst_any_frac": round(sq["SQ_ACTIVE_INST_ANY"] / wc, 3),
+                "wait_any_frac": round(sq["SQ_WAIT_ANY"] / wc, 3),
+                "per_launch": sq,
+                "what": "SQ_INSTS_VALU / SALU per bwt_extend (extends per read from the restatement x reads), "
+                        "SQ_ACTIVE_INST_ANY and SQ_WAIT_ANY over SQ_WAVE_CYCLES (all quad-cycles), one launch "
+                        "alone, counted by rocprofv3 on this kernel_id + variant"}
     return out
 
 
@@ -945,24 +984,25 @@ def time_seeding(args, d, gpu, reads, opt) -> dict:
             "compact_alone": compact_alone}
 
 
-def human_like_report(args, d, cores) -> dict:
-    """The same step on the human-like repeat profile (--genome-profile human:
-    ~46 % interspersed repeats + satellites, closer to human_g1k_v37 than the
-    uniform profile of the headline), same read seeds and sizes: value, busy
-    time, roofline fraction, request fraction (when tools/traffic.py recorded
-    this build on this workload), extends per read, parity sample and the
-    reference's CPU rate on a sample of these reads.  Its own index (cached
-    like the headline's)."""
+def profile_report(args, d, cores, profile: str) -> dict:
+    """The same step on the other genome profile (the headline runs the
+    human-like one: ~46 % interspersed repeats + satellites, the closer
+    stand-in for human_g1k_v37; beside it the uniform profile of rounds 1-4),
+    same read seeds and sizes: value, busy time, roofline fraction, request
+    fraction and counters (when tools/traffic.py recorded this kernel on this
+    workload), extends per read, parity sample and the reference's CPU rate on
+    a sample of these reads.  Its own index (cached like the headline's)."""
     import copy
     import smemgpu
     h = copy.copy(args)
-    h.genome_profile = "human"
-    h.traffic_json = os.path.join(os.path.dirname(args.traffic_json), "traffic_human.json")
+    h.genome_profile = profile
+    h.traffic_json = traffic_path(profile)
     t = time.time()
     idx, idx_path, sa, genome_codes = get_index(h, d.rank, d.barrier, d.gpu)
     t_index = time.time() - t
     reads = make_reads(h, d.rank, genome_codes, d.world)
     gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu, variant=args.variant, kmer_k=args.kmer_k)
+    gpu_variant = gpu.variant
     opt = smemgpu.Options(min_seed_len=args.min_seed_len)
     T = time_seeding(h, d, gpu, reads, opt)
     h.cpu_seconds = min(args.cpu_seconds, 10.0)
@@ -970,18 +1010,22 @@ def human_like_report(args, d, cores) -> dict:
     T["batch"].close()
     gpu.close()
     rf = roofline(h, bpr, bpr64, ostats, n_counted, reads.n, T["k_ms"], T["a_ms"], smemgpu.build_id(), T["busy_ms"],
-                  T["clock_check"], {"grid": T["st"]["grid"], "block": T["st"]["block"]})
+                  T["clock_check"], {"grid": T["st"]["grid"], "block": T["st"]["block"], "variant": gpu_variant})
     out = {"value": round(T["value"], 1), "unit": "reads/s", "ms_per_step": round(T["elapsed_max"] / args.steps * 1e3, 3),
-           "steps": args.steps, "genome_profile": "human", "reads": reads.n, "read_len": args.read_len,
+           "steps": args.steps, "genome_profile": profile, "reads": reads.n, "read_len": args.read_len,
            "kernel_busy_ms": rf["kernel_busy_ms"], "kernel_ms_alone": rf["kernel_ms_alone"],
            "frac": rf["frac"], "frac_alone": rf["frac_alone"], "achieved_GBps": rf["achieved"],
            "bytes_per_read": rf["bytes_per_read"], "extends_per_read": rf["extends_per_read"],
            "request_frac": (rf.get("request_roofline") or {}).get("frac"),
            "request_roofline": rf.get("request_roofline"),
+           "traffic": rf.get("traffic"), "write_bytes_per_launch": rf.get("write_bytes_per_launch"),
+           "sq_counters": rf.get("sq_counters"), "kernel": rf["kernel"], "kernel_variant": gpu_variant,
            "parity_sample": parity, "cpu_baseline": cpu,
            "index_s": round(t_index, 1),
-           "what": "the headline step on the human-like genome profile (~46 % interspersed repeats shaped like "
-                   "RepeatMasker's classes + 3 % satellites), same sizes and read seeds"}
+           "what": ("the headline step on the human-like genome profile (~46 % interspersed repeats shaped like "
+                    "RepeatMasker's classes + 3 % satellites)" if profile == "human" else
+                    "the headline step on the uniform genome profile (random + 2 % diverged repeat families, exact "
+                    "and tandem repeats: the headline profile of rounds 1-4)") + ", same sizes and read seeds"}
     del idx, sa, genome_codes
     return out
 
@@ -1000,6 +1044,7 @@ def main():
     idx, idx_path, sa, genome_codes = get_index(args, rank, barrier, d.gpu)
     reads = make_reads(args, rank, genome_codes, world)
     gpu = smemgpu.Gpu(idx, device=d.gpu, lanes_per_cu=args.lanes_per_cu, variant=args.variant, kmer_k=args.kmer_k)
+    gpu_variant = gpu.variant
     # the .sa upload + device densification, timed synchronously here (the
     # binding runs it in the background beside bwa's index load)
     os.environ["SMEM_GPU_SYNC_INIT"] = "1"
@@ -1075,10 +1120,11 @@ def main():
                                f"replicated, no collectives; {args.streams} host workers per GPU, each running whole "
                                f"steps on its own stream",
                 "grid": st["grid"], "block": st["block"],
-                "kernel_variant": args.variant or 2, "kmer_k": args.kmer_k,
+                "kernel_variant": gpu_variant, "kernel": kernel_name(gpu_variant), "kmer_k": args.kmer_k,
             },
             "roofline": roofline(args, bpr, bpr64, ostats, n_counted, reads.n, T["k_ms"], T["a_ms"], smemgpu.build_id(),
-                                 T["busy_ms"], T["clock_check"], {"grid": st["grid"], "block": st["block"]}),
+                                 T["busy_ms"], T["clock_check"], {"grid": st["grid"], "block": st["block"],
+                                                                  "variant": gpu_variant}),
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "compact_ms": round(T["compact_alone"], 3),
@@ -1097,7 +1143,7 @@ def main():
         }
     batch.close()
     gpu.close()
-    # the product path end to end and the human-like profile: one GPU (the
+    # the product path end to end and the other genome profile: one GPU (the
     # driver's N=1 line), after the headline's GPU state is released
     if rank == 0 and world == 1:
         if args.e2e_reads > 0:
@@ -1106,9 +1152,10 @@ def main():
                 creads = make_reads(args, 0, genome_codes, 1, args.e2e_chunk_reads, salt=2)
                 out["e2e"]["multi_chunk"] = e2e_chunks_report(args, genome_key(args), creads, cores, d.gpu)
                 del creads
-        if args.human_like and args.genome_profile == "uniform":
+        if args.other_profile:
             del idx, sa
-            out["human_like"] = human_like_report(args, d, cores)
+            other = "uniform" if args.genome_profile == "human" else "human"
+            out["uniform" if other == "uniform" else "human_like"] = profile_report(args, d, cores, other)
     if rank == 0:
         print(json.dumps(out), flush=True)
     d.close()

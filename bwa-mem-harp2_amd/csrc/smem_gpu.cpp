@@ -215,12 +215,18 @@ constexpr uint32_t SA_DENSE_SHIFT = 2;
 constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 2048, CHAIN_HEAVY_LDS = 150 * 1024,
                    CHAIN_REST_LDS = 28 * 1024;
 
+// the seeding kernel a handle starts with: seed_wp_kernel<32 owners, 20 LDS entries>
+// (variant 40; variant 2 is the lane-per-read seed_kernel of rounds 1-4)
+constexpr int kSeedDefault = 40;
+// lanes a launch gives each read: seed_wp_kernel's waves own 32 (variant 42: 24) reads
+static int seed_lanes_per_read(int variant) { return variant == 42 ? 3 : (variant >= 40 ? 2 : 1); }
+
 struct smem_gpu {
     int device = 0;
     int n_cu = 0;
     int lanes_per_cu = 768;  // 3 blocks of 256 per CU: what the default kernel's LDS allows
     int intv_cap = 0;
-    int variant = 2;  // see smem_gpu_set_kernel_variant
+    int variant = kSeedDefault;  // see smem_gpu_set_kernel_variant
     uint32_t* d_bwt = nullptr;      // reference layout (A/B variants 3, 4; freed after the Occ64 re-layout otherwise)
     uint32_t* d_occ64 = nullptr;    // Occ64 layout (default kernel)
     uint32_t* d_occ192 = nullptr;   // Occ192 layout (variant 10)
@@ -668,9 +674,11 @@ int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
         }
         g->d_occ192 = p;
     }
-    g->variant = variant == 0 ? 2 : variant;
+    g->variant = variant == 0 ? kSeedDefault : variant;
     return SMEM_OK;
 }
+
+int smem_gpu_get_kernel_variant(const smem_gpu_t* g) { return g ? g->variant : SMEM_E_ARG; }
 
 int smem_gpu_set_kmer_table(smem_gpu_t* g, int k) {
     g_err[0] = 0;
@@ -797,7 +805,8 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     b->cap_calls = (uint32_t)(max_len / 4 + 16);  // ~6 lists per 150 bp read; more -> overflow pass
     b->cap_list = (uint32_t)max_len + 2;   // forward/backward lists hold <= len+1 intervals
     const int want_lanes = g->n_cu * g->lanes_per_cu;
-    const int read_lanes = (max_reads + 255) / 256 * 256;
+    // seed_wp_kernel owns 32 reads per wave: two lanes per read cover a small batch
+    const int read_lanes = (int)std::min<int64_t>((int64_t)2 * max_reads + 255, INT32_MAX) / 256 * 256;
     b->lanes = std::max(256, std::min(want_lanes, read_lanes));
     int rc = SMEM_OK;
     hipError_t e = hipSuccess;
@@ -942,7 +951,7 @@ static int batch_run_impl(smem_batch_t* b, const smem_opt_t* opt) {
     P.ovf_count = b->d_ctr.p + 1;
     P.ovf_items = b->d_ovf_items.p;
     P.tspan = reinterpret_cast<uint64_t*>(b->d_ctr.p + 4);  // zeroed with the counters below
-    const int lanes = std::min(b->lanes, std::max(256, (n + 255) / 256 * 256));
+    const int lanes = std::min(b->lanes, std::max(256, (n * seed_lanes_per_read(g->variant) + 255) / 256 * 256));
     const int grid = lanes / 256;
     b->stats.grid = grid;
     HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
@@ -983,7 +992,7 @@ static int batch_run_impl(smem_batch_t* b, const smem_opt_t* opt) {
             Q.ovf_count = b->d_ctr.p + 3;
             Q.ovf_items = b->d_ovf_items2.p;
             HIP_TRY(hipMemsetAsync(b->d_ctr.p + 2, 0, 2 * sizeof(int32_t), b->st));
-            const int ql = std::min(b->lanes, (n_ovf + 255) / 256 * 256);
+            const int ql = std::min(b->lanes, (n_ovf * seed_lanes_per_read(g->variant) + 255) / 256 * 256);
             HIP_TRY(smem_launch_seed(&Q, std::max(1, ql / 256), 256, g->variant, b->st));
             HIP_TRY(hipMemcpyAsync(b->h_ctr.p, b->d_ctr.p, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, b->st));
             HIP_TRY(hipStreamSynchronize(b->st));

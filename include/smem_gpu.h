@@ -516,6 +516,14 @@ int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
  * extend result of at most k bases from the k-mer table (needs
  * smem_gpu_set_kmer_table) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
+/* the seeding kernel variant the handle runs (0 given to the setter = the
+ * default, 40: seed_wp_kernel -- the backward steps' entries extended by the
+ * whole wave and pruned by ballot / prefix rank (software/bwt.c:812-826), 32
+ * reads owned per wave, 20 list entries per read in LDS; 41: 16 entries; 42:
+ * 24 reads per wave with 24 entries; 43: 40 without wave priority; 2: the
+ * lane-per-read seed_kernel of rounds 1-4).  SMEM_GPU_SEED_VARIANT in the
+ * environment sets the default of every handle opened afterwards. */
+int  smem_gpu_get_kernel_variant(const smem_gpu_t *gpu);
 /* build (k = 1..15) or free (k = 0) the device table of the bi-intervals of
  * every string of 1..k bases, built on the device from the resident index:
  * 16 B x (4^(k+1) - 4) / 3 (k = 12: 358 MB, 14: 5.7 GB); a table of a string

@@ -9,7 +9,8 @@
 #   tests[:FILTER]    python -m pytest tests -m gpu [-k FILTER] (commas: spaces, e.g. tests:product,or,variants) -> tests.log
 #   smoke             __graft_entry__.smoke()                         -> smoke.log
 #   traffic[:ARGS]    tools/traffic.py for this build (TCC_EA0_RDREQ per launch) -> traffic.json,
-#                     copied to profiles/traffic.json (or profiles/traffic_human.json with --genome-profile,human)
+#                     copied to profiles/traffic_human.json (the default human-like workload) or, with
+#                     --genome-profile,uniform, profiles/traffic.json
 #   bench[:ARGS]      python bench.py ARGS                           -> bench<k>.json / .err
 #   rocprof[:ARGS]    rocprofv3 --kernel-trace --stats over bench.py's timed seeding steps -> prof<k>/
 #   pmc:PASSES[:ARGS] tools/pmc_passes.sh, passes "1,2" of its list, ARGS for tools/prof_run.py (bench workload
@@ -46,14 +47,15 @@ for step in "$@"; do
     traffic)
       timeout -k 10 600 python -u tools/traffic.py --out "$OUT/traffic$k.json" --tmp "$OUT/traffic$k" $args \
         > "$OUT/traffic$k.log" 2>&1 || { echo "traffic failed"; exit $k; }
-      if [[ "$args" == *human* ]]; then cp "$OUT/traffic$k.json" profiles/traffic_human.json
+      prof=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['workload']['genome_profile'])" "$OUT/traffic$k.json")
+      if [ "$prof" = human ]; then cp "$OUT/traffic$k.json" profiles/traffic_human.json
       else cp "$OUT/traffic$k.json" profiles/traffic.json; fi ;;
     bench)
       timeout -k 10 1000 python -u bench.py $args > "$OUT/bench$k.json" 2> "$OUT/bench$k.err" \
         || { echo "bench failed"; tail -5 "$OUT/bench$k.err"; exit $k; } ;;
     rocprof)
       timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof$k" -o run -- \
-        python3 -u bench.py --stream-reads -1 --parity 0 --side-stages 0 --cpu-seconds 0 --e2e-reads 0 --human-like 0 \
+        python3 -u bench.py --stream-reads -1 --parity 0 --side-stages 0 --cpu-seconds 0 --e2e-reads 0 --other-profile 0 \
         $args > "$OUT/prof$k.json" 2> "$OUT/prof$k.err" || { echo "rocprof failed"; exit $k; } ;;
     pmc)
       passes=${arg%%:*}

@@ -17,6 +17,6 @@ PASSES=(
 SEL=${PMC_PASSES:-$(seq 0 $((${#PASSES[@]} - 1)))}  # e.g. PMC_PASSES="0 1 2"
 for i in $SEL; do
   P=${PASSES[$i]}
-  timeout -k 10 240 rocprofv3 --pmc $P --kernel-include-regex ${PMC_KERNEL:-seed_kernel} --output-format csv -d "$OUT" -o pass$i -- python ${PMC_PROG:-tools/prof_run.py} "$@" > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  timeout -k 10 240 rocprofv3 --pmc $P --kernel-include-regex ${PMC_KERNEL:-'seed_(wp_)?kernel'} --output-format csv -d "$OUT" -o pass$i -- python ${PMC_PROG:-tools/prof_run.py} "$@" > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
 done
 echo "all passes ok"

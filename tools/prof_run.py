@@ -2,7 +2,7 @@
 cache) and the bench's own resident reads (bench.make_reads: same blocks,
 seeds and options), seeded --launches times.  Meant to run under
 
-    rocprofv3 --pmc <counters> --kernel-include-regex seed_kernel -- python tools/prof_run.py [bench args]
+    rocprofv3 --pmc <counters> --kernel-include-regex 'seed_(wp_)?kernel' -- python tools/prof_run.py [bench args]
 
 Any bench.py argument selects the workload (--config, --genome-profile,
 --reads, --genome-mbp ...); --launches is this tool's own (--variant / --kmer-k are bench's).
@@ -40,7 +40,7 @@ def main():
         st = b.stats()
         with open(own.stats_out, "w") as fh:
             json.dump({"grid": st["grid"], "block": st["block"], "build_id": smemgpu.build_id(),
-                       "kernel_id": smemgpu.kernel_id()}, fh)
+                       "kernel_id": smemgpu.kernel_id(), "variant": gpu.variant}, fh)
     b.close()
     gpu.close()
 

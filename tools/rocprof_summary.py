@@ -28,13 +28,14 @@ def main():
     p.add_argument("trace")
     p.add_argument("bench_json")
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--kernel", default="seed_kernel")
+    p.add_argument("--kernel", default="seed_", help="kernel-name substring (seed_kernel / seed_wp_kernel)")
     p.add_argument("--cmd", default="")
     a = p.parse_args()
     spans = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
-            if a.kernel in r["Kernel_Name"]:
+            if a.kernel in r["Kernel_Name"] and ("seed_kernel" in r["Kernel_Name"] or "seed_wp_kernel" in r["Kernel_Name"]
+                                                 or a.kernel != "seed_"):
                 spans.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     spans.sort()
     b = json.load(open(a.bench_json))

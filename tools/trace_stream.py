@@ -34,7 +34,7 @@ def main():
     for k in K:
         k["a"], k["b"] = int(k["Start_Timestamp"]), int(k["End_Timestamp"])
     K.sort(key=lambda k: k["a"])
-    seed = [k for k in K if "seed_kernel" in k["Kernel_Name"]]
+    seed = [k for k in K if "seed_kernel" in k["Kernel_Name"] or "seed_wp_kernel" in k["Kernel_Name"]]
     if a.last:
         s = seed[-a.last:]
     else:  # the last run of launches without a 50 ms gap

@@ -9,6 +9,7 @@ kernel's own sources and flags) and launch shape match, for runtime-only changes
 
   pass 1: TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum  -- L2 fabric read requests
   pass 2: WRITE_SIZE
+  pass 3: SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES
 
 Calibration (profiles/r02/probe/fetch_size_calibration.txt): on random 16-B
 and 32-B gathers of known count, TCC_EA0_RDREQ counts exactly one request per
@@ -32,7 +33,7 @@ sys.path.insert(0, ROOT)
 
 def run_pass(counters: list, out_dir: str, rest: list, extra: list = ()) -> dict:
     d = os.path.join(out_dir, "_".join(c.split("_")[0] + str(i) for i, c in enumerate(counters)))
-    cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", *counters, "--kernel-include-regex", "seed_kernel",
+    cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", *counters, "--kernel-include-regex", "seed_(wp_)?kernel",
            "--output-format", "csv", "-d", d, "-o", "p", "--", sys.executable, os.path.join(ROOT, "tools", "prof_run.py"),
            "--launches", "1", *extra, *rest]
     subprocess.run(cmd, check=True)
@@ -58,16 +59,22 @@ def main():
     r1 = run_pass(["TCC_EA0_RDREQ_sum", "TCC_HIT_sum", "TCC_MISS_sum"], own.tmp, rest)
     launch_json = os.path.join(own.tmp, "launch.json")
     r2 = run_pass(["WRITE_SIZE"], own.tmp, rest, ["--stats-out", launch_json])
+    sq_names = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES",
+                "SQ_BUSY_CYCLES", "SQ_WAVES"]
+    r3 = run_pass(sq_names, own.tmp, rest)
     with open(launch_json) as fh:
         launch = json.load(fh)
     out = {"rdreq_per_launch": r1["TCC_EA0_RDREQ_sum"][0], "tcc_hit_per_launch": r1["TCC_HIT_sum"][0],
            "tcc_miss_per_launch": r1["TCC_MISS_sum"][0], "write_bytes_per_launch": r2["WRITE_SIZE"][0] * 1024.0,
-           "dispatches": [r1["TCC_EA0_RDREQ_sum"][1], r2["WRITE_SIZE"][1]],
-           "counter": "TCC_EA0_RDREQ_sum (L2 -> fabric read requests), TCC_HIT/MISS_sum, WRITE_SIZE x 1024",
+           "dispatches": [r1["TCC_EA0_RDREQ_sum"][1], r2["WRITE_SIZE"][1], r3["SQ_WAVES"][1]],
+           "counter": "TCC_EA0_RDREQ_sum (L2 -> fabric read requests), TCC_HIT/MISS_sum, WRITE_SIZE x 1024; "
+                      "sq: SQ_* per launch (instructions; *_CYCLES / WAIT / ACTIVE in quad-cycles)",
+           "sq": {k: r3[k][0] for k in sq_names if k in r3},
            "workload": {"genome_mbp": a.genome_mbp, "reads": a.reads, "read_len": a.read_len, "seed": a.seed,
                         "sub": a.sub, "genome_profile": a.genome_profile},
            "build_id": launch["build_id"],  # the library the counted launches ran on
            "kernel_id": launch["kernel_id"],
+           "variant": launch.get("variant"),  # the seeding kernel the counted launches ran
            "launch": {"grid": launch["grid"], "block": launch["block"]},
            "measured": time.strftime("%Y-%m-%d %H:%M:%S")}
     os.makedirs(os.path.dirname(own.out) or ".", exist_ok=True)
