@@ -215,16 +215,33 @@ constexpr uint32_t SA_DENSE_SHIFT = 2;
 constexpr uint32_t CHAIN_HEAVY_MIN = 16, CHAIN_GIANT_MIN = 2048, CHAIN_HEAVY_LDS = 150 * 1024,
                    CHAIN_REST_LDS = 28 * 1024;
 
-// the seeding kernel a handle starts with: seed_wp_kernel<32 owners, 20 LDS entries>
-// (variant 40; variant 2 is the lane-per-read seed_kernel of rounds 1-4)
-constexpr int kSeedDefault = 40;
+// the seeding kernel a handle starts with: seed_wp_kernel<24 owners per wave, 18 LDS
+// list entries, 4 blocks per CU> (variant 49; variant 2 is the
+// lane-per-read seed_kernel of rounds 1-4)
+constexpr int kSeedDefault = 49;
+// the persistent grid's lanes per CU when the caller sets none: 4 blocks of 256
+// fit the 4-block variants' LDS, but a grid of exactly 4 per CU leaves no VGPR
+// room for the finalize / compaction kernels of another batch (measured: the
+// steps then serialise), so 3.75 (profiles/r05/ab_wp)
+static int seed_lanes_per_cu(int variant) {
+    switch (variant) {
+        case 44: case 45: case 46: case 49: case 50: case 51: return 960;
+        default: return 768;
+    }
+}
 // lanes a launch gives each read: seed_wp_kernel's waves own 32 (variant 42: 24) reads
-static int seed_lanes_per_read(int variant) { return variant == 42 ? 3 : (variant >= 40 ? 2 : 1); }
+static int seed_lanes_per_read(int variant) {
+    switch (variant) {
+        case 42: case 44: case 48: case 49: case 51: return 3;  // 24 owners per wave
+        case 50: return 4;                                     // 20
+        default: return variant >= 40 ? 2 : 1;
+    }
+}
 
 struct smem_gpu {
     int device = 0;
     int n_cu = 0;
-    int lanes_per_cu = 768;  // 3 blocks of 256 per CU: what the default kernel's LDS allows
+    int lanes_per_cu = 0;  // 0: the seeding kernel's own (seed_lanes_per_cu)
     int intv_cap = 0;
     int variant = kSeedDefault;  // see smem_gpu_set_kernel_variant
     uint32_t* d_bwt = nullptr;      // reference layout (A/B variants 3, 4; freed after the Occ64 re-layout otherwise)
@@ -645,13 +662,13 @@ int smem_gpu_init(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bw
 
 int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
     if (!g) return SMEM_E_ARG;
-    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 768;
+    g->lanes_per_cu = lanes_per_cu > 0 ? std::max(64, lanes_per_cu / 64 * 64) : 0;
     return SMEM_OK;
 }
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
     g_err[0] = 0;
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31) || (variant >= 40 && variant <= 43)))
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31) || (variant >= 40 && variant <= 51)))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
 
     if (!smem_seed_variant_built(variant))
@@ -804,7 +821,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     b->cap_intv = g->intv_cap > 0 ? (uint32_t)g->intv_cap : (uint32_t)std::max(32, max_len / 2 + 32);
     b->cap_calls = (uint32_t)(max_len / 4 + 16);  // ~6 lists per 150 bp read; more -> overflow pass
     b->cap_list = (uint32_t)max_len + 2;   // forward/backward lists hold <= len+1 intervals
-    const int want_lanes = g->n_cu * g->lanes_per_cu;
+    const int want_lanes = g->n_cu * (g->lanes_per_cu > 0 ? g->lanes_per_cu : seed_lanes_per_cu(g->variant));
     // seed_wp_kernel owns 32 reads per wave: two lanes per read cover a small batch
     const int read_lanes = (int)std::min<int64_t>((int64_t)2 * max_reads + 255, INT32_MAX) / 256 * 256;
     b->lanes = std::max(256, std::min(want_lanes, read_lanes));

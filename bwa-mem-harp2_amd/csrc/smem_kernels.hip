@@ -1319,7 +1319,8 @@ struct WpWave {
     uint4 d0[OWN];        // step descriptors: j, curr_n, prev_off, c | lr << 2 | last_x2 bits 32-33 << 8
     uint4 d1[OWN];        // min_intv, last_x2 low word
     uint4 q[OWN];         // query windows (LDS-DMA landing slots)
-    uint64_t res[64];     // extend result sizes by lane
+    uint64_t res[64];     // extend result sizes by lane (PAIR: of the lane's last entry)
+    uint64_t res1[64];    // PAIR: of the lane's first entry
     uint32_t tabS[64];    // owner whose segment starts at task position p (0xFF: none)
     uint32_t tabP[64];    // free-lane rank -> lane
 };
@@ -1350,8 +1351,11 @@ __device__ __forceinline__ void wave_lds_fence() {
     asm volatile("" ::: "memory");
 }
 
-template <int OWN, int NL, int PRIO>
-__global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
+// PAIR: a worker lane takes two consecutive entries of a step (two extends
+// in flight per lane: twice the requests per wave-iteration)
+template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false>
+__global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
+    constexpr uint32_t PR = PAIR ? 2u : 1u;  // entries per worker lane
     static_assert(OWN >= 1 && OWN <= 64 && NL >= 2 && NL < 32, "owners per wave / list entries");
     __shared__ WpWave<OWN, NL> wlds[4];
     WpWave<OWN, NL>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
@@ -1626,19 +1630,20 @@ __global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
         if (!__any(phase != P_EXIT)) break;
         const bool fwdreq = out && phase == P_FWD_RES;
         const uint32_t rem = phase == P_BWD_WAIT ? prev_n - j : 0u;
+        const uint32_t slots = (rem + PR - 1) / PR;  // worker lanes the step still needs
         if (rem) {  // what a worker needs of this owner's step
             L->d0[me] = make_uint4(j, curr_n, prev_off,
                                    (uint32_t)cur_c | lr << 2 | (uint32_t)(last_x2 >> 32) << 8);
-            L->d1[me] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, 0u, 0u);
+            L->d1[me] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, prev_n, 0u);
         }
         // the owners' remaining entries laid out in lane order over the free lanes
-        const uint32_t incl = wave_scan_add(rem);
-        const uint32_t excl = incl - rem;
+        const uint32_t incl = wave_scan_add(slots);
+        const uint32_t excl = incl - slots;
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint64_t fmask = ~(uint64_t)__ballot(fwdreq);
         const uint32_t nfree = (uint32_t)__popcll(fmask);
         const uint32_t ntask = total < nfree ? total : nfree;
-        const uint32_t take = (rem && excl < nfree) ? min(rem, nfree - excl) : 0u;
+        const uint32_t take = (slots && excl < nfree) ? min(slots, nfree - excl) : 0u;
         const bool freel = (fmask >> me) & 1;
         const uint32_t rank = mbcnt64(fmask);
         L->tabS[me] = 0xFFu;
@@ -1649,13 +1654,14 @@ __global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
         const uint64_t marks = __ballot(L->tabS[me] != 0xFFu);
         const bool worker = freel && rank < ntask;
         uint32_t s = 0, o = 0, jj = 0, lro = 0;
-        uint4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0}, ent = {0, 0, 0, 0};
+        bool has2 = false;
+        uint4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0}, ent = {0, 0, 0, 0}, ent2 = {0, 0, 0, 0};
         if (worker) {
             s = (uint32_t)hibit64(marks & ((2ull << rank) - 1ull));  // the segment holding task `rank`
             o = L->tabS[s];
             w0 = L->d0[o];
             w1 = L->d1[o];
-            jj = w0.x + (rank - s);
+            jj = w0.x + PR * (rank - s);
             lro = (w0.w >> 2) & 31u;
             if (jj < (uint32_t)NL) {
                 ent = L->e[WSLOT(lro, jj)][o];
@@ -1663,6 +1669,18 @@ __global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
                 const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
                 const uint32_t at = w0.z + jj;
                 ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+            }
+            if constexpr (PAIR) {
+                has2 = jj + 1 < w1.z;
+                if (has2) {
+                    if (jj + 1 < (uint32_t)NL) {
+                        ent2 = L->e[WSLOT(lro, jj + 1)][o];
+                    } else {
+                        const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                        const uint32_t at = w0.z + jj + 1;
+                        ent2 = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+                    }
+                }
             }
         }
         // the query window for owners that want one
@@ -1691,6 +1709,29 @@ __global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
                 l1 = *reinterpret_cast<const uint4*>(a1);
             }
         }
+        // PAIR: the lane's second entry (same base), its buckets in flight beside the first's
+        uint64_t ra2 = 0, rb2 = 0, rs2 = 0, kk2 = 0, ll2 = 0;
+        uint32_t bk2 = 0, bl2 = 0;
+        uint4 m0 = {0, 0, 0, 0}, m1 = {0, 0, 0, 0}, n0 = {0, 0, 0, 0}, n1 = {0, 0, 0, 0};
+        if constexpr (PAIR) {
+            if (has2) {
+                ra2 = p_x0(ent2), rb2 = p_x1(ent2), rs2 = p_x2(ent2);
+                const uint64_t k2 = ra2 - 1, l2 = k2 + rs2;
+                kk2 = k2 - (k2 >= P.primary), ll2 = l2 - (l2 >= P.primary);
+                if (kk2 >= P.L2[4]) kk2 = 0;
+                if (ll2 >= P.L2[4]) ll2 = 0;
+                bk2 = (uint32_t)(kk2 >> 6), bl2 = (uint32_t)(ll2 >> 6);
+                const uint32_t *a0, *a1;
+                block_chunks<false>(P.occ64, bk2, a0, a1);
+                m0 = *reinterpret_cast<const uint4*>(a0);
+                m1 = *reinterpret_cast<const uint4*>(a1);
+                if (bl2 != bk2) {
+                    block_chunks<false>(P.occ64, bl2, a0, a1);
+                    n0 = *reinterpret_cast<const uint4*>(a0);
+                    n1 = *reinterpret_cast<const uint4*>(a1);
+                }
+            }
+        }
         if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (ld_q) {
@@ -1702,43 +1743,66 @@ __global__ __launch_bounds__(256, 3) void seed_wp_kernel(SeedParams P) {
             const Bucket32 wl = bl != bk ? Bucket32{l0, l1} : wk;
             extend_counts64<false>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
         }
+        uint64_t na2 = 0, nb2 = 0, ns2 = 0;
+        if constexpr (PAIR) {
+            if (has2) {
+                const Bucket32 wk{m0, m1};
+                const Bucket32 wl = bl2 != bk2 ? Bucket32{n0, n1} : wk;
+                extend_counts64<false>(P, ra2, rb2, rs2, rc, kk2, ll2, wk, wl, na2, nb2, ns2);
+            }
+        }
         // ---- the backward results: survive, dedup, rank, write into curr ----
+        // entries of a segment in order: lane by lane, (PAIR) first then second entry
         const bool surv = worker && ns >= (uint64_t)w1.x;
+        const bool surv2 = PAIR && has2 && ns2 >= (uint64_t)w1.x;
         const uint64_t smask = __ballot(surv);
-        L->res[me] = ns;
+        const uint64_t smask2 = PAIR ? (uint64_t)__ballot(surv2) : 0ull;
+        L->res[me] = PAIR && has2 ? ns2 : ns;  // the lane's last entry
+        if constexpr (PAIR) L->res1[me] = ns;
         wave_lds_fence();
         bool keep = false;
         if (surv) {
             if (rank == s) {  // first entry of this chunk: against the last entry kept before it
                 const uint64_t lx = (uint64_t)((w0.w >> 8) & 3u) << 32 | w1.y;
                 keep = w0.y == 0 || ns != lx;
-            } else {          // against the previous entry (the previous free lane)
+            } else {          // against the previous entry: the previous free lane's last one
                 const int pp = hibit64(fmask & ((1ull << me) - 1ull));
-                keep = !((smask >> pp) & 1) || ns != L->res[pp];
+                keep = !(((PAIR ? smask2 : smask) >> pp) & 1) || ns != L->res[pp];
             }
         }
+        const bool keep2 = surv2 && (!surv || ns2 != ns);
         const uint64_t kmask = __ballot(keep);
-        if (keep) {
+        const uint64_t kmask2 = PAIR ? (uint64_t)__ballot(keep2) : 0ull;
+        if (keep || keep2) {
             const uint32_t pf = L->tabP[s];
-            const uint32_t kr = (uint32_t)__popcll(kmask & ((1ull << me) - 1ull) & ~((1ull << pf) - 1ull));
-            const uint32_t idx = w0.y + kr;
-            const uint4 e = pack_p(na, nb, ns, p_end(ent));
-            if (idx < (uint32_t)NL) {
-                L->e[WSLOT(lro, idx)][o] = e;
-            } else if (idx < cap) {
-                PIntv* obp = reinterpret_cast<PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
-                *reinterpret_cast<uint4*>(obp + cap + idx) = e;
+            const uint64_t before = (1ull << me) - 1ull & ~((1ull << pf) - 1ull);
+            const uint32_t kr = (uint32_t)(__popcll(kmask & before) + __popcll(kmask2 & before));
+            PIntv* obp = reinterpret_cast<PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+            if (keep) {
+                const uint32_t idx = w0.y + kr;
+                const uint4 e = pack_p(na, nb, ns, p_end(ent));
+                if (idx < (uint32_t)NL) L->e[WSLOT(lro, idx)][o] = e;
+                else if (idx < cap) *reinterpret_cast<uint4*>(obp + cap + idx) = e;
+            }
+            if (PAIR && keep2) {
+                const uint32_t idx = w0.y + kr + (keep ? 1u : 0u);
+                const uint4 e = pack_p(na2, nb2, ns2, p_end(ent2));
+                if (idx < (uint32_t)NL) L->e[WSLOT(lro, idx)][o] = e;
+                else if (idx < cap) *reinterpret_cast<uint4*>(obp + cap + idx) = e;
             }
         }
         // ---- owners whose entries ran: the chunk's outcome ----
         if (take) {
             const uint32_t pf = L->tabP[excl], pl = L->tabP[excl + take - 1];
             const uint64_t seg = ((2ull << pl) - 1ull) & ~((1ull << pf) - 1ull);
-            const uint64_t km = kmask & seg;
+            const uint64_t km = kmask & seg, km2 = kmask2 & seg;
             if (j == 0) fail0 = !((smask >> pf) & 1);
-            if (km) last_x2 = L->res[hibit64(km)];
-            curr_n += (uint32_t)__popcll(km);
-            j += take;
+            if (km | km2) {  // the last entry kept: the highest lane's second entry if it kept one
+                const int hb = hibit64(km | km2);
+                last_x2 = ((km2 >> hb) & 1) ? L->res[hb] : (PAIR ? L->res1[hb] : L->res[hb]);
+            }
+            curr_n += (uint32_t)(__popcll(km) + __popcll(km2));
+            j += min(rem, PR * take);
             if (j == prev_n) phase = P_BWD_DONE;
         }
         wave_lds_fence();  // this iteration's LDS reads before the next one's writes
@@ -1836,7 +1900,7 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
-    if (variant >= 40 && variant <= 43) return 1;  // seed_wp_kernel
+    if (variant >= 40 && variant <= 51) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
     return variant == 0 || (variant >= 2 && variant <= 31);
 #else
@@ -1869,6 +1933,17 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 41: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 16, 1>), dim3(grid), dim3(block), 0, st, *P); break;
         case 42: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 24, 1>), dim3(grid), dim3(block), 0, st, *P); break;
         case 43: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 0>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 44-46: 4 blocks (16 waves) per CU with shorter lists: <24 owners, 16 entries>, <32, 12>, <28, 14>
+        case 44: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 16, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 45: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 12, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 46: hipLaunchKernelGGL((smem::seed_wp_kernel<28, 14, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 47-48: two entries per worker lane (PAIR): <32, 20>, <24, 24> (3 blocks per CU)
+        case 47: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 1, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 48: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 24, 1, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 49-51: 4 blocks per CU: <24, 18>, <20, 22>, 44 without wave priority
+        case 49: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 50: hipLaunchKernelGGL((smem::seed_wp_kernel<20, 22, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 51: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 16, 0, 4>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

@@ -489,15 +489,18 @@ typedef struct {
 } smem_batch_stats_t;
 int  smem_batch_stats(const smem_batch_t *b, smem_batch_stats_t *st);
 
-/* tuning knobs (0 = default) — lanes per CU of the persistent seeding grid */
+/* tuning knobs (0 = default) — lanes per CU of the persistent seeding grid
+ * (default: the kernel's own -- 960 for the 4-block seed_wp_kernel variants,
+ * 768 otherwise) */
 int  smem_gpu_set_lanes_per_cu(smem_gpu_t *gpu, int lanes_per_cu);
 /* per-read output capacity (intervals) of batches created afterwards;
  * reads needing more go through the overflow pass (0 = len/2 + 32) */
 int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
 /* seeding-kernel variant, all bit-exact, kept for A/B measurement (the
- * product build has 0 = 2 = 20 = 26, 9, 23, 24, 25, 27 and 28; the others need a library built with
- * `make AB=1`, else SMEM_E_ARG):
- * 2 (default, also 0) Occ64 buckets (32 B per 64 symbols, re-laid on the
+ * product build has 0 = 49 (the default, seed_wp_kernel: see
+ * smem_gpu_get_kernel_variant below for 40-51), 2 = 20 = 26, 9, 23, 24, 25, 27
+ * and 28; the others need a library built with `make AB=1`, else SMEM_E_ARG):
+ * 2 (the default of rounds 1-4) Occ64 buckets (32 B per 64 symbols, re-laid on the
  * device at init), per-lane fetch into two register slots with bucket reuse,
  * the first 11 entries of every list in LDS (the forward list as a ring of its
  * last 11 pushes); 11 the same with LDS-DMA slots and 7 list entries; 12 that
@@ -517,11 +520,13 @@ int  smem_gpu_set_intv_cap(smem_gpu_t *gpu, int cap_per_read);
  * smem_gpu_set_kmer_table) */
 int  smem_gpu_set_kernel_variant(smem_gpu_t *gpu, int variant);
 /* the seeding kernel variant the handle runs (0 given to the setter = the
- * default, 40: seed_wp_kernel -- the backward steps' entries extended by the
- * whole wave and pruned by ballot / prefix rank (software/bwt.c:812-826), 32
- * reads owned per wave, 20 list entries per read in LDS; 41: 16 entries; 42:
- * 24 reads per wave with 24 entries; 43: 40 without wave priority; 2: the
- * lane-per-read seed_kernel of rounds 1-4).  SMEM_GPU_SEED_VARIANT in the
+ * default, 49: seed_wp_kernel -- the backward steps' entries extended by the
+ * whole wave and pruned by ballot / prefix rank (software/bwt.c:812-826), 24
+ * reads owned per wave, 18 list entries per read in LDS, 4 blocks per CU.
+ * A/B: 40 32 reads / 20 entries / 3 blocks; 41 32 / 16; 42 24 / 24; 43 = 40
+ * without wave priority; 44 24 / 16 / 4 blocks; 45 32 / 12; 46 28 / 14; 47, 48
+ * two entries per worker lane; 50 20 / 22; 51 = 44 without wave priority; 2:
+ * the lane-per-read seed_kernel of rounds 1-4).  SMEM_GPU_SEED_VARIANT in the
  * environment sets the default of every handle opened afterwards. */
 int  smem_gpu_get_kernel_variant(const smem_gpu_t *gpu);
 /* build (k = 1..15) or free (k = 0) the device table of the bi-intervals of
