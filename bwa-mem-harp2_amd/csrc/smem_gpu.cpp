@@ -230,13 +230,18 @@ static int seed_lanes_per_cu(int variant) {
     }
 }
 // lanes a launch gives each read: seed_wp_kernel's waves own 32 (variant 42: 24) reads
-static int seed_lanes_per_read(int variant) {
+// reads a wave of the seeding kernel owns at once (seed_wp_kernel<OWN, ...>; seed_kernel: one per lane)
+static int seed_owners_per_wave(int variant) {
     switch (variant) {
-        case 42: case 44: case 48: case 49: case 51: return 3;  // 24 owners per wave
-        case 50: return 4;                                     // 20
-        default: return variant >= 40 ? 2 : 1;
+        case 40: case 41: case 43: case 45: case 47: return 32;
+        case 42: case 44: case 48: case 49: case 51: return 24;
+        case 46: return 28;
+        case 50: return 20;
+        default: return 64;
     }
 }
+// lanes a launch gives each read so that every owner of a small batch's grid has one
+static int seed_lanes_per_read(int variant) { return (64 + seed_owners_per_wave(variant) - 1) / seed_owners_per_wave(variant); }
 
 struct smem_gpu {
     int device = 0;
@@ -696,6 +701,15 @@ int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
 }
 
 int smem_gpu_get_kernel_variant(const smem_gpu_t* g) { return g ? g->variant : SMEM_E_ARG; }
+
+int smem_gpu_grid_reads(const smem_gpu_t* g) {
+    if (!g) return SMEM_E_ARG;
+    int n_cu = g->n_cu;
+    if (n_cu <= 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess)
+        return SMEM_E_DEVICE;
+    const int lpc = g->lanes_per_cu > 0 ? g->lanes_per_cu : seed_lanes_per_cu(g->variant);
+    return (int)((int64_t)n_cu * lpc / 64 * seed_owners_per_wave(g->variant));
+}
 
 int smem_gpu_set_kmer_table(smem_gpu_t* g, int k) {
     g_err[0] = 0;

@@ -25,7 +25,7 @@ EXPORTED = [
     "smem_gpu_device_count", "smem_gpu_init", "smem_gpu_shutdown", "smem_gpu_collect",
     "smem_batch_create", "smem_batch_destroy", "smem_batch_set_reads", "smem_batch_set_reads_packed",
     "smem_batch_run", "smem_batch_fetch", "smem_batch_read", "smem_batch_results", "smem_batch_stats",
-    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_gpu_get_kernel_variant", "smem_gpu_set_kmer_table", "smem_batch_debug", "smem_strerror",
+    "smem_gpu_set_lanes_per_cu", "smem_gpu_set_intv_cap", "smem_gpu_set_kernel_variant", "smem_gpu_get_kernel_variant", "smem_gpu_grid_reads", "smem_gpu_set_kmer_table", "smem_batch_debug", "smem_strerror",
     "smem_gpu_build_id",
     "smem_bwt_build_sa", "smem_bwt_build_gpu_sa", "smem_sa_read", "smem_sa_write", "smem_sa_free", "smem_gpu_load_sa",
     "smem_batch_sa", "smem_batch_sa_results",
@@ -224,6 +224,8 @@ def load() -> C.CDLL:
     lib.smem_gpu_set_kernel_variant.argtypes = [C.c_void_p, C.c_int]
     lib.smem_gpu_get_kernel_variant.argtypes = [C.c_void_p]
     lib.smem_gpu_get_kernel_variant.restype = C.c_int
+    lib.smem_gpu_grid_reads.argtypes = [C.c_void_p]
+    lib.smem_gpu_grid_reads.restype = C.c_int
     lib.smem_gpu_set_kmer_table.argtypes = [C.c_void_p, C.c_int]
     if hasattr(lib, "smem_batch_debug"):  # absent from older A/B builds
         lib.smem_batch_debug.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
@@ -495,6 +497,11 @@ class Gpu:
     def set_variant(self, variant: int) -> None:
         """Seeding-kernel variant (0 = default; see smem_gpu_set_kernel_variant)."""
         _check(load().smem_gpu_set_kernel_variant(self._h, variant), "smem_gpu_set_kernel_variant")
+
+    @property
+    def grid_reads(self) -> int:
+        """Reads one seeding launch holds in flight (smem_gpu_grid_reads)."""
+        return int(load().smem_gpu_grid_reads(self._h))
 
     @property
     def variant(self) -> int:

@@ -200,13 +200,21 @@ int  smem_gpu_collect_ex(smem_gpu_t *gpu, int slot, int n_reads, const uint8_t *
 /* Pre-size worker slots [0, n_slots) of smem_gpu_collect_ex for batches of up
  * to reads_per_slot reads of up to max_len bases, with the later stages'
  * scratch and pinned result buffers sized at generous per-read estimates, and
- * run one warm-up pass of every stage over a few reads cut from the resident
- * .pac (a kernel's code object loads on its first launch).  Replaces the
+ * load the code object of every kernel file (hipFuncGetAttributes: a kernel's
+ * code object otherwise loads on its first launch); SMEM_GPU_WARMUP=full runs
+ * one warm-up pass of every stage over a few reads cut from the resident .pac
+ * instead.  Replaces the
  * per-worker buffers main_mem allocates before the first chunk
  * (software/fastmap.c:207-210).  Runs on a background host thread: the call
  * returns at once, and the first smem_gpu_collect* on the device waits for it.
  * A batch larger than reserved is re-created on first use, as without it. */
 int  smem_gpu_reserve_slots(smem_gpu_t *gpu, int n_slots, int reads_per_slot, int max_len);
+/* Reads one seeding launch holds in flight on the device at once: the
+ * persistent grid's read owners (CUs x lanes per CU x owners per wave / 64;
+ * 92,160 for the default kernel on MI355X).  A worker batch of at least this
+ * many reads fills the device by itself (the binding's batch plan).
+ * Needs no open device work: the CU count comes from the device's attributes. */
+int  smem_gpu_grid_reads(const smem_gpu_t *gpu);
 /* Admission, the HARP manager's role (software/fastmap.c:320-429): at most n
  * calls run work on the device at once, each on one of n leased stream pairs
  * (a device carries at most 2n streams however many workers share it); the

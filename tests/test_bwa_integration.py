@@ -119,8 +119,9 @@ def _golden(g, kind) -> list:
 
 
 def _run(fa, g, kind, threads, batch, env=None):
-    args = [BWA, "mem", "-t", str(threads), "-b", str(batch)] + (["-p"] if kind == "pe" else []) + \
-           [fa, os.path.join(GOLD, "sam", f"{g}_{kind}.fq.gz")]
+    """batch None: no -b (the binding's batch plan)."""
+    args = [BWA, "mem", "-t", str(threads)] + ([] if batch is None else ["-b", str(batch)]) + \
+           (["-p"] if kind == "pe" else []) + [fa, os.path.join(GOLD, "sam", f"{g}_{kind}.fq.gz")]
     p = subprocess.run(args, capture_output=True, text=True, env=dict(os.environ, **(env or {})), timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     return [l for l in p.stdout.split("\n") if l and not l.startswith("@PG")], p.stderr
@@ -162,6 +163,29 @@ def test_gpu_sam_identical(indexed, gpu_device, g, kind, threads, batch, mode):
     if mode == "two_ctx":
         assert "2 GPU context(s)" in err, err[-2000:]
     _same(got, _golden(g, kind))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("g,kind", CASES)
+@pytest.mark.parametrize("batch", [None, 4096, 37])
+def test_gpu_sam_identical_eight_contexts(indexed, gpu_device, g, kind, batch):
+    """The N = 8 fan-out on one GPU: SMEM_GPU_DEVICES=0,0,0,0,0,0,0,0 opens
+    eight device contexts (index, .sa, .pac and worker slots each), `-t 16`
+    deals worker tid to context tid % 8 / slot tid / 8 (software/fastmap.c:
+    204-210's per-worker buffers, one manager per device).  Without -b the
+    batch plan gives each context one batch of its share of the chunk (a
+    share under two seeding grids is not split further): 8 batches, 8
+    workers.  SAM byte-identical to the reference's."""
+    got, err = _run(indexed[g], g, kind, 16, batch,
+                    env={"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_TIMES": "1"})
+    assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
+    assert "8 GPU context(s)" in err, err[-2000:]
+    _same(got, _golden(g, kind))
+    if batch is None:
+        import re
+        sizes = [int(m) for m in re.findall(r"\[M::mem_batch_gpu\] (\d+) reads through the GPU stages", err)]
+        done = [int(m) for m in re.findall(r"\[M::mem_process_seqs\] Processed (\d+) reads", err)]
+        assert len(sizes) == 8 * len(done) and sum(sizes) == sum(done), (sizes, done)
 
 
 @pytest.mark.gpu
