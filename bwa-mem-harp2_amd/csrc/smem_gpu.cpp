@@ -57,6 +57,22 @@ static const double g_t_lib = now_s();  // the library's load (for a linked bina
 // SMEM_GPU_TIMES: time spent releasing batch buffers (device / pinned host) and their counts
 static std::atomic<int64_t> g_rel_dev_ns{0}, g_rel_host_ns{0}, g_rel_dev_n{0}, g_rel_host_n{0};
 
+// runtime errors after which the device (or its context) cannot be trusted:
+// a kernel fault, a lost or uninitialised device, a context gone; every later
+// call is refused.  Others -- a launch's configuration or an argument the
+// runtime rejected (hipErrorInvalidValue, hipErrorInvalidConfiguration, ...)
+// -- refuse that one call and leave the device usable.
+bool hip_error_breaks_device(hipError_t e) {
+    switch (e) {
+        case hipErrorLaunchFailure: case hipErrorIllegalAddress: case hipErrorECCNotCorrectable:
+        case hipErrorAssert: case hipErrorNoDevice: case hipErrorLaunchTimeOut: case hipErrorContextIsDestroyed:
+        case hipErrorNotInitialized: case hipErrorDeinitialized: case hipErrorIllegalState: case hipErrorUnknown:
+            return true;
+        default:
+            return false;
+    }
+}
+
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     if (e != hipSuccess)
         snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
@@ -64,17 +80,20 @@ int fail(int code, const char* what, hipError_t e = hipSuccess) {
         snprintf(g_err, sizeof(g_err), "%s", what);
     // an allocation that does not fit is a refusal, not a broken device
     if (code == SMEM_E_DEVICE && e == hipErrorOutOfMemory) return SMEM_E_NOMEM;
-    if (code == SMEM_E_DEVICE && e != hipSuccess) g_hip_fault = 1;
+    if (code == SMEM_E_DEVICE && hip_error_breaks_device(e)) g_hip_fault = 1;
     return code;
 }
 
-// SMEM_GPU_FAIL=<stage>:<k>[:sticky] -- fault injection for the reject -> CPU
-// path: every k-th call (process-wide) of the stage returns SMEM_E_DEVICE
-// after its work is enqueued and before it is waited for, so the drain on the
-// way out is what keeps that work from landing after the caller resumed.
-// stage: upload (smem_batch_set_reads*), seed (smem_batch_run), sa, chain,
-// aln (smem_batch_chain2aln), fetch, or any.  ":sticky" also marks the
-// device faulted, as a real runtime failure does.
+// SMEM_GPU_FAIL=<stage>:<k>[:sticky|:hip=<code>] -- fault injection for the
+// reject -> CPU path: every k-th call (process-wide) of the stage returns
+// SMEM_E_DEVICE after its work is enqueued and before it is waited for, so
+// the drain on the way out is what keeps that work from landing after the
+// caller resumed.  stage: upload (smem_batch_set_reads*), seed
+// (smem_batch_run), sa, chain, aln (smem_batch_chain2aln), fetch, or any.
+// ":sticky" also marks the device faulted, as a real runtime failure does;
+// ":hip=<code>" goes through fail() with that hipError_t, so the
+// classification decides (hip=9, hipErrorInvalidConfiguration: that call only;
+// hip=719, hipErrorLaunchFailure: the device).
 enum { ST_UPLOAD, ST_SEED, ST_SA, ST_CHAIN, ST_ALN, ST_FETCH, ST_N };
 const char* const k_stage_name[ST_N] = {"upload", "seed", "sa", "chain", "aln", "fetch"};
 std::atomic<uint64_t> g_stage_calls[ST_N];
@@ -93,6 +112,11 @@ int inject_fault(int stage) {
     snprintf(g_err, sizeof(g_err), "injected failure (SMEM_GPU_FAIL=%s): stage %s, call %llu", e, k_stage_name[stage],
              (unsigned long long)n);
     if (strstr(c + 1, ":sticky")) g_hip_fault = 2;
+    if (const char* h = strstr(c + 1, ":hip=")) {
+        char what[256];
+        snprintf(what, sizeof(what), "%s", g_err);
+        return fail(SMEM_E_DEVICE, what, (hipError_t)atoi(h + 5));
+    }
     return SMEM_E_DEVICE;
 }
 
@@ -483,7 +507,11 @@ struct DeviceCall {
             return;
         }
         std::unique_lock<std::mutex> lk(g->adm_mu);
-        g->adm_cv.wait(lk, [&] { return !g->free_pairs.empty() || (int)g->pairs.size() < g->max_active; });
+        // leases are counted against max_active (a lowered limit holds even
+        // when more pairs were made before it), pairs are reused first
+        g->adm_cv.wait(lk, [&] {
+            return g->n_leased < g->max_active && (!g->free_pairs.empty() || (int)g->pairs.size() < g->max_active);
+        });
         g_t_admit += now_s() - t1;
         if (!g->free_pairs.empty()) {
             pair = g->free_pairs.back();
@@ -516,7 +544,7 @@ struct DeviceCall {
             std::lock_guard<std::mutex> lk(g->adm_mu);
             g->free_pairs.push_back(pair);
             --g->n_leased;
-            g->adm_cv.notify_one();
+            g->adm_cv.notify_all();  // a waiter's predicate also depends on n_leased
         }
         if (g_hip_fault && !g->faulted.exchange(g_hip_fault)) {
             std::lock_guard<std::mutex> lk(g->adm_mu);
@@ -1196,6 +1224,18 @@ int smem_batch_fetch_mask(smem_batch_t* b, int mask) {
 
 
 static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa);
+// The densification's link scratch (n_dense x 8 B: 12.4 GB at human size)
+// comes from the device's default memory pool (hipMallocAsync on the init
+// stream) and goes back to it with hipFreeAsync; the pool keeps freed memory
+// reserved until trimmed.  Called once the densification has finished, so
+// that smem_gpu_memory's budget is what stays allocated.
+static hipError_t trim_default_pool(smem_gpu_t* g) {
+    hipMemPool_t pool = nullptr;
+    hipError_t e = hipDeviceGetDefaultMemPool(&pool, g->device);
+    if (e == hipSuccess && pool) e = hipMemPoolTrimTo(pool, 0);
+    return e;
+}
+
 int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
     g_err[0] = 0;
     gpu_wait(g);
@@ -1272,7 +1312,10 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
                 fprintf(stderr, "[M::smem_gpu_load_sa] device %d: .sa densified at %.3f s\n", (int)(intptr_t)d,
                         now_s() - g_t_lib);
             }, (void*)(intptr_t)g->device);
-        if (e == hipSuccess && getenv("SMEM_GPU_SYNC_INIT")) e = hipStreamSynchronize(g->init_st);
+        if (e == hipSuccess && getenv("SMEM_GPU_SYNC_INIT")) {
+            e = hipStreamSynchronize(g->init_st);
+            if (e == hipSuccess) e = trim_default_pool(g);
+        }
         if (e != hipSuccess) {
             (void)hipDeviceSynchronize();
             (void)hipFree(dense);
@@ -2820,6 +2863,7 @@ static void gpu_chain(smem_gpu_t* g, const char* what, std::function<int()> step
     g->ready = std::async(std::launch::async, [g, what, prev, step]() -> int {
         if (prev.valid() && prev.get() != SMEM_OK) return SMEM_E_DEVICE;
         const auto t0 = std::chrono::steady_clock::now();
+        g_hip_fault = 0;  // this thread's: set by fail() on a runtime error that breaks the device
         const int r = step();
         if (getenv("SMEM_GPU_TIMES"))
             fprintf(stderr, "[M::smem_gpu_async] device %d: %s %.4f s, done at %.3f s (rc %d)\n", g->device, what,
@@ -2827,7 +2871,9 @@ static void gpu_chain(smem_gpu_t* g, const char* what, std::function<int()> step
         if (r) {  // every call on the handle is refused from now on (SMEM_E_DEVICE): the caller's CPU path
             std::lock_guard<std::mutex> lk(g->adm_mu);
             snprintf(g->fault_msg, sizeof(g->fault_msg), "initialisation failed: %s", g_err);
-            g->faulted.store(3);
+            // a HIP runtime failure (1, as during a run: its diagnostics may have reached stdout)
+            // or a refusal such as an allocation that does not fit (3)
+            g->faulted.store(g_hip_fault == 1 ? 1 : 3);
         }
         return r;
     }).share();
@@ -2907,6 +2953,7 @@ int smem_gpu_wait_ready(smem_gpu_t* g) {
     if (g->sa_ready) {  // the .sa densification on the init stream (batches do not
         HIP_TRY(hipSetDevice(g->device));  // need it: their lookups use the uploaded
         HIP_TRY(hipEventSynchronize(g->sa_ready));  // samples until it is done)
+        HIP_TRY(trim_default_pool(g));
     }
     return SMEM_OK;
 }

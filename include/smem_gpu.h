@@ -225,7 +225,8 @@ int  smem_gpu_set_max_active(smem_gpu_t *gpu, int n);
  * HIP runtime may also have printed its own diagnostics -- on a queue abort,
  * a dump of the queue's packets on stdout); 2: an injected sticky fault
  * (SMEM_GPU_FAIL); 3: smem_gpu_init_devices_async could not upload the index
- * (nothing ran on the device).  msg (may be NULL) gets the first failure's text. */
+ * (a refusal, e.g. an allocation that does not fit; an upload that failed on a
+ * HIP runtime error reports 1).  msg (may be NULL) gets the first failure's text. */
 int  smem_gpu_fault(const smem_gpu_t *gpu, char *msg, int msg_len);
 /* Memory held: a batch's device and pinned host buffers (they grow to the
  * largest batch seen); a device's resident index (Occ64, densified SA and the

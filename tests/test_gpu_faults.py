@@ -2,7 +2,7 @@
 (include/smem_gpu.h, "Failure contract"; the reference's semantics:
 software/bwt.c:686-717, a refused batch computed on the CPU).
 
-SMEM_GPU_FAIL=<stage>:<k>[:sticky] makes every k-th call of a stage return
+SMEM_GPU_FAIL=<stage>:<k>[:sticky|:hip=<code>] makes every k-th call of a stage return
 SMEM_E_DEVICE after its work is enqueued and before it is waited for, so the
 drain on the way out of the call is what keeps that work from landing after
 the caller resumed.  ":sticky" also marks the device faulted, as a real HIP
@@ -102,20 +102,54 @@ def test_sticky_fault_refuses_every_later_call(small, gpu_device, fail_env):
         gpu.close()
 
 
+@pytest.mark.parametrize("code,sticky", [(9, False), (1, False), (719, True), (700, True)])
+def test_injected_hip_error_classification(small, gpu_device, fail_env, code, sticky):
+    """A HIP runtime error goes through the library's classification: a
+    launch-configuration or argument error (hipErrorInvalidConfiguration 9,
+    hipErrorInvalidValue 1) refuses that one call and leaves the device usable
+    (the same batch reruns bit-exact); a kernel fault (hipErrorLaunchFailure
+    719, hipErrorIllegalAddress 700) marks the device faulted for good."""
+    import smemgpu
+    gpu = smemgpu.Gpu(small["idx"], device=gpu_device)
+    try:
+        r = small["reads"]
+        b = gpu.batch(r.n, int(r.codes.size), int(r.lens.max()))
+        b.set_reads(r.codes, r.offs)
+        fail_env(f"seed:1:hip={code}")
+        with pytest.raises(smemgpu.SmemError, match="SMEM_E_DEVICE"):
+            b.run()
+        fail_env(None)
+        f, msg = gpu.fault()
+        if sticky:
+            assert f == 1 and "injected" in msg, (f, msg)
+            with pytest.raises(smemgpu.SmemError, match="faulted earlier"):
+                b.run()
+        else:
+            assert f == 0, (f, msg)
+            b.set_reads(r.codes, r.offs)
+            b.run()
+            assert b.fetch().to_smgo() == small["want"]
+        b.close()
+    finally:
+        fail_env(None)
+        gpu.close()
+
+
 def test_admission_bound_concurrent_workers(small, gpu_device):
     """More host workers than admitted calls (max_active 2, 6 threads): every
-    worker's results are bit-exact; the waiting workers are admitted in turn."""
+    worker's results are bit-exact; the waiting workers are admitted in turn.
+    A warm-up at max_active 4 makes four stream pairs first; lowering the
+    limit to 2 then holds (leases are counted against it, not pairs)."""
     import threading
     import smemgpu
     gpu = smemgpu.Gpu(small["idx"], device=gpu_device)
-    gpu.set_max_active(2)
     r = small["reads"]
     errs, ok = [], []
 
-    def worker():
+    def worker(reps):
         try:
             b = gpu.batch(r.n, int(r.codes.size), int(r.lens.max()))
-            for _ in range(3):
+            for _ in range(reps):
                 b.set_reads(r.codes, r.offs)
                 b.run()
                 ok.append(b.fetch().to_smgo() == small["want"])
@@ -123,14 +157,16 @@ def test_admission_bound_concurrent_workers(small, gpu_device):
         except Exception as e:  # surfaced below
             errs.append(e)
 
-    th = [threading.Thread(target=worker) for _ in range(6)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
+    for limit, reps in ((4, 1), (2, 3)):
+        gpu.set_max_active(limit)
+        th = [threading.Thread(target=worker, args=(reps,)) for _ in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
     gpu.close()
     assert not errs, errs[0]
-    assert len(ok) == 18 and all(ok)
+    assert len(ok) == 24 and all(ok)
 
 
 def test_async_init_devices(small, gpu_device):
