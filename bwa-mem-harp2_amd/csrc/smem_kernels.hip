@@ -1313,16 +1313,17 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
 // owners per wave: twice seed_kernel's entries per list in the same LDS),
 // entries beyond NL in the owner's arena.
 // ======================================================================
-template <int OWN, int NL>
+template <int OWN, int NL, bool PAIR>
 struct WpWave {
     uint4 e[NL][OWN];     // owners' lists: index k < NL at slot (lr - k) mod NL
     uint4 d0[OWN];        // step descriptors: j, curr_n, prev_off, c | lr << 2 | last_x2 bits 32-33 << 8
     uint4 d1[OWN];        // min_intv, last_x2 low word
     uint4 q[OWN];         // query windows (LDS-DMA landing slots)
+    uint4 noff[OWN];      // the next read's offs[rid], offs[rid + 1] (LDS-DMA landing slots)
     uint64_t res[64];     // extend result sizes by lane (PAIR: of the lane's last entry)
-    uint64_t res1[64];    // PAIR: of the lane's first entry
-    uint32_t tabS[64];    // owner whose segment starts at task position p (0xFF: none)
-    uint32_t tabP[64];    // free-lane rank -> lane
+    uint64_t res1[PAIR ? 64 : 1];  // PAIR: of the lane's first entry
+    uint8_t tabS[64];     // owner whose segment starts at task position p (0xFF: none)
+    uint8_t tabP[64];     // free-lane rank -> lane
 };
 
 // inclusive prefix sum over the 64 lanes (the row_shr / row_bcast pattern of
@@ -1357,8 +1358,8 @@ template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false>
 __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     constexpr uint32_t PR = PAIR ? 2u : 1u;  // entries per worker lane
     static_assert(OWN >= 1 && OWN <= 64 && NL >= 2 && NL < 32, "owners per wave / list entries");
-    __shared__ WpWave<OWN, NL> wlds[4];
-    WpWave<OWN, NL>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    __shared__ WpWave<OWN, NL, PAIR> wlds[4];
+    WpWave<OWN, NL, PAIR>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const int me = (int)(threadIdx.x & 63);
     const uint64_t wave_g = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);  // lane 0's global index
     const uint32_t cap = P.cap_list;
@@ -1367,7 +1368,10 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
 
     int phase = me < OWN ? P_FETCH : P_EXIT;  // lanes >= OWN only execute extends
     int item = -1, len = 0;
-    int nitem = 0, nlen = -2;  // next read: -2 nothing claimed, -1 claimed, >= 0 offsets loaded
+    // next read: -2 nothing claimed, -1 claimed, -3 its offsets to be fetched, -4 in flight, >= 0 loaded.
+    // The claim's atomic and the offsets' LDS-DMA are waited for by the uniform section's vmcnt(0), never
+    // on their own: a wave stalled a memory round trip per read for the offsets before (~5 % of iterations)
+    int nitem = 0, nlen = -2;
     int rid = 0, nrid = 0;
     uint32_t keep_n = 0;
     uint32_t o0 = 0, no0 = 0;
@@ -1419,8 +1423,19 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             if (nlen == -2) {  // claim the next read
                 nitem = atomicAdd(P.head, 1);
                 nlen = -1;
-            } else if (nlen == -1) {  // its offsets (the claim returned last iteration)
-                next_offsets(P, nitem, no0, nlen, nrid);
+            } else if (nlen == -1) {  // the claim returned last iteration
+                if (nitem >= P.n_items) {
+                    nlen = 0;  // nothing left: the FETCH block exits
+                } else if (P.read_ids) {  // overflow pass: through read_ids (a small launch)
+                    next_offsets(P, nitem, no0, nlen, nrid);
+                } else {
+                    nrid = nitem;
+                    nlen = -3;  // offsets fetched in the uniform section
+                }
+            } else if (nlen == -4) {  // landed last iteration
+                const uint4 v = L->noff[me];
+                no0 = v.x;  // batches hold < 2^32 bases: the low words
+                nlen = (int)(v.z - v.x);
             }
         }
         // ---- owners: advance the state machine one pass (seed_kernel's
@@ -1648,8 +1663,8 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         const uint32_t rank = mbcnt64(fmask);
         L->tabS[me] = 0xFFu;
         wave_lds_fence();
-        if (take) L->tabS[excl] = (uint32_t)me;
-        if (freel) L->tabP[rank] = (uint32_t)me;
+        if (take) L->tabS[excl] = (uint8_t)me;
+        if (freel) L->tabP[rank] = (uint8_t)me;
         wave_lds_fence();
         const uint64_t marks = __ballot(L->tabS[me] != 0xFFu);
         const bool worker = freel && rank < ntask;
@@ -1683,9 +1698,13 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                 }
             }
         }
-        // the query window for owners that want one
+        // the query window for owners that want one, the next read's offsets
         const bool ld_q = qwant != qb && qwant != ~0u;
         if (ld_q) __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&L->q[0]), 16, 0, 0);
+        if (nlen == -3) {
+            __builtin_amdgcn_global_load_lds(P.offs + nrid, LDS_PTR(&L->noff[0]), 16, 0, 0);
+            nlen = -4;
+        }
         // the extend: forward owners their own ik (a = x[1]), workers an entry backward (a = x[0])
         const bool task = worker || fwdreq;
         const uint64_t ra = fwdreq ? ik1 : p_x0(ent), rb = fwdreq ? ik0 : p_x1(ent), rs = fwdreq ? ik2 : p_x2(ent);
@@ -1900,7 +1919,7 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
-    if (variant >= 40 && variant <= 51) return 1;  // seed_wp_kernel
+    if (variant >= 40 && variant <= 53) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
     return variant == 0 || (variant >= 2 && variant <= 31);
 #else
@@ -1944,6 +1963,9 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 49: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 50: hipLaunchKernelGGL((smem::seed_wp_kernel<20, 22, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 51: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 16, 0, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 52-53: 4 blocks per CU: <24, 20>, <28, 16>
+        case 52: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 20, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 53: hipLaunchKernelGGL((smem::seed_wp_kernel<28, 16, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
