@@ -1386,7 +1386,7 @@ struct LeafHand {
 
 template <class N>
 __device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int64_t k, int lane,
-                                               LeafHand* hand = nullptr) {
+                                               LeafHand* hand = nullptr, int64_t* lkey = nullptr) {
     uint32_t x = root;
     int lower = -1;
     bool full = false;
@@ -1399,7 +1399,10 @@ __device__ __forceinline__ int tree_lower_wave(const N* pool, uint32_t root, int
         full = full || n == BT_MAX;
         bool eq;
         const int i = node_find_regs(n, kv, k, lane, eq);
-        if (i >= 0) lower = __builtin_amdgcn_readlane((int)idv, i);
+        if (i >= 0) {
+            lower = __builtin_amdgcn_readlane((int)idv, i);
+            if (lkey) *lkey = rl64(kv, i);  // the lower chain's key: its pos
+        }
         if (i >= 0 && eq && !leaf) return lower;
         if (leaf) {
             if (hand) *hand = LeafHand{!full, x, n, kv, idv};
@@ -1484,19 +1487,49 @@ __device__ int tree_inorder_wave(const N* pool, uint32_t root, uint32_t* out, in
 // time in seed order, each tree search and kb_putp by the whole wave (one
 // LDS round per node, shifts and splits in parallel: 35 -> 20 M cycles on
 // the bench's worst read against lane 0 walking the tree alone); lane 0
-// alone reads and writes the chain records.  The wave loads codes and seeds
-// 64 at a time.  A search whose path holds no full node hands its leaf to
-// the insert (no second descent).  Measured without effect on the walk's
-// time: that hand-off, one LDS round per node instead of three, wavefront-
-// instead of workgroup-scope fences, and the chain records prefetched a
-// window of 64 seeds at a time; the in-order listing's scratch stack was
-// what it waited on (tree_inorder_wave).
+// reads and writes the chain records.  The wave loads codes and seeds 64 at
+// a time.  A search whose path holds no full node hands its leaf to the
+// insert (no second descent).
+// Record cache (round 5): lane 0's read of the lower chain's record was a
+// dependent HBM round trip per seed, about half of a candidate's ~3,300
+// cycles.  The records of the chains the replay touches are kept in a
+// direct-mapped, write-through LDS cache keyed by chain id (32-B entries;
+// pos is the tree key the search returns): a chain made here is installed as
+// it is made, a cluster-pass chain as it is inserted (its record loaded with
+// its window's seeds), an append updates the entry and the HBM record.  The
+// cache takes the LDS the tree does not use, from the top down, and halves
+// when the growing tree needs its space (halving keeps every entry below the
+// new size where lookups find it; the HBM records are always current).  On the
+// heaviest uniform reads a 256-entry cache would serve 84 % of the lookups,
+// 1024 entries 99 % (tools/chain_cache_sim.py).
+struct CRec {
+    int64_t last_rbeg;
+    int32_t first_qbeg, last_qbeg, last_len, n;
+    uint32_t last, tag;
+};
+static_assert(sizeof(CRec) == 32, "CRec is 32 B");
+
 template <class N>
-__device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane) {
+__device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane, unsigned char* lds,
+                           uint32_t lds_bytes, bool pool_in_lds) {
     const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
     const SeedRec* seed = P.seed + S;
     ChainRec* chn = P.chn + S;
     uint32_t root = 0, n_nodes = 1, n_ch = 0;
+    // cache slot q at crec[-1 - q]: the top of the LDS region, growing down
+    CRec* crec = reinterpret_cast<CRec*>(lds + (lds_bytes & ~31u));
+    const uint32_t lo = pool_in_lds ? 8u * (uint32_t)sizeof(N) : 0u;  // the tree's first nodes
+    uint32_t C = 0;
+    {
+        const uint32_t room = lds_bytes > lo ? (lds_bytes - lo) / 32u : 0u;
+        C = !P.replay_cache ? 0u : (room >= 2048 ? 2048u : 0u);
+        if (!C && P.replay_cache) {
+            C = 1;
+            while (2 * C <= room) C *= 2;
+            if (C < 16) C = 0;
+        }
+    }
+    for (uint32_t q = (uint32_t)lane; q < C; q += 64) crec[-1 - (int)q].tag = 0xffffffffu;
     if (lane == 0) node_init(pool, 1);
     wave_fence();
     __builtin_amdgcn_wave_barrier();
@@ -1505,6 +1538,8 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
         const uint32_t cd = o < ns ? code[o] : CODE_SKIP;
         SeedRec sd{0, 0, 0};
         if (cd != CODE_SKIP) sd = seed[o];
+        ChainRec cn{};  // a cluster-pass chain's record, installed when it is inserted
+        if (cd == CODE_NEW && C) cn = chn[o];
         uint64_t m = __ballot(cd != CODE_SKIP);
         while (m) {
             const int t = __builtin_ctzll(m);
@@ -1514,24 +1549,49 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
             const int32_t qb = rl32(sd.qbeg, t), ln = rl32(sd.len, t);
             const uint32_t ot = base + (uint32_t)t;
             int lw = -1;
+            int64_t lpos = 0;
             LeafHand hand{false, 0, 0, 0, 0};
-            if (ct == CODE_REPLAY && n_ch) lw = tree_lower_wave(pool, root, rb, lane, &hand);
+            if (ct == CODE_REPLAY && n_ch) lw = tree_lower_wave(pool, root, rb, lane, &hand, &lpos);
             int make = 1;
             if (lw >= 0) {
                 if (lane == 0) {
-                    ChainRec c = chn[lw];
+                    const uint32_t q = (uint32_t)lw & (C - 1);
+                    CRec* e = C ? crec - 1 - (int)q : nullptr;
+                    ChainRec c;
+                    const bool hit = e && e->tag == (uint32_t)lw;
+                    if (hit) {
+                        const CRec r = *e;
+                        c = ChainRec{lpos, r.last_rbeg, r.first_qbeg, r.last_qbeg, r.last_len, r.n, (uint32_t)lw, r.last};
+                    } else {
+                        c = chn[lw];
+                    }
                     const int mg = merge_test(P, c, rb, qb, ln);
                     if (mg == MERGE_APPEND) {
                         P.next[S + c.last] = ot;
                         chain_append(c, ot, rb, qb, ln);
                         chn[lw] = c;
                     }
+                    if (e && (mg == MERGE_APPEND || !hit))
+                        *e = CRec{c.last_rbeg, c.first_qbeg, c.last_qbeg, c.last_len, c.n, c.last, (uint32_t)lw};
                     make = mg == MERGE_NEW;
                 }
                 make = __builtin_amdgcn_readfirstlane(make);
             }
             if (make) {
-                if (lane == 0 && ct == CODE_REPLAY) chn[ot] = ChainRec{rb, rb, qb, qb, ln, 1, ot, ot};
+                if (ct == CODE_REPLAY) {
+                    if (lane == 0) {
+                        chn[ot] = ChainRec{rb, rb, qb, qb, ln, 1, ot, ot};
+                        if (C) crec[-1 - (int)(ot & (C - 1))] = CRec{rb, qb, qb, ln, 1, ot, ot};
+                    }
+                } else if (lane == t && C) {
+                    crec[-1 - (int)(ot & (C - 1))] =
+                        CRec{cn.last_rbeg, cn.first_qbeg, cn.last_qbeg, cn.last_len, cn.n, cn.last, ot};
+                }
+                if (pool_in_lds) {  // an insert splits at most one node per level: keep the cache above them
+                    while (C && (n_nodes + 8) * (uint32_t)sizeof(N) > lds_bytes - C * 32u) C = C > 16 ? C / 2 : 0;
+                }
+                wave_fence();
+                __builtin_amdgcn_wave_barrier();
                 if (hand.ok) {  // no split on the search's path: insert into its leaf
                     leaf_insert_hand(pool, hand, ot, rb, lane);
                 } else {
@@ -1855,9 +1915,11 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                     __syncthreads();
                     if (n_cand / (BT_T - 1) + 8 <= P.lds_bytes / sizeof(LNode))
-                        n = replay_tree(P, S, (uint32_t)(E - S), reinterpret_cast<LNode*>(lds_raw), lane);
+                        n = replay_tree(P, S, (uint32_t)(E - S), reinterpret_cast<LNode*>(lds_raw), lane, lds_raw,
+                                        P.lds_bytes, true);
                     else
-                        n = replay_tree(P, S, (uint32_t)(E - S), P.node + (S / 7 + 3ull * (uint64_t)r), lane);
+                        n = replay_tree(P, S, (uint32_t)(E - S), P.node + (S / 7 + 3ull * (uint64_t)r), lane,
+                                        lds_raw, P.lds_bytes, false);
                 }
                 if (lane == 0) {
                     s_n = n;

@@ -193,8 +193,10 @@ def test_chain_paths_agree(gpu_device, monkeypatch, env):
         gpu.close()
 
 
-@pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_HEAVY_MIN="0"), dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_LDS="4096")],
-                         ids=["default", "all-wave", "all-wave-hbm-tree"])
+@pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_HEAVY_MIN="0"), dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_LDS="4096"),
+                                 dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_REPLAY_CACHE="0"),
+                                 dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_LDS="12288")],
+                         ids=["default", "all-wave", "all-wave-hbm-tree", "no-record-cache", "record-cache-shrinks"])
 def test_chain_equal_keys_replay(gpu_device, monkeypatch, env):
     """Reads X + Y + X whose two copies of X match one locus: test_and_merge
     rejects the far query offset, so two chains share a pos, and the
@@ -237,8 +239,9 @@ def test_chain_equal_keys_replay(gpu_device, monkeypatch, env):
         gpu.close()
 
 
-@pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_STREAMS="1"), dict(SMEM_CHAIN_GIANT_MIN="256")],
-                         ids=["tiers", "one-launch", "more-giants"])
+@pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_STREAMS="1"), dict(SMEM_CHAIN_GIANT_MIN="256"),
+                                 dict(SMEM_CHAIN_REPLAY_CACHE="0")],
+                         ids=["tiers", "one-launch", "more-giants", "no-record-cache"])
 def test_chain_human_like_giants(gpu_device, monkeypatch, env):
     """A 4 Mbp genome with the human-like repeat profile and 8 % satellite /
     simple-sequence arrays: reads from the arrays carry thousands of seed
