@@ -1354,9 +1354,17 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 // PAIR: a worker lane takes two consecutive entries of a step (two extends
 // in flight per lane: twice the requests per wave-iteration)
-template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false>
+// KT: an extend whose result is a string of at most P.kt_k bases reads that
+// string's bi-interval from the k-mer table (one 16-B probe; the table of
+// k = 11 is 90 MB and stays in the 256 MB MALL) instead of two Occ buckets
+// and the rank: a bi-interval is a function of the string alone, so the
+// result is bwt_extend's.  Owners keep the codes of their forward string's
+// first k bases and of the k bases from the backward position (variant 23's
+// bookkeeping); the step descriptor carries the latter and the position.
+template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false, bool KT = false>
 __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     constexpr uint32_t PR = PAIR ? 2u : 1u;  // entries per worker lane
+    const int K = KT && P.kt ? P.kt_k : 0;
     static_assert(OWN >= 1 && OWN <= 64 && NL >= 2 && NL < 32, "owners per wave / list entries");
     __shared__ WpWave<OWN, NL, PAIR> wlds[4];
     WpWave<OWN, NL, PAIR>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
@@ -1381,6 +1389,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     int start = 0, ori_start = 0;
     int x = 0, min_intv = 1, middle = 0, i = 0, ret = 0, cur_c = 0;
     uint32_t j = 0;
+    uint32_t kc = 0, kb = 0;  // KT: the forward string's codes, the K bases from backward position i
     uint64_t ik0 = 0, ik1 = 0, ik2 = 0;
     uint32_t ikend = 0;
     uint32_t fwd_n = 0, prev_off = 0, prev_n = 0, curr_n = 0;
@@ -1544,6 +1553,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                         ik2 = lq1 - lq;
                         ik1 = sel4(qx, P.L2[3], P.L2[2], P.L2[1], P.L2[0]) + 1;
                         ikend = (uint32_t)(x + 1);
+                        if constexpr (KT) kc = (uint32_t)qx;
                         fwd_n = 0;
                         lr = 0;
                         i = x + 1;
@@ -1580,6 +1590,9 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                 } else {
                     ik0 = nb; ik1 = na; ik2 = ns;
                     ikend = (uint32_t)(i + 1);
+                    if constexpr (KT) {
+                        if (i + 1 - x <= K) kc = kc << 2 | (uint32_t)(3 - cur_c);  // saturates at the first K bases
+                    }
                     ++i;
                     phase = P_FWD;
                 }
@@ -1614,6 +1627,10 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             if (phase == P_FWD_DONE) {  // software/bwt.c:805-808 (the ring read backwards is the reversal)
                 head = pack_p(ik0, ik1, ik2, ikend);  // the last push: prev[0]
                 ret = (int)ikend;
+                if constexpr (KT) {  // the K bases from x (those past the forward string are never read)
+                    const uint32_t lf = ikend - (uint32_t)x;
+                    kb = lf >= (uint32_t)K ? kc : kc << (2 * ((uint32_t)K - lf));
+                }
                 prev_off = cap - fwd_n;
                 prev_n = fwd_n;
                 lr = lr == 0 ? (uint32_t)NL - 1 : lr - 1;  // slot of the last push
@@ -1631,6 +1648,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                         j = 0;
                         curr_n = 0;
                         fail0 = 0;
+                        if constexpr (KT) kb = (uint32_t)cur_c << (2 * (K - 1)) | kb >> 2;
                         if (i > 0) qwant = QBLK(i - 1);  // the next step's base
                         phase = P_BWD_WAIT;               // -> the wave extends the step's entries
                     } else {
@@ -1648,8 +1666,8 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         const uint32_t slots = (rem + PR - 1) / PR;  // worker lanes the step still needs
         if (rem) {  // what a worker needs of this owner's step
             L->d0[me] = make_uint4(j, curr_n, prev_off,
-                                   (uint32_t)cur_c | lr << 2 | (uint32_t)(last_x2 >> 32) << 8);
-            L->d1[me] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, prev_n, 0u);
+                                   (uint32_t)cur_c | lr << 2 | (uint32_t)(last_x2 >> 32) << 8 | (uint32_t)i << 10);
+            L->d1[me] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, prev_n, kb);
         }
         // the owners' remaining entries laid out in lane order over the free lanes
         const uint32_t incl = wave_scan_add(slots);
@@ -1717,7 +1735,20 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         if (ll >= P.L2[4]) ll = 0;
         const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
         uint4 k0 = {0, 0, 0, 0}, k1 = {0, 0, 0, 0}, l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
-        if (task) {
+        // KT: a result of at most K bases from the table (forward: q[x, i]; backward: q[i, end))
+        bool ktp = false;
+        if constexpr (KT) {
+            if (task && K > 0) {
+                const int lq = fwdreq ? i + 1 - x : (int)p_end(ent) - (int)(w0.w >> 10);
+                if (lq <= K) {
+                    const uint32_t code = fwdreq ? kc << 2 | (uint32_t)(3 - cur_c) : w1.w >> (2 * (K - lq));
+                    const uint64_t base = ((1ull << (2 * lq)) - 4) / 3;
+                    k0 = P.kt[base + code];
+                    ktp = true;
+                }
+            }
+        }
+        if (task && !ktp) {
             const uint32_t *a0, *a1;
             block_chunks<false>(P.occ64, bk, a0, a1);
             k0 = *reinterpret_cast<const uint4*>(a0);
@@ -1757,7 +1788,11 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             qv = L->q[me];
             qb = qwant;
         }
-        if (task) {
+        if (ktp) {  // forward: na is the x[1] side, backward: the x[0] side
+            na = fwdreq ? p_x1(k0) : p_x0(k0);
+            nb = fwdreq ? p_x0(k0) : p_x1(k0);
+            ns = p_x2(k0);
+        } else if (task) {
             const Bucket32 wk{k0, k1};
             const Bucket32 wl = bl != bk ? Bucket32{l0, l1} : wk;
             extend_counts64<false>(P, ra, rb, rs, rc, kk, ll, wk, wl, na, nb, ns);
@@ -1919,7 +1954,7 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
-    if (variant >= 40 && variant <= 53) return 1;  // seed_wp_kernel
+    if (variant >= 40 && variant <= 55) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
     return variant == 0 || (variant >= 2 && variant <= 31);
 #else
@@ -1966,6 +2001,9 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 52-53: 4 blocks per CU: <24, 20>, <28, 16>
         case 52: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 20, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 53: hipLaunchKernelGGL((smem::seed_wp_kernel<28, 16, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 54-55: with the k-mer table (KT; smem_gpu_set_kmer_table, no table: plain): 49's shape, 40's shape
+        case 54: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 55: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 1, 3, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

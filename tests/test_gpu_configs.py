@@ -153,13 +153,15 @@ def test_human_kmer_table(human, gpu_device):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("variant", [40, 41])
+@pytest.mark.parametrize("variant", [40, 41, 54])
 def test_human_wp_kernel(human, variant):
     """seed_wp_kernel at human size: forward lists longer than the LDS lists
     (entries in the owner's arena, both list regions), 34-bit coordinates."""
     from smemgpu import synth
     gpu = human["gpu"]
     gpu.set_variant(variant)
+    if variant == 54:
+        gpu.set_kmer_table(11)  # 34-bit table entries
     try:
         reads = synth.make_reads(human["codes"], 10_000, 150, seed=12, sub_rate=0.02, n_rate=0.001)
         res, _ = _seed_and_compare(gpu, human["oidx"], reads, {})
@@ -169,6 +171,7 @@ def test_human_wp_kernel(human, variant):
             _seed_and_compare(gpu, human["oidx"], reads, opt)
     finally:
         gpu.set_variant(0)
+        gpu.set_kmer_table(0)
 
 
 @pytest.mark.timeout(900)

@@ -165,7 +165,7 @@ def test_kernel_variants(world, gpu_device, variant):
         gpu.close()
 
 
-WP_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53]
+WP_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55]
 
 
 def _edge_reads(g):
@@ -217,6 +217,22 @@ def test_wp_kernel_parity(world, gpu_device, variant):
     gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant, lanes_per_cu=64)
     try:  # many reads per owner
         assert smemgpu.seed(gpu, reads.codes, reads.offs).to_smgo() == want
+    finally:
+        gpu.close()
+
+
+@pytest.mark.parametrize("variant,k", [(54, 1), (54, 7), (54, 11), (55, 12), (55, 2)])
+def test_wp_kmer_table(world, gpu_device, variant, k):
+    """seed_wp_kernel with the k-mer table (variants 54, 55): forward and
+    backward extends whose result has <= k bases read the table; every read
+    kind and option set bit-exact against the oracle."""
+    import smemgpu
+    gpu = smemgpu.Gpu(world["idx"], device=gpu_device, variant=variant, kmer_k=k)
+    try:
+        reads = synth_concat(_reads(world["genome"], "mixed", seed=13), _reads(world["genome"], "250bp5", seed=14))
+        for opt in OPTS.values():
+            want, _, _ = oracle.seed(world["ref"], reads.codes, reads.offs, threads=4, **opt)
+            assert smemgpu.seed(gpu, reads.codes, reads.offs, smemgpu.Options(**opt)).to_smgo() == want, opt
     finally:
         gpu.close()
 
