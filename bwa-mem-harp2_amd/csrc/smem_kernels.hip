@@ -1313,18 +1313,33 @@ __global__ __launch_bounds__(256, WPE) void seed_kernel(SeedParams P) {
 // owners per wave: twice seed_kernel's entries per list in the same LDS),
 // entries beyond NL in the owner's arena.
 // ======================================================================
-template <int OWN, int NL, bool PAIR>
+template <int OWN, int NL, bool PAIR, bool DPOS = false>
 struct WpWave {
     uint4 e[NL][OWN];     // owners' lists: index k < NL at slot (lr - k) mod NL
-    uint4 d0[OWN];        // step descriptors: j, curr_n, prev_off, c | lr << 2 | last_x2 bits 32-33 << 8
-    uint4 d1[OWN];        // min_intv, last_x2 low word
+    // step descriptors, by owner lane (DPOS: by the task position where the owner's entries start):
+    // j, curr_n, prev_off, c | lr << 2 | last_x2 bits 32-33 << 8 | i << 10; min_intv, last_x2 low word,
+    // prev_n (DPOS: the owner lane), kb
+    uint4 d0[DPOS ? 64 : OWN];
+    uint4 d1[DPOS ? 64 : OWN];
     uint4 q[OWN];         // query windows (LDS-DMA landing slots)
     uint4 noff[OWN];      // the next read's offs[rid], offs[rid + 1] (LDS-DMA landing slots)
-    uint64_t res[64];     // extend result sizes by lane (PAIR: of the lane's last entry)
+    uint64_t res[DPOS ? 1 : 64];  // extend result sizes by lane (PAIR: of the lane's last entry; DPOS: in d1,
+                                  // which the workers have read before the results are written)
     uint64_t res1[PAIR ? 64 : 1];  // PAIR: of the lane's first entry
     uint8_t tabS[64];     // owner whose segment starts at task position p (0xFF: none)
     uint8_t tabP[64];     // free-lane rank -> lane
 };
+
+// the OR of v over the 64 lanes (the same pattern; lane 63 holds it)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 
 // inclusive prefix sum over the 64 lanes (the row_shr / row_bcast pattern of
 // ksw_device.h's scan_max)
@@ -1361,13 +1376,19 @@ __device__ __forceinline__ void wave_lds_fence() {
 // result is bwt_extend's.  Owners keep the codes of their forward string's
 // first k bases and of the k bases from the backward position (variant 23's
 // bookkeeping); the step descriptor carries the latter and the position.
-template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false, bool KT = false>
+// DPOS: the segment starts' mask by a DPP OR over the owners and each owner's
+// descriptor stored at its start position, so a worker reads its owner's
+// descriptor one LDS round after the scan (three rounds before the loads:
+// start marks, owner, descriptor, entry -> descriptor, entry)
+template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false, bool KT = false, bool DPOS = false>
 __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
+    static_assert(!(DPOS && PAIR), "DPOS keeps the owner lane where PAIR keeps prev_n");
     constexpr uint32_t PR = PAIR ? 2u : 1u;  // entries per worker lane
     const int K = KT && P.kt ? P.kt_k : 0;
     static_assert(OWN >= 1 && OWN <= 64 && NL >= 2 && NL < 32, "owners per wave / list entries");
-    __shared__ WpWave<OWN, NL, PAIR> wlds[4];
-    WpWave<OWN, NL, PAIR>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    __shared__ WpWave<OWN, NL, PAIR, DPOS> wlds[4];
+    WpWave<OWN, NL, PAIR, DPOS>* L = &wlds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    uint64_t* const RES = DPOS ? reinterpret_cast<uint64_t*>(&L->d1[0]) : &L->res[0];
     const int me = (int)(threadIdx.x & 63);
     const uint64_t wave_g = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);  // lane 0's global index
     const uint32_t cap = P.cap_list;
@@ -1664,7 +1685,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         const bool fwdreq = out && phase == P_FWD_RES;
         const uint32_t rem = phase == P_BWD_WAIT ? prev_n - j : 0u;
         const uint32_t slots = (rem + PR - 1) / PR;  // worker lanes the step still needs
-        if (rem) {  // what a worker needs of this owner's step
+        if (!DPOS && rem) {  // what a worker needs of this owner's step
             L->d0[me] = make_uint4(j, curr_n, prev_off,
                                    (uint32_t)cur_c | lr << 2 | (uint32_t)(last_x2 >> 32) << 8 | (uint32_t)i << 10);
             L->d1[me] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, prev_n, kb);
@@ -1679,21 +1700,41 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         const uint32_t take = (slots && excl < nfree) ? min(slots, nfree - excl) : 0u;
         const bool freel = (fmask >> me) & 1;
         const uint32_t rank = mbcnt64(fmask);
-        L->tabS[me] = 0xFFu;
-        wave_lds_fence();
-        if (take) L->tabS[excl] = (uint8_t)me;
-        if (freel) L->tabP[rank] = (uint8_t)me;
-        wave_lds_fence();
-        const uint64_t marks = __ballot(L->tabS[me] != 0xFFu);
+        uint64_t marks;
+        if constexpr (DPOS) {
+            if (take) {  // the descriptor where the owner's entries start
+                L->d0[excl] = make_uint4(j, curr_n, prev_off,
+                                         (uint32_t)cur_c | lr << 2 | (uint32_t)(last_x2 >> 32) << 8 | (uint32_t)i << 10);
+                L->d1[excl] = make_uint4((uint32_t)min_intv, (uint32_t)last_x2, (uint32_t)me, kb);
+            }
+            if (freel) L->tabP[rank] = (uint8_t)me;
+            const uint32_t mlo = wave_or(take && excl < 32 ? 1u << excl : 0u);
+            const uint32_t mhi = wave_or(take && excl >= 32 ? 1u << (excl - 32) : 0u);
+            marks = (uint64_t)mhi << 32 | mlo;
+            wave_lds_fence();
+        } else {
+            L->tabS[me] = 0xFFu;
+            wave_lds_fence();
+            if (take) L->tabS[excl] = (uint8_t)me;
+            if (freel) L->tabP[rank] = (uint8_t)me;
+            wave_lds_fence();
+            marks = __ballot(L->tabS[me] != 0xFFu);
+        }
         const bool worker = freel && rank < ntask;
         uint32_t s = 0, o = 0, jj = 0, lro = 0;
         bool has2 = false;
         uint4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0}, ent = {0, 0, 0, 0}, ent2 = {0, 0, 0, 0};
         if (worker) {
             s = (uint32_t)hibit64(marks & ((2ull << rank) - 1ull));  // the segment holding task `rank`
-            o = L->tabS[s];
-            w0 = L->d0[o];
-            w1 = L->d1[o];
+            if constexpr (DPOS) {
+                w0 = L->d0[s];
+                w1 = L->d1[s];
+                o = w1.z;
+            } else {
+                o = L->tabS[s];
+                w0 = L->d0[o];
+                w1 = L->d1[o];
+            }
             jj = w0.x + PR * (rank - s);
             lro = (w0.w >> 2) & 31u;
             if (jj < (uint32_t)NL) {
@@ -1811,7 +1852,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         const bool surv2 = PAIR && has2 && ns2 >= (uint64_t)w1.x;
         const uint64_t smask = __ballot(surv);
         const uint64_t smask2 = PAIR ? (uint64_t)__ballot(surv2) : 0ull;
-        L->res[me] = PAIR && has2 ? ns2 : ns;  // the lane's last entry
+        RES[me] = PAIR && has2 ? ns2 : ns;  // the lane's last entry
         if constexpr (PAIR) L->res1[me] = ns;
         wave_lds_fence();
         bool keep = false;
@@ -1821,7 +1862,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                 keep = w0.y == 0 || ns != lx;
             } else {          // against the previous entry: the previous free lane's last one
                 const int pp = hibit64(fmask & ((1ull << me) - 1ull));
-                keep = !(((PAIR ? smask2 : smask) >> pp) & 1) || ns != L->res[pp];
+                keep = !(((PAIR ? smask2 : smask) >> pp) & 1) || ns != RES[pp];
             }
         }
         const bool keep2 = surv2 && (!surv || ns2 != ns);
@@ -1853,7 +1894,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             if (j == 0) fail0 = !((smask >> pf) & 1);
             if (km | km2) {  // the last entry kept: the highest lane's second entry if it kept one
                 const int hb = hibit64(km | km2);
-                last_x2 = ((km2 >> hb) & 1) ? L->res[hb] : (PAIR ? L->res1[hb] : L->res[hb]);
+                last_x2 = ((km2 >> hb) & 1) ? RES[hb] : (PAIR ? L->res1[hb] : RES[hb]);
             }
             curr_n += (uint32_t)(__popcll(km) + __popcll(km2));
             j += min(rem, PR * take);
@@ -1954,7 +1995,7 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
-    if (variant >= 40 && variant <= 55) return 1;  // seed_wp_kernel
+    if (variant >= 40 && variant <= 57) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
     return variant == 0 || (variant >= 2 && variant <= 31);
 #else
@@ -2004,6 +2045,9 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 54-55: with the k-mer table (KT; smem_gpu_set_kmer_table, no table: plain): 49's shape, 40's shape
         case 54: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 55: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 1, 3, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 56-57: descriptors by start position (DPOS): 49's shape, and with the k-mer table
+        case 56: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 57: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

@@ -165,7 +165,7 @@ def test_kernel_variants(world, gpu_device, variant):
         gpu.close()
 
 
-WP_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55]
+WP_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57]
 
 
 def _edge_reads(g):
@@ -221,7 +221,7 @@ def test_wp_kernel_parity(world, gpu_device, variant):
         gpu.close()
 
 
-@pytest.mark.parametrize("variant,k", [(54, 1), (54, 7), (54, 11), (55, 12), (55, 2)])
+@pytest.mark.parametrize("variant,k", [(54, 1), (54, 7), (54, 11), (55, 12), (55, 2), (57, 11)])
 def test_wp_kmer_table(world, gpu_device, variant, k):
     """seed_wp_kernel with the k-mer table (variants 54, 55): forward and
     backward extends whose result has <= k bases read the table; every read
