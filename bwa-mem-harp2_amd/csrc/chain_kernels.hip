@@ -1182,6 +1182,110 @@ __device__ __forceinline__ int mark_pred(const uint32_t* bm, const uint32_t* sm,
     }
 }
 
+// A big cluster's pass by the whole wave (round 5): the lane-per-cluster loop
+// left one lane walking a cluster of thousands of seeds (the human-like
+// profile's satellite reads: 8,500 seeds, 8,500 chains, 7-13 M cycles on one
+// lane).  Optimistic batches of 64 seeds in seed order: assume every seed of
+// the batch starts a chain; then a seed's lower chain (kb_intervalp) is the
+// higher of the last committed mark below its rank (mark_pred) and the
+// highest rank below it among the batch's earlier seeds, every lane tests its
+// merge at once (test_and_merge, software/bwamem.c:334-354), and the seeds
+// before the first one that does not start a clean chain (it merges, is
+// contained, or makes an equal chain key) are exactly what the serial loop
+// would have done: they are committed together.  That first seed is applied
+// as the serial loop applies it, and the next batch starts after it.  A
+// tandem-repeat cluster (several seeds per chain) advances a few seeds per
+// batch, a satellite cluster (a chain per seed) 64.  Returns true when the
+// cluster made an equal chain key (its later seeds are CODE_REPLAY).
+__device__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, uint32_t* bm, uint32_t* sm, uint32_t cs,
+                             uint32_t ce, ChainRec* chn, const SeedRec* seed, uint32_t* code, int lane,
+                             uint32_t& n_mine) {
+    uint32_t pb = cs;
+    bool cdup = false;
+    while (pb < ce && !cdup) {
+        const uint32_t p = pb + (uint32_t)lane;
+        const bool valid = p < ce;
+        uint64_t e = 0;
+        SeedRec sd{0, 0, 0};
+        uint32_t o = 0, rk = 0;
+        int A = -1;
+        if (valid) {
+            e = key[p];
+            o = (uint32_t)(e >> CL_OBITS) & (uint32_t)CL_OMASK;
+            rk = (uint32_t)e & (uint32_t)CL_OMASK;
+            sd = seed[o];
+            A = mark_pred(bm, sm, cs, rk);  // committed marks only
+        }
+        const uint32_t nb = (uint32_t)__popcll(__ballot(valid));
+        // the highest rank below mine among the batch's earlier seeds
+        int B = -1, Bl = -1;
+        for (uint32_t t = 0; t + 1 < nb; ++t) {
+            const int rt = __builtin_amdgcn_readlane((int)rk, (int)t);
+            if ((uint32_t)lane > t && rt < (int)rk && rt > B) {
+                B = rt;
+                Bl = (int)t;
+            }
+        }
+        // the batch chain's record is its first seed's, from that lane
+        const int bl4 = (Bl < 0 ? 0 : Bl) << 2;
+        const int64_t brb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl4, (int)(uint32_t)sd.rbeg) |
+                                      (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl4, (int)((uint64_t)sd.rbeg >> 32))
+                                          << 32);
+        const int32_t bqb = __builtin_amdgcn_ds_bpermute(bl4, sd.qbeg), bln = __builtin_amdgcn_ds_bpermute(bl4, sd.len);
+        const uint32_t bo = (uint32_t)__builtin_amdgcn_ds_bpermute(bl4, (int)o);
+        ChainRec c{};
+        uint32_t id = 0;
+        int mg = MERGE_NEW;
+        const bool has_lower = valid && (A >= 0 || B >= 0);
+        if (valid && B > A) {
+            c = ChainRec{brb, brb, bqb, bqb, bln, 1, bo, bo};
+            id = bo;
+        } else if (valid && A >= 0) {
+            id = (uint32_t)(key[A] >> (2 * CL_OBITS));
+            c = chn[id];
+        }
+        if (has_lower) mg = merge_test(P, c, sd.rbeg, sd.qbeg, sd.len);
+        const bool clean = mg == MERGE_NEW && !(has_lower && c.pos == sd.rbeg);
+        const uint64_t bad = __ballot(valid && !clean);
+        const uint32_t first = bad ? (uint32_t)__builtin_ctzll(bad) : nb;
+        if (valid && (uint32_t)lane < first) {  // starts a chain, as the serial loop would have it
+            chn[o] = ChainRec{sd.rbeg, sd.rbeg, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
+            code[o] = CODE_NEW;
+            mark_set(bm, sm, rk);
+        }
+        n_mine += (uint32_t)lane < first && valid ? 1u : 0u;
+        wave_fence();
+        __builtin_amdgcn_wave_barrier();
+        if (first < nb) {  // the serial loop's step for that seed
+            if ((uint32_t)lane == first) {
+                if (mg == MERGE_APPEND) {
+                    P.next[S + c.last] = o;
+                    chain_append(c, o, sd.rbeg, sd.qbeg, sd.len);
+                    chn[id] = c;
+                    code[o] = CODE_SKIP;
+                } else if (mg == MERGE_CONTAINED) {
+                    code[o] = CODE_SKIP;
+                } else {  // an equal chain key: it starts a chain, unmarked; the replay decides the rest
+                    chn[o] = ChainRec{sd.rbeg, sd.rbeg, sd.qbeg, sd.qbeg, sd.len, 1, o, o};
+                    code[o] = CODE_NEW;
+                    ++n_mine;
+                }
+            }
+            cdup = __builtin_amdgcn_readlane(mg == MERGE_NEW ? 1 : 0, (int)first) != 0;  // lane `first`'s
+            wave_fence();
+            __builtin_amdgcn_wave_barrier();
+        }
+        pb += first + 1;
+    }
+    if (cdup) {  // past the equal chain key: the tree replay decides
+        for (uint32_t p = pb + (uint32_t)lane; p < ce; p += 64) {
+            code[(uint32_t)(key[p] >> CL_OBITS) & (uint32_t)CL_OMASK] = CODE_REPLAY;
+            ++n_mine;
+        }
+    }
+    return cdup;
+}
+
 // true: chains built, tree order in ord[0, n_out); false: a cluster made an
 // equal chain key and the tree replay must finish the read.  Chain ids are
 // the index of the chain's first seed.  code[o] records, per seed, what the
@@ -1266,7 +1370,7 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
     wave_fence();
     __builtin_amdgcn_wave_barrier();
     bool dup = false;
-    uint32_t n_tot = 0, n_mine = 0;
+    uint32_t n_mine = 0;
     for (uint32_t r0 = 0; r0 < n_cl; r0 += 64) {
         const uint32_t kc = r0 + lane;
         uint32_t cs = 0, ce = 0;
@@ -1274,7 +1378,7 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
             cs = cstart[kc];
             ce = kc + 1 < n_cl ? cstart[kc + 1] : n_valid;
         }
-        uint32_t n_ch = 0;
+        if (ce - cs > P.wave_min) ce = cs;  // a big cluster: the whole wave takes it below
         bool cdup = false;
         // seed p + 1's record and its lower chain's record are loaded while
         // seed p is decided (against the marks before p); p's own mark or
@@ -1335,7 +1439,6 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
                 ++n_mine;
                 if (!cdup) {
                     mark_set(bm, sm, rk);
-                    ++n_ch;
                     // the new mark is seed p + 1's lower chain when it lies between
                     if (p + 1 < ce && rk < rk_n && (L_n < 0 || (uint32_t)L_n < rk)) {
                         L_n = (int)rk;
@@ -1345,22 +1448,37 @@ __device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t 
             }
         }
         dup = dup || cdup;
+    }
+    wave_fence();
+    __builtin_amdgcn_wave_barrier();
+    // the big clusters, one at a time by the whole wave
+    for (uint32_t r0 = 0; r0 < n_cl; r0 += 64) {
+        const uint32_t kc = r0 + lane;
+        uint32_t sz = 0;
+        if (kc < n_cl) sz = (kc + 1 < n_cl ? cstart[kc + 1] : n_valid) - cstart[kc];
+        uint64_t big = __ballot(sz > P.wave_min);
+        while (big) {
+            const uint32_t k = r0 + (uint32_t)__builtin_ctzll(big);
+            big &= big - 1;
+            const uint32_t cs = cstart[k], ce = k + 1 < n_cl ? cstart[k + 1] : n_valid;
+            if (cluster_wave(P, S, key, bm, sm, cs, ce, chn, seed, code, lane, n_mine)) dup = true;
+        }
+    }
+    wave_fence();
+    __builtin_amdgcn_wave_barrier();
+    // every cluster's chains in pos order: the marks in rank order (ranks are
+    // the read's seeds in rbeg order, and clusters are rank ranges in order)
+    uint32_t n_tot = 0;
+    for (uint32_t w0 = 0; w0 < nbw; w0 += 64) {
+        const uint32_t w = w0 + lane;
+        uint32_t bits = w < nbw ? bm[w] : 0u;
+        if (w * 32 >= n_valid) bits = 0;
         uint32_t tot;
-        const uint32_t base = wave_excl_scan(n_ch, lane, tot);
-        // the cluster's chains in pos order: its marks in rank order
-        uint32_t q = n_tot + base;
-        if (n_ch) {
-            const uint32_t w0 = cs >> 5, w1 = (ce - 1) >> 5;
-            for (uint32_t w = w0; w <= w1; ++w) {
-                uint32_t bits = bm[w];
-                if (w == w0) bits &= ~0u << (cs & 31);
-                if (w == w1) bits &= 0xffffffffu >> (31 - ((ce - 1) & 31));
-                while (bits) {
-                    const uint32_t b = (uint32_t)__builtin_ctz(bits);
-                    bits &= bits - 1;
-                    ord[q++] = (uint32_t)(key[w * 32 + b] >> (2 * CL_OBITS));
-                }
-            }
+        uint32_t q = n_tot + wave_excl_scan((uint32_t)__builtin_popcount(bits), lane, tot);
+        while (bits) {
+            const uint32_t b = (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1;
+            ord[q++] = (uint32_t)(key[w * 32 + b] >> (2 * CL_OBITS));
         }
         n_tot += tot;
     }

@@ -1481,6 +1481,8 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.sort_lane_max = 256;
     P.drop_blocked = getenv("SMEM_CHAIN_DROP_PRUNED") ? 0 : 1;
     P.replay_cache = getenv("SMEM_CHAIN_REPLAY_CACHE") && atoi(getenv("SMEM_CHAIN_REPLAY_CACHE")) == 0 ? 0 : 1;
+    P.wave_min = 256;  // SMEM_CHAIN_WAVE_MIN: clusters of more seeds by the whole wave (0xffffffff: none)
+    if (const char* v = getenv("SMEM_CHAIN_WAVE_MIN")) P.wave_min = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("SMEM_CHAIN_SORT_LANE_MAX")) P.sort_lane_max = (uint32_t)std::max(17, atoi(v));
     if (getenv("SMEM_CHAIN_DBG")) {
         HIP_TRY(b->d_dbg.ensure(256 * 16));
