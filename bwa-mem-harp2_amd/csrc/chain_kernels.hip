@@ -1202,9 +1202,13 @@ __device__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, ui
                              uint32_t& n_mine) {
     uint32_t pb = cs;
     bool cdup = false;
+    // batch size: halved while batches end early (a cluster whose seeds merge
+    // often: its lower-chain records are a round trip per batch), doubled
+    // back while they commit at least half
+    uint32_t nbmax = 64;
     while (pb < ce && !cdup) {
         const uint32_t p = pb + (uint32_t)lane;
-        const bool valid = p < ce;
+        const bool valid = p < ce && (uint32_t)lane < nbmax;
         uint64_t e = 0;
         SeedRec sd{0, 0, 0};
         uint32_t o = 0, rk = 0;
@@ -1276,6 +1280,7 @@ __device__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, ui
             __builtin_amdgcn_wave_barrier();
         }
         pb += first + 1;
+        nbmax = first >= nbmax / 2 ? (nbmax < 64 ? 2 * nbmax : 64u) : (nbmax > 8 ? nbmax / 2 : 8u);
     }
     if (cdup) {  // past the equal chain key: the tree replay decides
         for (uint32_t p = pb + (uint32_t)lane; p < ce; p += 64) {
