@@ -1279,7 +1279,7 @@ __device__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, ui
             wave_fence();
             __builtin_amdgcn_wave_barrier();
         }
-        pb += first + 1;
+        pb += first < nb ? first + 1 : nb;  // the committed seeds, and the one handled after them
         nbmax = first >= nbmax / 2 ? (nbmax < 64 ? 2 * nbmax : 64u) : (nbmax > 8 ? nbmax / 2 : 8u);
     }
     if (cdup) {  // past the equal chain key: the tree replay decides
