@@ -1397,10 +1397,13 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
 
     int phase = me < OWN ? P_FETCH : P_EXIT;  // lanes >= OWN only execute extends
     int item = -1, len = 0;
-    // next read: -2 nothing claimed, -1 claimed, -3 its offsets to be fetched, -4 in flight, >= 0 loaded.
-    // The claim's atomic and the offsets' LDS-DMA are waited for by the uniform section's vmcnt(0), never
-    // on their own: a wave stalled a memory round trip per read for the offsets before (~5 % of iterations)
+    // next read: -2 nothing claimed, -5 claim in flight, -1 claimed, -3 its offsets to be fetched, -4 in
+    // flight, >= 0 loaded.  Claimed as soon as the current read starts.  The claim's atomic and the
+    // offsets' LDS-DMA are waited for by the uniform section's vmcnt(0), never on their own: a wave
+    // stalled a memory round trip per read for each before (the compiler's atomicAdd waits for the
+    // result to broadcast it)
     int nitem = 0, nlen = -2;
+    uint32_t clead = 0;  // the last claim's leader lane (wave-uniform); its atomic's return lands in no0
     int rid = 0, nrid = 0;
     uint32_t keep_n = 0;
     uint32_t o0 = 0, no0 = 0;
@@ -1449,11 +1452,12 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
 
     for (;;) {
         if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(2);
-        if (phase == P_FETCH) {
-            if (nlen == -2) {  // claim the next read
-                nitem = atomicAdd(P.head, 1);
+        if (phase != P_EXIT) {
+            if (nlen == -5) {  // the claim returned: the leader's base + this lane's rank
+                nitem += (int)__builtin_amdgcn_readlane(no0, clead);
                 nlen = -1;
-            } else if (nlen == -1) {  // the claim returned last iteration
+            }
+            if (nlen == -1) {
                 if (nitem >= P.n_items) {
                     nlen = 0;  // nothing left: the FETCH block exits
                 } else if (P.read_ids) {  // overflow pass: through read_ids (a small launch)
@@ -1757,13 +1761,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                 }
             }
         }
-        // the query window for owners that want one, the next read's offsets
         const bool ld_q = qwant != qb && qwant != ~0u;
-        if (ld_q) __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&L->q[0]), 16, 0, 0);
-        if (nlen == -3) {
-            __builtin_amdgcn_global_load_lds(P.offs + nrid, LDS_PTR(&L->noff[0]), 16, 0, 0);
-            nlen = -4;
-        }
         // the extend: forward owners their own ik (a = x[1]), workers an entry backward (a = x[0])
         const bool task = worker || fwdreq;
         const uint64_t ra = fwdreq ? ik1 : p_x0(ent), rb = fwdreq ? ik0 : p_x1(ent), rs = fwdreq ? ik2 : p_x2(ent);
@@ -1775,6 +1773,32 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         if (kk >= P.L2[4]) kk = 0;
         if (ll >= P.L2[4]) ll = 0;
         const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
+        // the bucket indices exist here (the entry has landed) before anything below is issued
+        asm volatile("" ::"v"(bk), "v"(bl) : "memory");
+        // the query window for owners that want one, the next read's offsets and claim: issued here,
+        // after the entry's first use (the compiler's wait for an entry loaded from the arena would
+        // otherwise cover them too, LDS-DMA and the hand-rolled atomic being untracked: a second round
+        // trip before the buckets) and before the buckets, so that all land in one round trip
+        if (ld_q) __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&L->q[0]), 16, 0, 0);
+        if (nlen == -3) {
+            __builtin_amdgcn_global_load_lds(P.offs + nrid, LDS_PTR(&L->noff[0]), 16, 0, 0);
+            nlen = -4;
+        }
+        // one returning atomic per wave for every owner that wants its next read, by hand
+        // (not waited for here; read at the top of the next iteration, after the vmcnt(0) below)
+        const uint64_t want_claim = __ballot(nlen == -2 && phase != P_EXIT);
+        if (want_claim) {
+            clead = (uint32_t)(__builtin_ffsll((long long)want_claim) - 1);
+            if (nlen == -2 && phase != P_EXIT) {
+                nitem = (int)__popcll(want_claim & ((1ull << me) - 1));
+                if ((uint32_t)me == clead) {
+                    const int cnt = (int)__popcll(want_claim);
+                    // early clobber: the return register must not overlap the address
+                    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(no0) : "v"(P.head), "v"(cnt) : "memory");
+                }
+                nlen = -5;
+            }
+        }
         uint4 k0 = {0, 0, 0, 0}, k1 = {0, 0, 0, 0}, l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
         // KT: a result of at most K bases from the table (forward: q[x, i]; backward: q[i, end))
         bool ktp = false;
