@@ -1728,6 +1728,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         uint32_t s = 0, o = 0, jj = 0, lro = 0;
         bool has2 = false;
         uint4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0}, ent = {0, 0, 0, 0}, ent2 = {0, 0, 0, 0};
+        bool far = false, far2 = false;  // the entry (PAIR: the second) is in the owner's arena
         if (worker) {
             s = (uint32_t)hibit64(marks & ((2ull << rank) - 1ull));  // the segment holding task `rank`
             if constexpr (DPOS) {
@@ -1741,25 +1742,34 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             }
             jj = w0.x + PR * (rank - s);
             lro = (w0.w >> 2) & 31u;
-            if (jj < (uint32_t)NL) {
+            if (jj < (uint32_t)NL)
                 ent = L->e[WSLOT(lro, jj)][o];
-            } else {  // beyond the LDS list: the owner's arena (the bound only guards a broken list)
-                const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
-                const uint32_t at = w0.z + jj;
-                ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
-            }
+            else
+                far = true;
             if constexpr (PAIR) {
                 has2 = jj + 1 < w1.z;
                 if (has2) {
-                    if (jj + 1 < (uint32_t)NL) {
+                    if (jj + 1 < (uint32_t)NL)
                         ent2 = L->e[WSLOT(lro, jj + 1)][o];
-                    } else {
-                        const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
-                        const uint32_t at = w0.z + jj + 1;
-                        ent2 = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
-                    }
+                    else
+                        far2 = true;
                 }
             }
+        }
+        // entries beyond the LDS list: the owner's arena (the bound only guards a broken list), in a
+        // wave-uniform branch that waits for them itself -- a wait at the join would run every
+        // iteration, and one vmcnt counts the owners' result stores too (their acks, every iteration)
+        if (__builtin_expect(__any(far || far2), 0)) {
+            const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+            if (far) {
+                const uint32_t at = w0.z + jj;
+                ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+            }
+            if (PAIR && far2) {
+                const uint32_t at = w0.z + jj + 1;
+                ent2 = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         }
         const bool ld_q = qwant != qb && qwant != ~0u;
         // the extend: forward owners their own ik (a = x[1]), workers an entry backward (a = x[0])
@@ -1848,7 +1858,10 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             }
         }
         if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // vmcnt(0) as the builtin, not inline asm: the compiler's wait insertion sees it and knows the
+        // LDS-DMA above has landed (after an opaque asm wait it re-waited vmcnt(0) before the next
+        // iteration's LDS reads, i.e. for the acks of the result stores)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
         if (ld_q) {
             qv = L->q[me];
             qb = qwant;
