@@ -249,7 +249,8 @@ constexpr int kSeedDefault = 49;
 // steps then serialise), so 3.75 (profiles/r05/ab_wp)
 static int seed_lanes_per_cu(int variant) {
     switch (variant) {
-        case 44: case 45: case 46: case 49: case 50: case 51: case 52: case 53: case 54: case 56: case 57: return 960;
+        case 44: case 45: case 46: case 49: case 50: case 51: case 52: case 53: case 54: case 56: case 57:
+        case 58: case 59: case 60: case 61: case 62: return 960;
         default: return 768;
     }
 }
@@ -258,7 +259,8 @@ static int seed_lanes_per_cu(int variant) {
 static int seed_owners_per_wave(int variant) {
     switch (variant) {
         case 40: case 41: case 43: case 45: case 47: case 55: return 32;
-        case 42: case 44: case 48: case 49: case 51: case 52: case 54: case 56: case 57: return 24;
+        case 42: case 44: case 48: case 49: case 51: case 52: case 54: case 56: case 57:
+        case 58: case 59: case 60: case 61: case 62: return 24;
         case 46: case 53: return 28;
         case 50: return 20;
         default: return 64;
@@ -701,7 +703,7 @@ int smem_gpu_set_lanes_per_cu(smem_gpu_t* g, int lanes_per_cu) {
 
 int smem_gpu_set_kernel_variant(smem_gpu_t* g, int variant) {
     g_err[0] = 0;
-    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31) || (variant >= 40 && variant <= 57)))
+    if (!g || !(variant == 0 || (variant >= 2 && variant <= 31) || (variant >= 40 && variant <= 62)))
         return fail(SMEM_E_ARG, "smem_gpu_set_kernel_variant");
 
     if (!smem_seed_variant_built(variant))

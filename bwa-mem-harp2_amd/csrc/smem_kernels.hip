@@ -1380,7 +1380,13 @@ __device__ __forceinline__ void wave_lds_fence() {
 // descriptor stored at its start position, so a worker reads its owner's
 // descriptor one LDS round after the scan (three rounds before the loads:
 // start marks, owner, descriptor, entry -> descriptor, entry)
-template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false, bool KT = false, bool DPOS = false>
+// OPT (A/B of the memory-issue order; default all): 1 claim the next read when the current one ends
+// (else as soon as it starts), 2 arena entries in a wave-uniform branch with their own wait (else
+// inline: the join's wait then runs every iteration and covers the owners' result-store acks), 4 the
+// query-window / offsets DMA and the claim issued after the entry has landed (else before it: the
+// compiler's wait for the entry covers them), 8 the claim as one hand-issued atomic per wave waited
+// for by the iteration's vmcnt(0) (else the compiler's atomicAdd at the top, which waits for it)
+template <int OWN, int NL, int PRIO, int WPE = 3, bool PAIR = false, bool KT = false, bool DPOS = false, int OPT = 15>
 __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     static_assert(!(DPOS && PAIR), "DPOS keeps the owner lane where PAIR keeps prev_n");
     constexpr uint32_t PR = PAIR ? 2u : 1u;  // entries per worker lane
@@ -1450,26 +1456,58 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         }                                                                                                    \
     }
 
+// the query window for owners that want one, the next read's offsets, and (OPT 8) one returning atomic
+// per wave for every owner that wants its next read, issued by hand: not waited for here, read at the
+// top of the next iteration after the iteration's vmcnt(0); early clobber, so that the return
+// register does not overlap the address.  OPT 4 issues this after the entry has landed and before the
+// buckets (all land in one round trip); else before the entry, whose wait then covers them.
+#define WP_ISSUE()                                                                                                            \
+    {                                                                                                                         \
+        if (ld_q) __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&L->q[0]), 16, 0, 0);                             \
+        if (nlen == -3) {                                                                                                     \
+            __builtin_amdgcn_global_load_lds(P.offs + nrid, LDS_PTR(&L->noff[0]), 16, 0, 0);                                  \
+            nlen = -4;                                                                                                        \
+        }                                                                                                                     \
+        const bool wc_ = nlen == -2 && ((OPT & 1) ? phase == P_FETCH : phase != P_EXIT);                                      \
+        const uint64_t want_claim = (OPT & 8) ? __ballot(wc_) : 0ull;                                                         \
+        if (want_claim) {                                                                                                     \
+            clead = (uint32_t)(__builtin_ffsll((long long)want_claim) - 1);                                                   \
+            if (wc_) {                                                                                                        \
+                nitem = (int)__popcll(want_claim & ((1ull << me) - 1));                                                       \
+                if ((uint32_t)me == clead) {                                                                                  \
+                    const int cnt = (int)__popcll(want_claim);                                                                \
+                    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(no0) : "v"(P.head), "v"(cnt) : "memory");    \
+                }                                                                                                             \
+                nlen = -5;                                                                                                    \
+            }                                                                                                                 \
+        }                                                                                                                     \
+    }
+
     for (;;) {
         if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(2);
         if (phase != P_EXIT) {
-            if (nlen == -5) {  // the claim returned: the leader's base + this lane's rank
-                nitem += (int)__builtin_amdgcn_readlane(no0, clead);
+            if (!(OPT & 8) && nlen == -2 && phase == P_FETCH) {
+                nitem = atomicAdd(P.head, 1);  // (the compiler waits for the result here)
                 nlen = -1;
-            }
-            if (nlen == -1) {
-                if (nitem >= P.n_items) {
-                    nlen = 0;  // nothing left: the FETCH block exits
-                } else if (P.read_ids) {  // overflow pass: through read_ids (a small launch)
-                    next_offsets(P, nitem, no0, nlen, nrid);
-                } else {
-                    nrid = nitem;
-                    nlen = -3;  // offsets fetched in the uniform section
+            } else {
+                if ((OPT & 8) && nlen == -5) {  // the claim returned: the leader's base + this lane's rank
+                    nitem += (int)__builtin_amdgcn_readlane(no0, clead);
+                    nlen = -1;
                 }
-            } else if (nlen == -4) {  // landed last iteration
-                const uint4 v = L->noff[me];
-                no0 = v.x;  // batches hold < 2^32 bases: the low words
-                nlen = (int)(v.z - v.x);
+                if (nlen == -1) {
+                    if (nitem >= P.n_items) {
+                        nlen = 0;  // nothing left: the FETCH block exits
+                    } else if (P.read_ids) {  // overflow pass: through read_ids (a small launch)
+                        next_offsets(P, nitem, no0, nlen, nrid);
+                    } else {
+                        nrid = nitem;
+                        nlen = -3;  // offsets fetched in the uniform section
+                    }
+                } else if (nlen == -4) {  // landed last iteration
+                    const uint4 v = L->noff[me];
+                    no0 = v.x;  // batches hold < 2^32 bases: the low words
+                    nlen = (int)(v.z - v.x);
+                }
             }
         }
         // ---- owners: advance the state machine one pass (seed_kernel's
@@ -1742,24 +1780,36 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             }
             jj = w0.x + PR * (rank - s);
             lro = (w0.w >> 2) & 31u;
-            if (jj < (uint32_t)NL)
+            if (jj < (uint32_t)NL) {
                 ent = L->e[WSLOT(lro, jj)][o];
-            else
+            } else if constexpr (OPT & 2) {
                 far = true;
+            } else {
+                const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                const uint32_t at = w0.z + jj;
+                ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+            }
             if constexpr (PAIR) {
                 has2 = jj + 1 < w1.z;
                 if (has2) {
-                    if (jj + 1 < (uint32_t)NL)
+                    if (jj + 1 < (uint32_t)NL) {
                         ent2 = L->e[WSLOT(lro, jj + 1)][o];
-                    else
+                    } else if constexpr (OPT & 2) {
                         far2 = true;
+                    } else {
+                        const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                        const uint32_t at = w0.z + jj + 1;
+                        ent2 = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
+                    }
                 }
             }
         }
+        const bool ld_q = qwant != qb && qwant != ~0u;
+        if constexpr (!(OPT & 4)) WP_ISSUE();
         // entries beyond the LDS list: the owner's arena (the bound only guards a broken list), in a
         // wave-uniform branch that waits for them itself -- a wait at the join would run every
         // iteration, and one vmcnt counts the owners' result stores too (their acks, every iteration)
-        if (__builtin_expect(__any(far || far2), 0)) {
+        if (OPT & 2 && __builtin_expect(__any(far || far2), 0)) {
             const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
             if (far) {
                 const uint32_t at = w0.z + jj;
@@ -1771,7 +1821,6 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             }
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         }
-        const bool ld_q = qwant != qb && qwant != ~0u;
         // the extend: forward owners their own ik (a = x[1]), workers an entry backward (a = x[0])
         const bool task = worker || fwdreq;
         const uint64_t ra = fwdreq ? ik1 : p_x0(ent), rb = fwdreq ? ik0 : p_x1(ent), rs = fwdreq ? ik2 : p_x2(ent);
@@ -1783,31 +1832,10 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         if (kk >= P.L2[4]) kk = 0;
         if (ll >= P.L2[4]) ll = 0;
         const uint32_t bk = (uint32_t)(kk >> 6), bl = (uint32_t)(ll >> 6);
-        // the bucket indices exist here (the entry has landed) before anything below is issued
-        asm volatile("" ::"v"(bk), "v"(bl) : "memory");
-        // the query window for owners that want one, the next read's offsets and claim: issued here,
-        // after the entry's first use (the compiler's wait for an entry loaded from the arena would
-        // otherwise cover them too, LDS-DMA and the hand-rolled atomic being untracked: a second round
-        // trip before the buckets) and before the buckets, so that all land in one round trip
-        if (ld_q) __builtin_amdgcn_global_load_lds(P.codes + qwant, LDS_PTR(&L->q[0]), 16, 0, 0);
-        if (nlen == -3) {
-            __builtin_amdgcn_global_load_lds(P.offs + nrid, LDS_PTR(&L->noff[0]), 16, 0, 0);
-            nlen = -4;
-        }
-        // one returning atomic per wave for every owner that wants its next read, by hand
-        // (not waited for here; read at the top of the next iteration, after the vmcnt(0) below)
-        const uint64_t want_claim = __ballot(nlen == -2 && phase != P_EXIT);
-        if (want_claim) {
-            clead = (uint32_t)(__builtin_ffsll((long long)want_claim) - 1);
-            if (nlen == -2 && phase != P_EXIT) {
-                nitem = (int)__popcll(want_claim & ((1ull << me) - 1));
-                if ((uint32_t)me == clead) {
-                    const int cnt = (int)__popcll(want_claim);
-                    // early clobber: the return register must not overlap the address
-                    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(no0) : "v"(P.head), "v"(cnt) : "memory");
-                }
-                nlen = -5;
-            }
+        if constexpr (OPT & 4) {
+            // the bucket indices exist here (the entry has landed) before anything below is issued
+            asm volatile("" ::"v"(bk), "v"(bl) : "memory");
+            WP_ISSUE();
         }
         uint4 k0 = {0, 0, 0, 0}, k1 = {0, 0, 0, 0}, l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
         // KT: a result of at most K bases from the table (forward: q[x, i]; backward: q[i, end))
@@ -2032,7 +2060,7 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 // SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
 // in every library for numbers already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
-    if (variant >= 40 && variant <= 57) return 1;  // seed_wp_kernel
+    if (variant >= 40 && variant <= 62) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
     return variant == 0 || (variant >= 2 && variant <= 31);
 #else
@@ -2085,6 +2113,14 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         // 56-57: descriptors by start position (DPOS): 49's shape, and with the k-mer table
         case 56: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 57: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 58-62: 49 with the memory-issue order taken apart (OPT bits, seed_wp_kernel): 58 none, 59 no
+        // uniform arena branch, 60 the DMA / claim before the entry, 61 the claim when a read starts,
+        // 62 the compiler's atomicAdd
+        case 58: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 0>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 59: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 13>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 60: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 11>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 61: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 14>), dim3(grid), dim3(block), 0, st, *P); break;
+        case 62: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 7>), dim3(grid), dim3(block), 0, st, *P); break;
 #ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in

@@ -165,7 +165,7 @@ def test_kernel_variants(world, gpu_device, variant):
         gpu.close()
 
 
-WP_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57]
+WP_VARIANTS = [40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62]
 
 
 def _edge_reads(g):
