@@ -1482,8 +1482,12 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.wave_sort = getenv("SMEM_CHAIN_SERIAL_SORT") ? 0 : 1;
     P.sort_lane_max = 256;
     P.drop_blocked = getenv("SMEM_CHAIN_DROP_PRUNED") ? 0 : 1;
-    P.replay_cache = getenv("SMEM_CHAIN_REPLAY_CACHE") && atoi(getenv("SMEM_CHAIN_REPLAY_CACHE")) == 0 ? 0 : 1;
-    P.wave_min = 256;  // SMEM_CHAIN_WAVE_MIN: clusters of more seeds by the whole wave (0xffffffff: none)
+    // the replay's chain-record cache and the wave-batched big clusters are off by default: both
+    // measured slower (filtered, 1M reads: uniform 14.7 -> 16.1-16.2 ms with both, human-like 26.2 ->
+    // 26.6-27.4; each alone between; profiles/r05/chain_ab.txt).  SMEM_CHAIN_REPLAY_CACHE=1 and
+    // SMEM_CHAIN_WAVE_MIN=<seeds> turn them on (tests/test_gpu_chain.py keeps them bit-exact)
+    P.replay_cache = getenv("SMEM_CHAIN_REPLAY_CACHE") && atoi(getenv("SMEM_CHAIN_REPLAY_CACHE")) == 1 ? 1 : 0;
+    P.wave_min = 0xFFFFFFFFu;  // SMEM_CHAIN_WAVE_MIN: clusters of more seeds by the whole wave
     if (const char* v = getenv("SMEM_CHAIN_WAVE_MIN")) P.wave_min = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("SMEM_CHAIN_SORT_LANE_MAX")) P.sort_lane_max = (uint32_t)std::max(17, atoi(v));
     if (getenv("SMEM_CHAIN_DBG")) {
