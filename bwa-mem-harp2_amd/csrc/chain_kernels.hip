@@ -550,52 +550,62 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
     for (int k = lane; k < I0; k += 64) kidx[k] = (uint32_t)k;
     wave_fence();
     __builtin_amdgcn_wave_barrier();
-    // the kept list's first 64 records live in registers (lane j: kept j),
-    // the chains i in registers a block of 64 at a time: a chain whose
-    // droppers' prefix ends inside the first 64 is decided without a load
+    // the kept list's first 64 records live in registers (lane j: kept j);
+    // the chains i go 64 at a time, one per lane (round 5; before, one chain
+    // at a time against the kept list across the lanes: ~900 cycles a chain
+    // on the giants, whose drop loops walk 8,000-10,000 chains).  A block:
+    // (1) every lane walks the kept list as it stands, in order, while the
+    //     kept chain can drop its chain (a prefix: the list is in weight
+    //     order), to the first significant overlap -- one broadcast record a
+    //     step for all lanes;
+    // (2) the lanes left undecided, in order: the first is kept (it was tested
+    //     against every kept chain before it), and the later undecided lanes
+    //     are tested against it.
+    // Same jst / kept list as the chain-at-a-time loop.
     int m = I0;
     FltRec kr{0, 0, 0, 0, -1};
     if (lane < I0) kr = a[lane];
     for (int blk = I0; blk < n; blk += 64) {
-        FltRec rb{0, 0, 0, 0, -1};
-        if (blk + lane < n) rb = a[blk + lane];
-        const int nb = n - blk < 64 ? n - blk : 64;
-        for (int t = 0; t < nb; ++t) {
-            const int i = blk + t;
-            const FltRec ai{__builtin_amdgcn_readlane(rb.beg, t), __builtin_amdgcn_readlane(rb.end, t),
-                            __builtin_amdgcn_readlane(rb.w, t), i, -1};
-            const int mr = m < 64 ? m : 64;
-            const bool can_r = lane < mr && flt_can_drop(ai, kr, drop_ratio, msl);
-            const uint64_t bh_r = __ballot(can_r && flt_sig(ai, kr, mask_level));
-            int jstar = bh_r ? (int)__builtin_ctzll(bh_r) : -1;
-            if (!bh_r && m > 64 && __ballot(can_r) == __ballot(lane < mr)) {
-                // the prefix goes on past the registers
-                for (int base = 64; base < m; base += 64) {
-                    const int j = base + lane;
-                    bool can = false, hit = false;
-                    if (j < m) {
-                        const FltRec aj = a[kidx[j]];
-                        can = flt_can_drop(ai, aj, drop_ratio, msl);
-                        hit = can && flt_sig(ai, aj, mask_level);
-                    }
-                    const uint64_t bh = __ballot(hit);
-                    if (bh) {
-                        jstar = base + (int)__builtin_ctzll(bh);
-                        break;
-                    }
-                    if (__ballot(can) != __ballot(j < m)) break;  // the prefix ends in this chunk
-                }
+        const int i = blk + lane;
+        const bool valid = i < n;
+        FltRec ai{0, 0, 0, 0, -1};
+        if (valid) ai = a[i];
+        int jstar = -1;
+        const int m0 = m;
+        uint64_t srch = __ballot(valid);
+        for (int j = 0; srch && j < m0; ++j) {
+            FltRec aj{0, 0, 0, 0, -1};
+            if (j < 64) {
+                aj.beg = __builtin_amdgcn_readlane(kr.beg, j);
+                aj.end = __builtin_amdgcn_readlane(kr.end, j);
+                aj.w = __builtin_amdgcn_readlane(kr.w, j);
+            } else {
+                const uint32_t o = (uint32_t)__builtin_amdgcn_readfirstlane((int)kidx[j]);
+                aj = a[o];
             }
-            jstar = __builtin_amdgcn_readfirstlane(jstar);
-            if (lane == 0) {
-                jst[i] = jstar;
-                if (jstar < 0) kidx[m] = (uint32_t)i;
-            }
-            if (jstar < 0) {
-                if (lane == m) kr = ai;
-                ++m;
-            }
+            const bool on = (srch >> lane) & 1;
+            const bool can = on && flt_can_drop(ai, aj, drop_ratio, msl);
+            const bool hit = can && flt_sig(ai, aj, mask_level);
+            if (hit) jstar = j;
+            srch &= ~__ballot(on && (hit || !can));
         }
+        uint64_t und = __ballot(valid && jstar < 0);
+        while (und) {
+            const int t = (int)__builtin_ctzll(und);
+            und &= und - 1;
+            const FltRec at{__builtin_amdgcn_readlane(ai.beg, t), __builtin_amdgcn_readlane(ai.end, t),
+                            __builtin_amdgcn_readlane(ai.w, t), blk + t, -1};
+            const int km = m++;
+            if (lane == 0) kidx[km] = (uint32_t)(blk + t);
+            if (lane == km) kr = at;
+            const bool later = (und >> lane) & 1;
+            const bool hit = later && flt_can_drop(ai, at, drop_ratio, msl) && flt_sig(ai, at, mask_level);
+            if (hit) jstar = km;
+            und &= ~__ballot(hit);
+        }
+        if (valid) jst[i] = jstar;
+        wave_fence();
+        __builtin_amdgcn_wave_barrier();
     }
     wave_fence();
     __builtin_amdgcn_wave_barrier();
