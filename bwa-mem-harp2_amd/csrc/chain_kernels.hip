@@ -534,7 +534,7 @@ __device__ __forceinline__ bool flt_can_drop(const FltRec& ai, const FltRec& aj,
 }
 
 __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_t* U, int n, float mask_level,
-                                float drop_ratio, int msl, int lane) {
+                                float drop_ratio, int msl, int lane, uint64_t* dbg = nullptr) {
     // I0: the first i >= 1 that a[0] can drop
     const FltRec a0 = a[0];
     int I0 = n;
@@ -573,21 +573,24 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
         int jstar = -1;
         const int m0 = m;
         uint64_t srch = __ballot(valid);
-        for (int j = 0; srch && j < m0; ++j) {
-            FltRec aj{0, 0, 0, 0, -1};
-            if (j < 64) {
-                aj.beg = __builtin_amdgcn_readlane(kr.beg, j);
-                aj.end = __builtin_amdgcn_readlane(kr.end, j);
-                aj.w = __builtin_amdgcn_readlane(kr.w, j);
-            } else {
-                const uint32_t o = (uint32_t)__builtin_amdgcn_readfirstlane((int)kidx[j]);
-                aj = a[o];
+        // the kept list 64 records at a time: the first 64 from the registers,
+        // later tiles gathered one record a lane (one round trip a tile)
+        for (int j0 = 0; srch && j0 < m0; j0 += 64) {
+            FltRec tile = kr;
+            if (j0) {
+                const int jj = j0 + lane;
+                if (jj < m0) tile = a[kidx[jj]];
             }
-            const bool on = (srch >> lane) & 1;
-            const bool can = on && flt_can_drop(ai, aj, drop_ratio, msl);
-            const bool hit = can && flt_sig(ai, aj, mask_level);
-            if (hit) jstar = j;
-            srch &= ~__ballot(on && (hit || !can));
+            const int jn = m0 - j0 < 64 ? m0 - j0 : 64;
+            for (int jl = 0; srch && jl < jn; ++jl) {
+                const FltRec aj{__builtin_amdgcn_readlane(tile.beg, jl), __builtin_amdgcn_readlane(tile.end, jl),
+                                __builtin_amdgcn_readlane(tile.w, jl), 0, -1};
+                const bool on = (srch >> lane) & 1;
+                const bool can = on && flt_can_drop(ai, aj, drop_ratio, msl);
+                const bool hit = can && flt_sig(ai, aj, mask_level);
+                if (hit) jstar = j0 + jl;
+                srch &= ~__ballot(on && (hit || !can));
+            }
         }
         uint64_t und = __ballot(valid && jstar < 0);
         while (und) {
@@ -609,6 +612,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
     }
     wave_fence();
     __builtin_amdgcn_wave_barrier();
+    if (dbg && lane == 0) dbg[13] = __builtin_readcyclecounter();  // SMEM_CHAIN_DBG: the kept list's end
     // p2, 64 chains i at a time
     int nu = 0, m_run = 0;
     for (int b = 0; b < n; b += 64) {
@@ -662,17 +666,20 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
         wave_fence();
         __builtin_amdgcn_wave_barrier();
     }
-    // compact the kept records (with their p2) to a[0 .. m)
-    for (int base = 0; base < m; base += 64) {
+    // compact the kept records (with their p2) to a[0 .. m): kidx[k] >= k, so
+    // a chunk's loads never read a slot an earlier chunk stored, and its own
+    // stores wait for its loads (their data); a kept prefix stays in place
+    // (the heaviest chain drops nothing of it: a whole all-kept read moves nothing)
+    for (int base = I0 & ~63; base < m; base += 64) {
         const int k = base + lane;
+        const uint32_t src = k < m ? kidx[k] : (uint32_t)k;
+        if (__ballot(src != (uint32_t)k) == 0) continue;
         FltRec r{};
-        if (k < m) r = a[kidx[k]];
-        wave_fence();
-        __builtin_amdgcn_wave_barrier();
-        if (k < m) a[k] = r;
-        wave_fence();
-        __builtin_amdgcn_wave_barrier();
+        if (src != (uint32_t)k) r = a[src];
+        if (src != (uint32_t)k) a[k] = r;
     }
+    wave_fence();
+    __builtin_amdgcn_wave_barrier();
     return m;
 }
 
@@ -2182,8 +2189,8 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 uint32_t* xs = x_lds ? kidx + n : reinterpret_cast<uint32_t*>(P.node + (S / 7 + 3ull * (uint64_t)r));
                 jst = reinterpret_cast<int32_t*>(xs);
                 U = xs + n;
-                m = in_lds ? flt_drop_blocked(la, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane)
-                           : flt_drop_blocked(ga, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane);
+                m = in_lds ? flt_drop_blocked(la, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane, dbg)
+                           : flt_drop_blocked(ga, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane, dbg);
             } else if (P.drop_ratio > 0.f) {
                 // U: LDS after the records while both fit, else the read's ord
                 // rows (free until the marks below)

@@ -63,7 +63,7 @@ def main():
         out["heavy_phases_cycles"] = [dict(total=int(x[9] - x[2]), us=(x[15] - x[14]) / 100.0, read=int(x[0]), seeds=int(x[1]), chains=int(x[4]), insert=int(x[3] - x[2]),
                                            weights=int(x[5] - x[3]), sort=int(x[6] - x[5]), drop=int(x[7] - x[6]),
                                            kept=int(x[8]), tail=int(x[9] - x[7]), replay=int(x[10]), cluster_pass=int(x[11] - x[2]) if x[11] else 0,
-                                           n_cand=int(x[12])) for x in d[:16] if x[9]]
+                                           n_cand=int(x[12]), drop_kept=int(x[13] - x[6]) if x[13] > x[6] else None) for x in d[:16] if x[9]]
     res = b.fetch()
     n_seed = np.array([res.read_sa(i).size for i in range(reads.n)]) if reads.n <= 2_000_000 else None
     n_chain = np.diff(res.chain_off)
