@@ -533,7 +533,7 @@ __device__ __forceinline__ bool flt_can_drop(const FltRec& ai, const FltRec& aj,
     return (float)ai.w < (float)aj.w * drop_ratio && aj.w - ai.w >= msl << 1;
 }
 
-__device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_t* U, int n, float mask_level,
+__device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* U, int n, float mask_level,
                                 float drop_ratio, int msl, int lane, uint64_t* dbg = nullptr) {
     // I0: the first i >= 1 that a[0] can drop
     const FltRec a0 = a[0];
@@ -626,10 +626,12 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
             ji = i < I0 ? -1 : jst[i];
             kept = ji < 0;
         }
-        // the block's kept chains join U (they can be marked by later i of the block)
+        // the block's kept chains join U (they can be marked by later i of the
+        // block); a U entry carries what the test needs (kept index, position,
+        // query span): one load a member, not three dependent ones
         const uint64_t bk = __ballot(kept);
         const uint32_t below = (uint32_t)__builtin_popcountll(bk & ((1ull << lane) - 1));
-        if (kept) U[nu + below] = (uint32_t)(m_run + below);
+        if (kept) U[nu + below] = make_uint4(m_run + below, (uint32_t)i, (uint32_t)bi, (uint32_t)ei);
         nu += __builtin_popcountll(bk);
         m_run += __builtin_popcountll(bk);
         wave_fence();
@@ -639,15 +641,24 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
         for (int c = 0; c < nu; c += 64) {
             const int u = c + lane;
             const bool act = u < nu;
-            uint32_t kp = 0, oj = 0;
-            FltRec rj{0, 0, 0, 0, -1};
-            if (act) {
-                kp = U[u];
-                oj = kidx[kp];
-                rj = a[oj];
-            }
+            uint4 ue = make_uint4(0, 0, 0, 0);
+            if (act) ue = U[u];
+            const uint32_t kp = ue.x, oj = ue.y;
+            const FltRec rj{(int32_t)ue.z, (int32_t)ue.w, 0, 0, -1};
             int hit = -1;
-            for (int t = 0; t < nb; ++t) {
+            // from the first chain after the earliest searching member; done
+            // when every member found its chain
+            int t0 = nb;
+            {
+                const int st = act ? ((int)oj + 1 - b > 0 ? (int)oj + 1 - b : 0) : nb;
+                t0 = st;
+                for (int off = 32; off > 0; off >>= 1) {
+                    const int o2 = __shfl_xor(t0, off);
+                    t0 = o2 < t0 ? o2 : t0;
+                }
+            }
+            for (int t = t0; t < nb; ++t) {
+                if ((t & 7) == 0 && !__ballot(act && hit < 0)) break;
                 const int32_t bt = __builtin_amdgcn_readlane(bi, t), et = __builtin_amdgcn_readlane(ei, t);
                 const int32_t jt = __builtin_amdgcn_readlane(ji, t);
                 if (act && hit < 0 && (uint32_t)(b + t) > oj && (jt < 0 || (int32_t)kp <= jt) &&
@@ -659,7 +670,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint32_
             const uint64_t bq = __ballot(keep);
             wave_fence();
             __builtin_amdgcn_wave_barrier();
-            if (keep) U[out + __builtin_popcountll(bq & ((1ull << lane) - 1))] = kp;
+            if (keep) U[out + __builtin_popcountll(bq & ((1ull << lane) - 1))] = ue;
             out += __builtin_popcountll(bq);
         }
         nu = out;
@@ -1898,8 +1909,11 @@ __device__ void wave_bitonic32(uint32_t* key, uint32_t npad, int lane) {
 // the whole ks_introsort(mem_flt) for n < 2^16 chains of weights in
 // [0, 2^16); small: 3 words per lane-cut segment, stk: 3 words per wave-cut
 // segment (at most 64 pending); keys: npad words; tmp: n records
+// cnt / cnt_cap: LDS words free once the partitions are done (the closing
+// sort's weight counts); wmax: the largest weight
 __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t* tl, uint32_t* tr, uint32_t* keys,
-                              FltRec* tmp, uint32_t* small, uint32_t* stk, int lane) {
+                              FltRec* tmp, uint32_t* small, uint32_t* stk, int lane, int wmin, int wmax,
+                              uint32_t* cnt, uint32_t cnt_cap, uint64_t* dbg = nullptr) {
     if (n < 2) return;
     if (n == 2) {
         if (lane == 0 && flt_lt(a[1], a[0])) flt_swap(a, 0, 1);
@@ -1929,25 +1943,79 @@ __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t
         wave_sync_mem();
         if (--dd == 0) {
             if (lane == 0) flt_combsort(a + s, t - s + 1);
+            if (dbg && lane == 0) dbg[16] += 1, dbg[17] += t - s + 1;
         } else {
             const uint32_t i = flt_partition_wave(a, s, t, tl, tr, lane);
+            if (dbg && lane == 0) dbg[18] += 1, dbg[19] += t - s + 1;
             if (i - s > 16) add(s, i - 1, dd);
             if (t - i > 16) add(i + 1, t, dd);
         }
         wave_sync_mem();
     }
+    if (dbg && lane == 0) dbg[20] = __builtin_readcyclecounter(), dbg[21] = n_small;
     for (uint32_t q = lane; q < n_small; q += 64)
         flt_sort_seg_serial(a, small[3 * q], small[3 * q + 1], (int)small[3 * q + 2]);
     wave_sync_mem();
+    if (dbg && lane == 0) dbg[22] = __builtin_readcyclecounter();
     // the closing insertion sort: a stable sort by weight, descending
-    uint32_t npad = 2;
-    while (npad < n) npad <<= 1;
-    for (uint32_t p = lane; p < npad; p += 64)
-        keys[p] = p < n ? ((uint32_t)(0xFFFF - a[p].w) << 16) | p : 0xFFFFFFFFu;
-    wave_sync_mem();
-    wave_bitonic32(keys, npad, lane);
-    for (uint32_t r = lane; r < n; r += 64) tmp[r] = a[keys[r] & 0xFFFFu];
-    wave_sync_mem();
+    const uint32_t R = (uint32_t)(wmax - wmin) + 1u;
+    if (cnt && R <= cnt_cap) {
+        // by counting (weights span R <= cnt_cap values): counts by wmax - w
+        // in LDS, their exclusive scan, then the records scattered 64 at a
+        // time in array order, each lane behind the earlier lanes of its
+        // weight -- stable, as the insertion sort (round 5: the bitonic sort of
+        // (weight, position) keys over the node pool took ~2.8 M cycles of a
+        // 5,000-chain read)
+        for (uint32_t q = lane; q < R; q += 64) cnt[q] = 0;
+        wave_sync_mem();
+        for (uint32_t p = lane; p < n; p += 64) atomicAdd(&cnt[(uint32_t)(wmax - a[p].w)], 1u);
+        wave_sync_mem();
+        uint32_t run = 0;
+        for (uint32_t q0 = 0; q0 < R; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            const uint32_t v = q < R ? cnt[q] : 0u;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan(v, lane, tot);
+            if (q < R) cnt[q] = run + ex;
+            run += tot;
+        }
+        wave_sync_mem();
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t p = c + (uint32_t)lane;
+            const bool valid = p < n;
+            FltRec r{};
+            uint32_t d = 0xFFFFFFFFu;
+            if (valid) {
+                r = a[p];
+                d = (uint32_t)(wmax - r.w);
+            }
+            uint64_t rem = __ballot(valid);
+            uint32_t pos = 0;
+            while (rem) {
+                const int ld = (int)__builtin_ctzll(rem);
+                const uint32_t dl = (uint32_t)__builtin_amdgcn_readlane((int)d, ld);
+                const uint64_t m = __ballot(d == dl);
+                const uint32_t b = cnt[dl];
+                if (d == dl) pos = b + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+                wave_sync_mem();
+                if (lane == ld) cnt[dl] = b + (uint32_t)__builtin_popcountll(m);
+                wave_sync_mem();
+                rem &= ~m;
+            }
+            if (valid) tmp[pos] = r;
+        }
+        wave_sync_mem();
+    } else {
+        uint32_t npad = 2;
+        while (npad < n) npad <<= 1;
+        for (uint32_t p = lane; p < npad; p += 64)
+            keys[p] = p < n ? ((uint32_t)(0xFFFF - a[p].w) << 16) | p : 0xFFFFFFFFu;
+        wave_sync_mem();
+        wave_bitonic32(keys, npad, lane);
+        for (uint32_t r = lane; r < n; r += 64) tmp[r] = a[keys[r] & 0xFFFFu];
+        wave_sync_mem();
+    }
+    if (dbg && lane == 0) dbg[24] = __builtin_readcyclecounter();
     for (uint32_t r = lane; r < n; r += 64) a[r] = tmp[r];
     wave_sync_mem();
 }
@@ -2019,7 +2087,7 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
         uint32_t* ord = P.ord + S;
         uint32_t* ord2 = P.ord2 + S;
         __shared__ int s_n;
-        uint64_t* dbg = (P.dbg && item < 256) ? P.dbg + item * 16 : nullptr;
+        uint64_t* dbg = (P.dbg && item < 256) ? P.dbg + item * 32 : nullptr;  // 32 words a read
         if (dbg && lane == 0) {
             dbg[0] = r;
             dbg[1] = P.occ_off[i1] - S;
@@ -2118,14 +2186,63 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
             for (int i = lane; i < n; i += 64) ord2[i] = ord[i];
         } else {
             const bool in_lds = (uint64_t)n * sizeof(FltRec) <= (uint64_t)P.lds_bytes;
+            if (dbg && lane == 0) dbg[23] = in_lds;
             FltRec* la = reinterpret_cast<FltRec*>(lds_raw);
             FltRec* ga = P.flt + S;
-            // weights, one chain per lane
-            for (int i = lane; i < n; i += 64) {
-                const ChainRec c = P.chn[S + ord[i]];
-                const FltRec f{c.first_qbeg, c.last_qbeg + c.last_len, chain_weight(c, P.seed + S, P.next + S), i, -1};
-                if (in_lds) la[i] = f;
-                else ga[i] = f;
+            // weights, four chains per lane at a time: their seed walks are
+            // independent, so each step's loads overlap (one walk per lane was
+            // a dependent round trip per seed, ~2 M cycles on a 5,000-chain
+            // read).  Only the query-coordinate loop of mem_chain_weight: its
+            // second loop starts from the first's total and only adds (this
+            // version never resets w), so min(w, tmp) is tmp (chain_weight)
+            for (int i0 = lane; i0 < n; i0 += 256) {
+                ChainRec c[4];
+                uint32_t o[4];
+                int rem[4], w[4];
+                int64_t end[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int i = i0 + 64 * k;
+                    rem[k] = 0;
+                    if (i < n) {
+                        c[k] = P.chn[S + ord[i]];
+                        rem[k] = c[k].n;
+                        o[k] = c[k].first;
+                    }
+                    w[k] = 0;
+                    end[k] = 0;
+                }
+                while (rem[0] > 0 || rem[1] > 0 || rem[2] > 0 || rem[3] > 0) {
+                    SeedRec sd[4];
+                    uint32_t nx[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (rem[k] > 0) {
+                            sd[k] = P.seed[S + o[k]];
+                            nx[k] = P.next[S + o[k]];
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (rem[k] > 0) {
+                            const SeedRec& q = sd[k];
+                            if (q.qbeg >= end[k]) w[k] += q.len;
+                            else if (q.qbeg + q.len > end[k]) w[k] = (int)(w[k] + (q.qbeg + q.len - end[k]));
+                            end[k] = end[k] > q.qbeg + q.len ? end[k] : q.qbeg + q.len;
+                            o[k] = nx[k];
+                            --rem[k];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int i = i0 + 64 * k;
+                    if (i < n) {
+                        const FltRec f{c[k].first_qbeg, c[k].last_qbeg + c[k].last_len, w[k], i, -1};
+                        if (in_lds) la[i] = f;
+                        else ga[i] = f;
+                    }
+                }
             }
             __syncthreads();
             if (dbg && lane == 0) dbg[5] = __builtin_readcyclecounter();
@@ -2152,8 +2269,13 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 if (in_lds && (uint64_t)n * sizeof(FltRec) + need <= P.lds_bytes) tl = reinterpret_cast<uint32_t*>(la + n);
                 else if (!in_lds && need <= P.lds_bytes) tl = reinterpret_cast<uint32_t*>(lds_raw);
                 else tl = reinterpret_cast<uint32_t*>(gs + (uint64_t)n * sizeof(FltRec));
+                // the closing sort's counts: the LDS after the records (the
+                // stopper lists there are dead by then), or all of it
+                uint32_t* cnt = in_lds ? reinterpret_cast<uint32_t*>(la + n) : reinterpret_cast<uint32_t*>(lds_raw);
+                const uint64_t cnt_room = ((uint64_t)P.lds_bytes - (in_lds ? (uint64_t)n * sizeof(FltRec) : 0)) / 4;
+                const uint32_t cnt_cap = P.sort_count ? (uint32_t)(cnt_room < 65536 ? cnt_room : 65536) : 0u;
                 flt_sort_wave(in_lds ? la : ga, (uint32_t)n, P.sort_lane_max, tl, tl + n, tl + 2 * n,
-                              reinterpret_cast<FltRec*>(gs), ord2, s_stk, lane);
+                              reinterpret_cast<FltRec*>(gs), ord2, s_stk, lane, wmin, wmax, cnt, cnt_cap, dbg);
             } else if (lane == 0) {
                 if (in_lds) flt_sort(la, (uint32_t)n, s_stk);
                 else flt_sort(ga, (uint32_t)n, s_stk);
@@ -2175,12 +2297,12 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 // kidx / jst / U: LDS after the records while all fit, else
                 // kidx in the read's ord rows (free until the marks below),
                 // jst and U in its kbtree node pool (free after the sort; the
-                // pool holds >= (E - S) / 7 + 2 nodes of 256 B, > 8 n bytes
-                // as n <= E - S)
-                const bool x_lds = in_lds && (uint64_t)n * (sizeof(FltRec) + 12) <= (uint64_t)P.lds_bytes;
+                // pool holds >= (E - S) / 7 + 2 nodes of 256 B, > 36 n bytes
+                // as n <= E - S: jst takes 4 n, U 16 n)
+                const bool x_lds = in_lds && (uint64_t)n * (sizeof(FltRec) + 24) + 16 <= (uint64_t)P.lds_bytes;
                 uint32_t* kidx;
                 int32_t* jst;
-                uint32_t* U;
+                uint4* U;
                 if (x_lds) {
                     kidx = reinterpret_cast<uint32_t*>(la + n);
                 } else {
@@ -2188,7 +2310,8 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 }
                 uint32_t* xs = x_lds ? kidx + n : reinterpret_cast<uint32_t*>(P.node + (S / 7 + 3ull * (uint64_t)r));
                 jst = reinterpret_cast<int32_t*>(xs);
-                U = xs + n;
+                // 16-B entries (kept index, position, span), 16-B aligned
+                U = reinterpret_cast<uint4*>((reinterpret_cast<uintptr_t>(xs + n) + 15) & ~(uintptr_t)15);
                 m = in_lds ? flt_drop_blocked(la, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane, dbg)
                            : flt_drop_blocked(ga, kidx, jst, U, n, P.mask_level, P.drop_ratio, P.min_seed_len, lane, dbg);
             } else if (P.drop_ratio > 0.f) {

@@ -1488,11 +1488,12 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     // SMEM_CHAIN_WAVE_MIN=<seeds> turn them on (tests/test_gpu_chain.py keeps them bit-exact)
     P.replay_cache = getenv("SMEM_CHAIN_REPLAY_CACHE") && atoi(getenv("SMEM_CHAIN_REPLAY_CACHE")) == 1 ? 1 : 0;
     P.wave_min = 0xFFFFFFFFu;  // SMEM_CHAIN_WAVE_MIN: clusters of more seeds by the whole wave
+    P.sort_count = getenv("SMEM_CHAIN_SORT_COUNT") && atoi(getenv("SMEM_CHAIN_SORT_COUNT")) == 0 ? 0 : 1;
     if (const char* v = getenv("SMEM_CHAIN_WAVE_MIN")) P.wave_min = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("SMEM_CHAIN_SORT_LANE_MAX")) P.sort_lane_max = (uint32_t)std::max(17, atoi(v));
     if (getenv("SMEM_CHAIN_DBG")) {
-        HIP_TRY(b->d_dbg.ensure(256 * 16));
-        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 256 * 16 * sizeof(uint64_t), b->st));
+        HIP_TRY(b->d_dbg.ensure(256 * 32));
+        HIP_TRY(hipMemsetAsync(b->d_dbg.p, 0, 256 * 32 * sizeof(uint64_t), b->st));
         P.dbg = b->d_dbg.p;
     }
     // the heavy reads' second tier beside the giants (SMEM_CHAIN_STREAMS=1:

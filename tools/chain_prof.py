@@ -58,12 +58,15 @@ def main():
     if own.sweep:
         b.chain(idx.seq_len // 2, filter=True)
     if os.environ.get("SMEM_CHAIN_DBG"):
-        d = b.debug_words(256 * 16).reshape(256, 16).astype(np.int64)
+        d = b.debug_words(256 * 32).reshape(256, 32).astype(np.int64)
         d = d[np.argsort(-(d[:, 9] - d[:, 2]))]
         out["heavy_phases_cycles"] = [dict(total=int(x[9] - x[2]), us=(x[15] - x[14]) / 100.0, read=int(x[0]), seeds=int(x[1]), chains=int(x[4]), insert=int(x[3] - x[2]),
                                            weights=int(x[5] - x[3]), sort=int(x[6] - x[5]), drop=int(x[7] - x[6]),
                                            kept=int(x[8]), tail=int(x[9] - x[7]), replay=int(x[10]), cluster_pass=int(x[11] - x[2]) if x[11] else 0,
-                                           n_cand=int(x[12]), drop_kept=int(x[13] - x[6]) if x[13] > x[6] else None) for x in d[:16] if x[9]]
+                                           n_cand=int(x[12]), drop_kept=int(x[13] - x[6]) if x[13] > x[6] else None, in_lds=int(x[23]),
+                                           combsort=[int(x[16]), int(x[17])], partitions=[int(x[18]), int(x[19])],
+                                           sort_parts=int(x[20] - x[5]) if x[20] else None, n_small=int(x[21]),
+                                           sort_small=int(x[22] - x[20]) if x[22] else None, sort_close=int(x[24] - x[22]) if x[24] else None) for x in d[:16] if x[9]]
     res = b.fetch()
     n_seed = np.array([res.read_sa(i).size for i in range(reads.n)]) if reads.n <= 2_000_000 else None
     n_chain = np.diff(res.chain_off)
