@@ -2087,7 +2087,7 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
         uint32_t* ord = P.ord + S;
         uint32_t* ord2 = P.ord2 + S;
         __shared__ int s_n;
-        uint64_t* dbg = (P.dbg && item < 256) ? P.dbg + item * 32 : nullptr;  // 32 words a read
+        uint64_t* dbg = (P.dbg && item - P.dbg_lo < 256u) ? P.dbg + (item - P.dbg_lo) * 32 : nullptr;  // 32 words a read
         if (dbg && lane == 0) {
             dbg[0] = r;
             dbg[1] = P.occ_off[i1] - S;

@@ -67,6 +67,12 @@ def main():
                                            combsort=[int(x[16]), int(x[17])], partitions=[int(x[18]), int(x[19])],
                                            sort_parts=int(x[20] - x[5]) if x[20] else None, n_small=int(x[21]),
                                            sort_small=int(x[22] - x[20]) if x[22] else None, sort_close=int(x[24] - x[22]) if x[24] else None) for x in d[:16] if x[9]]
+        live = d[d[:, 9] > 0]
+        out["recorded_phase_sums"] = dict(reads=int(len(live)), total=int((live[:, 9] - live[:, 2]).sum()),
+                                          insert=int((live[:, 3] - live[:, 2]).sum()), weights=int((live[:, 5] - live[:, 3]).sum()),
+                                          sort=int((live[:, 6] - live[:, 5]).sum()), drop=int((live[:, 7] - live[:, 6]).sum()),
+                                          tail=int((live[:, 9] - live[:, 7]).sum()), chains=int(live[:, 4].sum()),
+                                          seeds=int(live[:, 1].sum()))
     res = b.fetch()
     n_seed = np.array([res.read_sa(i).size for i in range(reads.n)]) if reads.n <= 2_000_000 else None
     n_chain = np.diff(res.chain_off)
