@@ -1404,8 +1404,9 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     int phase = me < OWN ? P_FETCH : P_EXIT;  // lanes >= OWN only execute extends
     int item = -1, len = 0;
     // next read: -2 nothing claimed, -5 claim in flight, -1 claimed, -3 its offsets to be fetched, -4 in
-    // flight, >= 0 loaded.  Claimed as soon as the current read starts.  The claim's atomic and the
-    // offsets' LDS-DMA are waited for by the uniform section's vmcnt(0), never on their own: a wave
+    // flight, >= 0 loaded.  Claimed when the current read ends (OPT 1; claimed when it starts, a read
+    // held in reserve behind a busy owner lengthened the launch's tail).  The claim's atomic (OPT 8)
+    // and the offsets' LDS-DMA are waited for by the iteration's vmcnt(0), never on their own: a wave
     // stalled a memory round trip per read for each before (the compiler's atomicAdd waits for the
     // result to broadcast it)
     int nitem = 0, nlen = -2;
