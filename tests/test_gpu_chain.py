@@ -159,10 +159,12 @@ def test_chain_strand_bridging_and_empty(gpu_device):
                                  dict(SMEM_CHAIN_STREAMS="1", SMEM_CHAIN_HEAVY_MIN="0"),
                                  dict(SMEM_CHAIN_LDS_REST="2048", SMEM_CHAIN_HEAVY_MIN="0"),
                                  dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_WAVE_MIN="2"),
-                                 dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_WAVE_MIN="256", SMEM_CHAIN_REPLAY_CACHE="1")],
+                                 dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_WAVE_MIN="256", SMEM_CHAIN_REPLAY_CACHE="1"),
+                                 dict(SMEM_CHAIN_HEAVY_MIN="0", SMEM_CHAIN_SORT_COUNT="0")],
                          ids=["all-wave", "all-lane", "lds-overflow", "tree-only", "tree-only-all-wave",
                               "serial-sort", "wave-cut-sort", "wave-cut-sort-hbm", "drop-pruned", "drop-hbm",
-                              "one-launch", "rest-tier-hbm", "cluster-wave-all", "cluster-wave-256-cache"])
+                              "one-launch", "rest-tier-hbm", "cluster-wave-all", "cluster-wave-256-cache",
+                              "bitonic-close"])
 def test_chain_paths_agree(gpu_device, monkeypatch, env):
     """The lane-per-read path, the wave-per-read paths (position clusters,
     and the chain tree they fall back to on equal chain keys), the wave
@@ -244,8 +246,9 @@ def test_chain_equal_keys_replay(gpu_device, monkeypatch, env):
 
 
 @pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_STREAMS="1"), dict(SMEM_CHAIN_GIANT_MIN="256"),
-                                 dict(SMEM_CHAIN_REPLAY_CACHE="1"), dict(SMEM_CHAIN_WAVE_MIN="256")],
-                         ids=["tiers", "one-launch", "more-giants", "record-cache", "cluster-wave-256"])
+                                 dict(SMEM_CHAIN_REPLAY_CACHE="1"), dict(SMEM_CHAIN_WAVE_MIN="256"),
+                                 dict(SMEM_CHAIN_SORT_COUNT="0")],
+                         ids=["tiers", "one-launch", "more-giants", "record-cache", "cluster-wave-256", "bitonic-close"])
 def test_chain_human_like_giants(gpu_device, monkeypatch, env):
     """A 4 Mbp genome with the human-like repeat profile and 8 % satellite /
     simple-sequence arrays: reads from the arrays carry thousands of seed
