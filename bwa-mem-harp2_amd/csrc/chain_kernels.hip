@@ -1662,7 +1662,8 @@ static_assert(sizeof(CRec) == 32, "CRec is 32 B");
 
 template <class N>
 __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane, unsigned char* lds,
-                           uint32_t lds_bytes, bool pool_in_lds) {
+                           uint32_t lds_bytes, bool pool_in_lds, uint64_t* dbg = nullptr) {
+    uint64_t t_search = 0, t_merge = 0, t_insert = 0, n_search = 0, n_insert = 0;  // SMEM_CHAIN_DBG
     const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
     const SeedRec* seed = P.seed + S;
     ChainRec* chn = P.chn + S;
@@ -1702,7 +1703,14 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
             int lw = -1;
             int64_t lpos = 0;
             LeafHand hand{false, 0, 0, 0, 0};
-            if (ct == CODE_REPLAY && n_ch) lw = tree_lower_wave(pool, root, rb, lane, &hand, &lpos);
+            uint64_t c0 = dbg ? __builtin_readcyclecounter() : 0;
+            if (ct == CODE_REPLAY && n_ch) {
+                lw = tree_lower_wave(pool, root, rb, lane, &hand, &lpos);
+                if (dbg) {
+                    const uint64_t c1 = __builtin_readcyclecounter();
+                    t_search += c1 - c0, ++n_search, c0 = c1;
+                }
+            }
             int make = 1;
             if (lw >= 0) {
                 if (lane == 0) {
@@ -1727,6 +1735,10 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
                     make = mg == MERGE_NEW;
                 }
                 make = __builtin_amdgcn_readfirstlane(make);
+                if (dbg) {
+                    const uint64_t c1 = __builtin_readcyclecounter();
+                    t_merge += c1 - c0, c0 = c1;
+                }
             }
             if (make) {
                 if (ct == CODE_REPLAY) {
@@ -1751,9 +1763,11 @@ __device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* poo
                     n_nodes = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_nodes);
                 }
                 ++n_ch;
+                if (dbg) t_insert += __builtin_readcyclecounter() - c0, ++n_insert;
             }
         }
     }
+    if (dbg && lane == 0) dbg[25] = t_search, dbg[26] = t_merge, dbg[27] = t_insert, dbg[28] = n_search, dbg[29] = n_insert;
     return n_ch ? tree_inorder_wave(pool, root, P.ord + S, lane) : 0;
 }
 
@@ -2124,10 +2138,10 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                     __syncthreads();
                     if (n_cand / (BT_T - 1) + 8 <= P.lds_bytes / sizeof(LNode))
                         n = replay_tree(P, S, (uint32_t)(E - S), reinterpret_cast<LNode*>(lds_raw), lane, lds_raw,
-                                        P.lds_bytes, true);
+                                        P.lds_bytes, true, dbg);
                     else
                         n = replay_tree(P, S, (uint32_t)(E - S), P.node + (S / 7 + 3ull * (uint64_t)r), lane,
-                                        lds_raw, P.lds_bytes, false);
+                                        lds_raw, P.lds_bytes, false, dbg);
                 }
                 if (lane == 0) {
                     s_n = n;

@@ -66,7 +66,9 @@ def main():
                                            n_cand=int(x[12]), drop_kept=int(x[13] - x[6]) if x[13] > x[6] else None, in_lds=int(x[23]),
                                            combsort=[int(x[16]), int(x[17])], partitions=[int(x[18]), int(x[19])],
                                            sort_parts=int(x[20] - x[5]) if x[20] else None, n_small=int(x[21]),
-                                           sort_small=int(x[22] - x[20]) if x[22] else None, sort_close=int(x[24] - x[22]) if x[24] else None) for x in d[:16] if x[9]]
+                                           sort_small=int(x[22] - x[20]) if x[22] else None, sort_close=int(x[24] - x[22]) if x[24] else None,
+                                           replay_split=dict(search=int(x[25]), merge=int(x[26]), insert=int(x[27]),
+                                                             n_search=int(x[28]), n_insert=int(x[29])) if x[10] else None) for x in d[:16] if x[9]]
         live = d[d[:, 9] > 0]
         out["recorded_phase_sums"] = dict(reads=int(len(live)), total=int((live[:, 9] - live[:, 2]).sum()),
                                           insert=int((live[:, 3] - live[:, 2]).sum()), weights=int((live[:, 5] - live[:, 3]).sum()),
