@@ -1225,7 +1225,7 @@ __device__ __forceinline__ int mark_pred(const uint32_t* bm, const uint32_t* sm,
 // tandem-repeat cluster (several seeds per chain) advances a few seeds per
 // batch, a satellite cluster (a chain per seed) 64.  Returns true when the
 // cluster made an equal chain key (its later seeds are CODE_REPLAY).
-__device__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, uint32_t* bm, uint32_t* sm, uint32_t cs,
+__device__ __forceinline__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, uint32_t* bm, uint32_t* sm, uint32_t cs,
                              uint32_t ce, ChainRec* chn, const SeedRec* seed, uint32_t* code, int lane,
                              uint32_t& n_mine) {
     uint32_t pb = cs;
@@ -1325,7 +1325,7 @@ __device__ bool cluster_wave(const ChainParams& P, uint64_t S, uint64_t* key, ui
 // replay does with it: CODE_NEW (this seed starts a chain: kb_putp it),
 // CODE_REPLAY (a seed of a cluster past its first equal key), or CODE_SKIP;
 // n_cand counts the first two.
-__device__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t E, uint64_t* key, int lane,
+__device__ __forceinline__ bool insert_read_clusters(const ChainParams& P, uint64_t S, uint64_t E, uint64_t* key, int lane,
                                      int& n_out, uint32_t& n_cand) {
     const uint32_t N = (uint32_t)(E - S);
     uint32_t npad = 2;
@@ -1590,7 +1590,7 @@ __device__ __forceinline__ void leaf_insert_hand(N* pool, const LeafHand& h, uin
 // lane-serial walk of a several-thousand-chain tree waited on a scratch
 // round trip per step, most of the kbtree replay's time.
 template <class N>
-__device__ int tree_inorder_wave(const N* pool, uint32_t root, uint32_t* out, int lane) {
+__device__ __forceinline__ int tree_inorder_wave(const N* pool, uint32_t root, uint32_t* out, int lane) {
     int sxv = lane == 0 ? (int)root : 0, siv = 0;
     int top = 0, n_out = 0;
     while (top >= 0) {
@@ -1661,7 +1661,7 @@ struct CRec {
 static_assert(sizeof(CRec) == 32, "CRec is 32 B");
 
 template <class N>
-__device__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane, unsigned char* lds,
+__device__ __forceinline__ int replay_tree(const ChainParams& P, uint64_t S, uint32_t ns, N* pool, int lane, unsigned char* lds,
                            uint32_t lds_bytes, bool pool_in_lds, uint64_t* dbg = nullptr) {
     uint64_t t_search = 0, t_merge = 0, t_insert = 0, n_search = 0, n_insert = 0;  // SMEM_CHAIN_DBG
     const uint32_t* code = reinterpret_cast<const uint32_t*>(P.flt + S);
