@@ -130,7 +130,8 @@ def parse(argv=None):
                    help="reads of the end-to-end leg (bwa-gpu mem vs the reference pipeline; 0: skip; N=1 only)")
     p.add_argument("--e2e-pairs", type=int, default=250_000,
                    help="e2e: also this many interleaved pairs through bwa-gpu mem -p vs the reference (0: skip)")
-    p.add_argument("--e2e-batch", type=int, default=0, help="-b of bwa-gpu mem (0: reads / threads)")
+    p.add_argument("--e2e-batch", type=int, default=0,
+                   help="-b of bwa-gpu mem (0: none -- the binding's own per-device batch plan, the product default)")
     p.add_argument("--e2e-chunk-reads", type=int, default=3_200_000,
                    help="e2e.multi_chunk: this many SE reads (several bwa mem chunks of 10 Mbp x threads; 0: off)")
     p.add_argument("--other-profile", "--human-like", dest="other_profile", type=int, default=1,
@@ -694,8 +695,9 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
         log(f"bwa .pac/.ann/.amb written in {time.time() - t:.1f} s")
     m = min(args.e2e_reads, reads.n)
     sub = reads.subset(np.arange(m))
-    batch = args.e2e_batch or max(1024, -(-m // threads))
-    out = {"reads": m, "read_len": args.read_len, "threads": threads, "batch": batch,
+    batch = args.e2e_batch or None  # None: no -b, the binding's batch plan (mem_gpu_auto_batch)
+    bflag = ["-b", str(batch)] if batch else []
+    out = {"reads": m, "read_len": args.read_len, "threads": threads, "batch": batch or "auto (per-device plan)",
            "what": "bwa-gpu mem (the reference's bwa mem with integration/patches, libsmemgpu.so: seeding -> "
                    "bwt_sa -> mem_chain + mem_chain_flt -> mem_chain2aln on the GPU, the regions copied back, "
                    "mem_sort_and_dedup / mem_mark_primary_se / mem_reg2sam_se on the CPU) vs the unpatched "
@@ -705,8 +707,8 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
         fq = os.path.join(d, "r.fq")
         synth.write_fastq(fq, sub)
         env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu), SMEM_GPU_TIMES="1")
-        legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq], {}),
-                ("gpu_chains_only", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq],
+        legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), *bflag, base, fq], {}),
+                ("gpu_chains_only", [BWA_GPU, "mem", "-t", str(threads), *bflag, base, fq],
                  {"SMEM_GPU_STAGES": "1"}),
                 ("reference", [REF_HARNESS, "mem", base, fq, str(threads), "1", "0"], {})]
         runs = _e2e_legs(d, legs, env_base, m)
@@ -724,14 +726,16 @@ def e2e_report(args, base: str, genome_codes, reads, threads: int, gpu: int) -> 
             fq2 = os.path.join(d, "p.fq")
             synth.write_fastq(fq2, pe, prefix="p", pairs=True)
             log(f"e2e pe: {args.e2e_pairs} pairs made in {time.time() - t:.1f} s")
-            pbatch = args.e2e_batch or max(1024, 2 * -(-args.e2e_pairs // threads))
-            legs = [("gpu", [BWA_GPU, "mem", "-p", "-t", str(threads), "-b", str(pbatch), base, fq2], {}),
+            pbatch = args.e2e_batch or None
+            legs = [("gpu", [BWA_GPU, "mem", "-p", "-t", str(threads), *(["-b", str(pbatch)] if pbatch else []),
+                             base, fq2], {}),
                     ("reference", [REF_HARNESS, "mem", base, fq2, str(threads), "1", "1"], {})]
             pr = _e2e_legs(d, legs, env_base, 2 * args.e2e_pairs, tag="pe ")
             if pr is None:
                 out["pe"] = {"error": "a leg failed (see the bench log)"}
             else:
-                out["pe"] = {"pairs": args.e2e_pairs, "reads": 2 * args.e2e_pairs, "batch": pbatch,
+                out["pe"] = {"pairs": args.e2e_pairs, "reads": 2 * args.e2e_pairs,
+                             "batch": pbatch or "auto (per-device plan)",
                              "insert": "N(500, 50)", **pr,
                              "sam_identical": pr["gpu"]["sam_sha256"] == pr["reference"]["sam_sha256"],
                              **_e2e_speedups(pr)}
@@ -745,15 +749,15 @@ def e2e_chunks_report(args, base: str, reads, threads: int, gpu: int) -> dict:
     processed), against the reference's sequential loop on the same reads."""
     from smemgpu import synth
     m = reads.n
-    batch = args.e2e_batch or 62500
-    out = {"reads": m, "read_len": args.read_len, "threads": threads, "batch": batch,
+    batch = args.e2e_batch or None
+    out = {"reads": m, "read_len": args.read_len, "threads": threads, "batch": batch or "auto (per-device plan)",
            "what": "bwa-gpu mem vs the unpatched reference pipeline over several chunks of 10 Mbp x threads: "
                    "wall clock, and the reference's mem_process_seqs real time summed over the chunks"}
     with tempfile.TemporaryDirectory(dir=args.cache) as d:
         fq = os.path.join(d, "c.fq")
         synth.write_fastq(fq, reads, prefix="c")
         env_base = dict(os.environ, SMEM_GPU_DEVICES=str(gpu), SMEM_GPU_TIMES="1")
-        legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), "-b", str(batch), base, fq], {}),
+        legs = [("gpu", [BWA_GPU, "mem", "-t", str(threads), *(["-b", str(batch)] if batch else []), base, fq], {}),
                 ("reference", [REF_HARNESS, "mem", base, fq, str(threads), "1", "0"], {})]
         runs = _e2e_legs(d, legs, env_base, m, tag="chunks ")
         if runs is None:
