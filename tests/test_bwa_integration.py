@@ -173,9 +173,10 @@ def test_gpu_sam_identical_eight_contexts(indexed, gpu_device, g, kind, batch):
     eight device contexts (index, .sa, .pac and worker slots each), `-t 16`
     deals worker tid to context tid % 8 / slot tid / 8 (software/fastmap.c:
     204-210's per-worker buffers, one manager per device).  Without -b the
-    batch plan gives each context one batch of its share of the chunk (a
-    share under two seeding grids is not split further): 8 batches, 8
-    workers.  SAM byte-identical to the reference's."""
+    batch plan deals each context its share of the chunk in batches whose
+    admitted ones hold a seeding grid together -- a share under one grid
+    (these small inputs) is one batch: 8 batches, 8 workers.  SAM
+    byte-identical to the reference's."""
     got, err = _run(indexed[g], g, kind, 16, batch,
                     env={"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_TIMES": "1"})
     assert "seeding on the CPU" not in err and "refused" not in err, err[-2000:]
