@@ -797,6 +797,12 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
                       "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
                       "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
                       "cpu_fallback": "seeding on the CPU" in err or "refused" in err}
+        # the binding's start-up / teardown lines (SMEM_GPU_TIMES=1): where the
+        # time outside mem_process_seqs goes
+        tl = [ln for ln in err.splitlines()
+              if ln.startswith(("[M::main_mem]", "[M::smem_gpu_", "[M::mem_gpu_")) and "reads through" not in ln]
+        if tl:
+            runs[name]["startup_lines"] = tl[:24]
         ch = _mem_chunks(err)
         if len(ch) > 1:
             runs[name]["mem_process_seqs_chunks"] = [[c, round(t, 3)] for c, t in ch]
