@@ -800,9 +800,10 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
         # the binding's start-up / teardown lines (SMEM_GPU_TIMES=1): where the
         # time outside mem_process_seqs goes
         tl = [ln for ln in err.splitlines()
-              if ln.startswith(("[M::main_mem]", "[M::smem_gpu_", "[M::mem_gpu_")) and "reads through" not in ln]
+              if ln.startswith(("[M::main_mem]", "[M::smem_gpu_", "[M::mem_gpu_")) and "reads through" not in ln
+              and "smem_gpu_reserve_slots] device" not in ln and "smem_gpu_collect" not in ln]
         if tl:
-            runs[name]["startup_lines"] = tl[:24]
+            runs[name]["startup_lines"] = tl[:32]
         ch = _mem_chunks(err)
         if len(ch) > 1:
             runs[name]["mem_process_seqs_chunks"] = [[c, round(t, 3)] for c, t in ch]
