@@ -1787,38 +1787,83 @@ __device__ __forceinline__ int replay_tree(const ChainParams& P, uint64_t S, uin
 // (weight, position) keys and a permute.
 // ---------------------------------------------------------------------------
 
+// The sort runs on 32-bit keys w << 16 | p (p: the record's position before
+// the sort, w < 2^16), not on the 20-byte records: a swap moves one word, the
+// keys sit in LDS even when the records are in HBM (the giants), and the
+// records move once, in the closing sort's permute.  Only weights are
+// compared -- x.w > y.w iff Kx > (Ky | 0xFFFF) -- so every key goes where
+// ks_introsort moves its record.
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
+
+template <typename KP>
+__device__ __forceinline__ void key_swap(KP k, uint32_t i, uint32_t j) {
+    const uint32_t x = k[i];
+    k[i] = k[j];
+    k[j] = x;
+}
+
+// flt_combsort on keys (ks_combsort, software/ksort.h:153-174)
+template <typename KP>
+__device__ __forceinline__ void key_combsort(KP k, uint32_t n) {
+    const double shrink = 1.2473309501039786540366528676643;
+    uint32_t gap = n;
+    bool swapped;
+    do {
+        if (gap > 2) {
+            gap = (uint32_t)((double)gap / shrink);
+            if (gap == 9 || gap == 10) gap = 11;
+        }
+        swapped = false;
+        for (uint32_t i = 0; i + gap < n; ++i)
+            if (k[i + gap] > (k[i] | 0xFFFFu)) {
+                key_swap(k, i, i + gap);
+                swapped = true;
+            }
+    } while (swapped || gap > 2);
+    if (gap != 1)
+        for (uint32_t i = 1; i < n; ++i)
+            for (uint32_t j = i; j > 0 && k[j] > (k[j - 1] | 0xFFFFu); --j) key_swap(k, j, j - 1);
+}
+
 // the serial loop from segment [s, t] (t < 2^16: flt_sort_wave takes n <
 // 2^16) with depth budget d, without the closing insertion sort; at most
 // log2(2^16 / 16) + 1 = 13 segments are pending (see flt_sort), kept as
-// s | t << 16 and d in 16-entry arrays small enough for registers
-__device__ void flt_sort_seg_serial(FltRec* a, uint32_t s, uint32_t t, int d) {
+// s | t << 16 and d in 16-entry arrays small enough for registers.  KP is
+// uint32_t* or, for keys in LDS, an LDS-qualified pointer: the scans' loads
+// and the swaps are then ds_ operations, not flat ones that wait on both
+// counters.
+template <typename KP>
+__device__ void key_sort_seg_serial(KP k, uint32_t s, uint32_t t, int d) {
     uint32_t sst[16];
     uint8_t sdd[16];
     int top = 0;
     for (;;) {
         if (s < t) {
             if (--d == 0) {
-                flt_combsort(a + s, t - s + 1);
+                key_combsort(k + s, t - s + 1);
                 t = s;
                 continue;
             }
-            uint32_t i = s, j = t, k = i + ((j - i) >> 1) + 1;
-            if (flt_lt(a[k], a[i])) {
-                if (flt_lt(a[k], a[j])) k = j;
-            } else {
-                k = flt_lt(a[j], a[i]) ? i : j;
+            uint32_t i = s, j = t, m = i + ((j - i) >> 1) + 1;
+            {
+                const uint32_t wi = k[i] >> 16, wj = k[j] >> 16, wm = k[m] >> 16;
+                if (wm > wi) {
+                    if (wm > wj) m = j;
+                } else {
+                    m = wj > wi ? i : j;
+                }
             }
-            const FltRec rp = a[k];
-            if (k != t) flt_swap(a, k, t);
+            const uint32_t rp = k[m], hi = rp | 0xFFFFu, lo = rp & 0xFFFF0000u;
+            if (m != t) key_swap(k, m, t);
             for (;;) {
                 do ++i;
-                while (flt_lt(a[i], rp));
+                while (k[i] > hi);  // a[i].w > pivot
                 do --j;
-                while (i <= j && flt_lt(rp, a[j]));
+                while (i <= j && k[j] < lo);  // pivot > a[j].w
                 if (j <= i) break;
-                flt_swap(a, i, j);
+                key_swap(k, i, j);
             }
-            flt_swap(a, i, t);
+            key_swap(k, i, t);
             if (i - s > t - i) {
                 if (i - s > 16) {
                     sst[top] = s | (i - 1) << 16;
@@ -1849,33 +1894,33 @@ __device__ __forceinline__ void wave_sync_mem() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// one partition of a[s..t] (s < t) as ks_introsort makes it; returns the
+// one partition of keys ky[s..t] (s < t) as ks_introsort makes it; returns the
 // pivot's final position.  tl / tr: the stopper positions by rank
-__device__ uint32_t flt_partition_wave(FltRec* a, uint32_t s, uint32_t t, uint32_t* tl, uint32_t* tr, int lane) {
+__device__ uint32_t key_partition_wave(uint32_t* ky, uint32_t s, uint32_t t, uint32_t* tl, uint32_t* tr, int lane) {
     uint32_t k = s + ((t - s) >> 1) + 1;
     {
-        const int wi = a[s].w, wj = a[t].w, wk = a[k].w;  // flt_lt(x, y) = x.w > y.w
+        const uint32_t wi = ky[s] >> 16, wj = ky[t] >> 16, wk = ky[k] >> 16;  // flt_lt(x, y) = x.w > y.w
         if (wk > wi) {
             if (wk > wj) k = t;
         } else {
             k = wj > wi ? s : t;
         }
     }
-    const int pw = a[k].w;
+    const uint32_t pw = ky[k] >> 16;
     if (k != t) {
-        if (lane == 0) flt_swap(a, k, t);
+        if (lane == 0) key_swap(ky, k, t);
         wave_sync_mem();
     }
     uint32_t tot_r = 0;
     for (uint32_t b = s; b < t; b += 64) {
         const uint32_t p = b + (uint32_t)lane;
-        tot_r += (uint32_t)__builtin_popcountll(__ballot(p < t && a[p].w >= pw));
+        tot_r += (uint32_t)__builtin_popcountll(__ballot(p < t && ky[p] >> 16 >= pw));
     }
     const uint64_t below = (1ull << lane) - 1;
     uint32_t run_l = 0, run_r = 0, K = 0;
     for (uint32_t b = s; b <= t; b += 64) {
         const uint32_t p = b + (uint32_t)lane;
-        const int w = p <= t ? a[p].w : 0;
+        const uint32_t w = p <= t ? ky[p] >> 16 : 0u;
         const bool is_l = p > s && p <= t && w <= pw;
         const bool is_r = p < t && w >= pw;
         const uint64_t ml = __ballot(is_l), mr = __ballot(is_r);
@@ -1894,9 +1939,9 @@ __device__ uint32_t flt_partition_wave(FltRec* a, uint32_t s, uint32_t t, uint32
         const uint32_t q = q0 + (uint32_t)lane;
         if (q < K) {
             const uint32_t pl = tl[q], pr = tr[q];
-            const FltRec x = a[pl], y = a[pr];
-            a[pl] = y;
-            a[pr] = x;
+            const uint32_t x = ky[pl], y = ky[pr];
+            ky[pl] = y;
+            ky[pr] = x;
         }
     }
     wave_sync_mem();
@@ -1905,7 +1950,7 @@ __device__ uint32_t flt_partition_wave(FltRec* a, uint32_t s, uint32_t t, uint32
         const uint32_t r = tr[K - 1];
         i = r < i ? r : i;
     }
-    if (lane == 0) flt_swap(a, i, t);
+    if (lane == 0) key_swap(ky, i, t);
     wave_sync_mem();
     return i;
 }
@@ -1921,19 +1966,24 @@ __device__ void wave_bitonic32(uint32_t* key, uint32_t npad, int lane) {
 }
 
 // the whole ks_introsort(mem_flt) for n < 2^16 chains of weights in
-// [0, 2^16); small: 3 words per lane-cut segment, stk: 3 words per wave-cut
-// segment (at most 64 pending); keys: npad words; tmp: n records
-// cnt / cnt_cap: LDS words free once the partitions are done (the closing
-// sort's weight counts); wmax: the largest weight
-__device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t* tl, uint32_t* tr, uint32_t* keys,
-                              FltRec* tmp, uint32_t* small, uint32_t* stk, int lane, int wmin, int wmax,
-                              uint32_t* cnt, uint32_t cnt_cap, uint64_t* dbg = nullptr) {
+// [0, 2^16); K: 3 n words (the keys, then two n-word stopper lists, whose
+// room the bitonic sort's npad < 2 n keys reuse), k_lds: K is in LDS;
+// small: 3 words per lane-cut segment, stk: 3 words per wave-cut segment (at
+// most 64 pending); tmp: n records; cnt / cnt_cap: LDS words free once the
+// partitions are done, apart from the keys (the closing sort's weight
+// counts); wmax: the largest weight
+__device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t* K, bool k_lds, FltRec* tmp,
+                              uint32_t* small, uint32_t* stk, int lane, int wmin, int wmax, uint32_t* cnt,
+                              uint32_t cnt_cap, uint64_t* dbg = nullptr) {
     if (n < 2) return;
     if (n == 2) {
         if (lane == 0 && flt_lt(a[1], a[0])) flt_swap(a, 0, 1);
         wave_sync_mem();
         return;
     }
+    uint32_t* tl = K + n;
+    uint32_t* tr = K + 2 * n;
+    for (uint32_t p = lane; p < n; p += 64) K[p] = (uint32_t)a[p].w << 16 | p;
     int d = 2;
     while ((1ull << d) < n) ++d;
     d <<= 1;
@@ -1956,10 +2006,10 @@ __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t
         int dd = (int)stk[3 * top + 2];
         wave_sync_mem();
         if (--dd == 0) {
-            if (lane == 0) flt_combsort(a + s, t - s + 1);
+            if (lane == 0) key_combsort(K + s, t - s + 1);
             if (dbg && lane == 0) dbg[16] += 1, dbg[17] += t - s + 1;
         } else {
-            const uint32_t i = flt_partition_wave(a, s, t, tl, tr, lane);
+            const uint32_t i = key_partition_wave(K, s, t, tl, tr, lane);
             if (dbg && lane == 0) dbg[18] += 1, dbg[19] += t - s + 1;
             if (i - s > 16) add(s, i - 1, dd);
             if (t - i > 16) add(i + 1, t, dd);
@@ -1967,8 +2017,14 @@ __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t
         wave_sync_mem();
     }
     if (dbg && lane == 0) dbg[20] = __builtin_readcyclecounter(), dbg[21] = n_small;
-    for (uint32_t q = lane; q < n_small; q += 64)
-        flt_sort_seg_serial(a, small[3 * q], small[3 * q + 1], (int)small[3 * q + 2]);
+    if (k_lds) {
+        LdsU32* kl = (LdsU32*)K;
+        for (uint32_t q = lane; q < n_small; q += 64)
+            key_sort_seg_serial(kl, small[3 * q], small[3 * q + 1], (int)small[3 * q + 2]);
+    } else {
+        for (uint32_t q = lane; q < n_small; q += 64)
+            key_sort_seg_serial(K, small[3 * q], small[3 * q + 1], (int)small[3 * q + 2]);
+    }
     wave_sync_mem();
     if (dbg && lane == 0) dbg[22] = __builtin_readcyclecounter();
     // the closing insertion sort: a stable sort by weight, descending
@@ -1982,7 +2038,7 @@ __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t
         // 5,000-chain read)
         for (uint32_t q = lane; q < R; q += 64) cnt[q] = 0;
         wave_sync_mem();
-        for (uint32_t p = lane; p < n; p += 64) atomicAdd(&cnt[(uint32_t)(wmax - a[p].w)], 1u);
+        for (uint32_t p = lane; p < n; p += 64) atomicAdd(&cnt[(uint32_t)wmax - (K[p] >> 16)], 1u);
         wave_sync_mem();
         uint32_t run = 0;
         for (uint32_t q0 = 0; q0 < R; q0 += 64) {
@@ -2000,8 +2056,9 @@ __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t
             FltRec r{};
             uint32_t d = 0xFFFFFFFFu;
             if (valid) {
-                r = a[p];
-                d = (uint32_t)(wmax - r.w);
+                const uint32_t kp = K[p];
+                r = a[kp & 0xFFFFu];
+                d = (uint32_t)wmax - (kp >> 16);
             }
             uint64_t rem = __ballot(valid);
             uint32_t pos = 0;
@@ -2022,11 +2079,12 @@ __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t
     } else {
         uint32_t npad = 2;
         while (npad < n) npad <<= 1;
+        uint32_t* keys = tl;
         for (uint32_t p = lane; p < npad; p += 64)
-            keys[p] = p < n ? ((uint32_t)(0xFFFF - a[p].w) << 16) | p : 0xFFFFFFFFu;
+            keys[p] = p < n ? ((0xFFFFu - (K[p] >> 16)) << 16) | p : 0xFFFFFFFFu;
         wave_sync_mem();
         wave_bitonic32(keys, npad, lane);
-        for (uint32_t r = lane; r < n; r += 64) tmp[r] = a[keys[r] & 0xFFFFu];
+        for (uint32_t r = lane; r < n; r += 64) tmp[r] = a[K[keys[r] & 0xFFFFu] & 0xFFFFu];
         wave_sync_mem();
     }
     if (dbg && lane == 0) dbg[24] = __builtin_readcyclecounter();
@@ -2272,24 +2330,25 @@ __global__ __launch_bounds__(64) void chain_heavy_kernel(ChainParams P) {
                 wmax = a1 > wmax ? a1 : wmax;
             }
             if (P.wave_sort && n < 0x10000 && wmin >= 0 && wmax < 0x10000) {
-                // scratch: stopper lists and keys in LDS after the records
-                // while they fit, else (and the permute's copy always) in the
-                // read's kbtree node pool, free once the chains are listed
-                uint32_t npad = 2;
-                while (npad < (uint32_t)n) npad <<= 1;
-                const uint64_t need = (uint64_t)n * 8 + (uint64_t)npad * 4;
+                // scratch: the keys and stopper lists (3 n words) in LDS,
+                // after the records when they are there, while they fit, else
+                // (and the permute's copy always) in the read's kbtree node
+                // pool, free once the chains are listed (>= 36 n bytes, see
+                // below: the copy takes 20 n, the keys 12 n)
+                const uint64_t need = (uint64_t)n * 12;
                 uint8_t* gs = reinterpret_cast<uint8_t*>(P.node + (S / 7 + 3ull * (uint64_t)r));
-                uint32_t* tl;
-                if (in_lds && (uint64_t)n * sizeof(FltRec) + need <= P.lds_bytes) tl = reinterpret_cast<uint32_t*>(la + n);
-                else if (!in_lds && need <= P.lds_bytes) tl = reinterpret_cast<uint32_t*>(lds_raw);
-                else tl = reinterpret_cast<uint32_t*>(gs + (uint64_t)n * sizeof(FltRec));
-                // the closing sort's counts: the LDS after the records (the
-                // stopper lists there are dead by then), or all of it
-                uint32_t* cnt = in_lds ? reinterpret_cast<uint32_t*>(la + n) : reinterpret_cast<uint32_t*>(lds_raw);
-                const uint64_t cnt_room = ((uint64_t)P.lds_bytes - (in_lds ? (uint64_t)n * sizeof(FltRec) : 0)) / 4;
+                const uint64_t k_off = in_lds ? (uint64_t)n * sizeof(FltRec) : 0;
+                const bool k_lds = k_off + need <= P.lds_bytes;
+                uint32_t* K = k_lds ? reinterpret_cast<uint32_t*>(lds_raw + k_off)
+                                    : reinterpret_cast<uint32_t*>(gs + (uint64_t)n * sizeof(FltRec));
+                // the closing sort's counts: the LDS after the records and
+                // the keys (the stopper lists there are dead by then)
+                const uint64_t c_off = k_off + (k_lds ? (uint64_t)n * 4 : 0);
+                uint32_t* cnt = reinterpret_cast<uint32_t*>(lds_raw + c_off);
+                const uint64_t cnt_room = ((uint64_t)P.lds_bytes - c_off) / 4;
                 const uint32_t cnt_cap = P.sort_count ? (uint32_t)(cnt_room < 65536 ? cnt_room : 65536) : 0u;
-                flt_sort_wave(in_lds ? la : ga, (uint32_t)n, P.sort_lane_max, tl, tl + n, tl + 2 * n,
-                              reinterpret_cast<FltRec*>(gs), ord2, s_stk, lane, wmin, wmax, cnt, cnt_cap, dbg);
+                flt_sort_wave(in_lds ? la : ga, (uint32_t)n, P.sort_lane_max, K, k_lds, reinterpret_cast<FltRec*>(gs),
+                              ord2, s_stk, lane, wmin, wmax, cnt, cnt_cap, dbg);
             } else if (lane == 0) {
                 if (in_lds) flt_sort(la, (uint32_t)n, s_stk);
                 else flt_sort(ga, (uint32_t)n, s_stk);
