@@ -94,11 +94,13 @@ struct ChainParams {
     int tier;                  // chain_heavy_kernel's items: 0 giants, 1 the rest, -1 both (one launch)
     uint32_t lds_rest;         // dynamic LDS of the tier-1 launch
     int drop_blocked;          // heavy path: drop loop's kept list first, then p2 in blocks (0: flt_drop_pruned)
-    int replay_cache;
-    int sort_count;
-    uint32_t dbg_lo;  // SMEM_CHAIN_DBG: the first heavy item recorded (SMEM_CHAIN_DBG_LO)  // mem_chain_flt's closing stable sort by weight counts (else a bitonic sort of keys)          // heavy path: the kbtree replay's LDS chain-record cache (0: records from HBM only)
+    int replay_cache;          // heavy path: the kbtree replay's LDS chain-record cache (0: records from HBM only)
+    int sort_count;            // mem_chain_flt's closing stable sort by weight counts (else a bitonic sort of keys)
+    int giant_order;           // giants in listing order (0), longest first (1) or shortest first (2)
+    uint32_t giant_waves;      // the giant tier's waves (0: one per CU)
+    uint32_t dbg_lo;           // SMEM_CHAIN_DBG: the first heavy item recorded (SMEM_CHAIN_DBG_LO)
     uint32_t wave_min;         // heavy path: clusters of more seeds are passed by the whole wave (cluster_wave)
-    uint64_t* dbg;             // optional phase clocks of the heavy path (16 words per item)
+    uint64_t* dbg;             // optional phase clocks of the heavy path (32 words per item)
     // output (write kernel)
     const uint64_t* chain_off; // [n_reads + 1]
     const uint64_t* seed_off;  // [n_reads + 1]

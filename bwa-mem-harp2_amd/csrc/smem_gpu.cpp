@@ -1489,6 +1489,8 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     P.replay_cache = getenv("SMEM_CHAIN_REPLAY_CACHE") && atoi(getenv("SMEM_CHAIN_REPLAY_CACHE")) == 1 ? 1 : 0;
     P.wave_min = 0xFFFFFFFFu;  // SMEM_CHAIN_WAVE_MIN: clusters of more seeds by the whole wave
     P.sort_count = getenv("SMEM_CHAIN_SORT_COUNT") && atoi(getenv("SMEM_CHAIN_SORT_COUNT")) == 0 ? 0 : 1;
+    P.giant_order = getenv("SMEM_CHAIN_GIANT_ORDER") ? std::min(2, std::max(0, atoi(getenv("SMEM_CHAIN_GIANT_ORDER")))) : 0;
+    P.giant_waves = getenv("SMEM_CHAIN_GIANT_WAVES") ? (uint32_t)std::max(1, atoi(getenv("SMEM_CHAIN_GIANT_WAVES"))) : 0u;
     P.dbg_lo = getenv("SMEM_CHAIN_DBG_LO") ? (uint32_t)strtoul(getenv("SMEM_CHAIN_DBG_LO"), nullptr, 10) : 0u;
     if (const char* v = getenv("SMEM_CHAIN_WAVE_MIN")) P.wave_min = (uint32_t)strtoul(v, nullptr, 10);
     if (const char* v = getenv("SMEM_CHAIN_SORT_LANE_MAX")) P.sort_lane_max = (uint32_t)std::max(17, atoi(v));

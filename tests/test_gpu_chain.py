@@ -247,15 +247,19 @@ def test_chain_equal_keys_replay(gpu_device, monkeypatch, env):
 
 @pytest.mark.parametrize("env", [dict(), dict(SMEM_CHAIN_STREAMS="1"), dict(SMEM_CHAIN_GIANT_MIN="256"),
                                  dict(SMEM_CHAIN_REPLAY_CACHE="1"), dict(SMEM_CHAIN_WAVE_MIN="256"),
-                                 dict(SMEM_CHAIN_SORT_COUNT="0")],
-                         ids=["tiers", "one-launch", "more-giants", "record-cache", "cluster-wave-256", "bitonic-close"])
+                                 dict(SMEM_CHAIN_SORT_COUNT="0"), dict(SMEM_CHAIN_GIANT_ORDER="1"),
+                                 dict(SMEM_CHAIN_STREAMS="1", SMEM_CHAIN_GIANT_MIN="256", SMEM_CHAIN_GIANT_ORDER="1"),
+                                 dict(SMEM_CHAIN_GIANT_ORDER="2", SMEM_CHAIN_GIANT_WAVES="3")],
+                         ids=["tiers", "one-launch", "more-giants", "record-cache", "cluster-wave-256", "bitonic-close",
+                              "longest-first", "one-launch-longest-first", "shortest-first-3-waves"])
 def test_chain_human_like_giants(gpu_device, monkeypatch, env):
     """A 4 Mbp genome with the human-like repeat profile and 8 % satellite /
     simple-sequence arrays: reads from the arrays carry thousands of seed
     occurrences (the giant LDS tier, > 2048), thousands of chains per read
     (rank-bitmap clusters, the kbtree replay, the two-pass drop loop with its
     kept list past the 64 register slots).  Chains == the restatement's, with
-    and without the filter, in both heavy-read launch layouts."""
+    and without the filter, in both heavy-read launch layouts, with the giants
+    in listing order (the default), longest or shortest first, on a few waves."""
     import smemgpu
     from smemgpu import synth
     for k, v in env.items():
