@@ -535,6 +535,7 @@ __device__ __forceinline__ bool flt_can_drop(const FltRec& ai, const FltRec& aj,
 
 __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* U, int n, float mask_level,
                                 float drop_ratio, int msl, int lane, uint64_t* dbg = nullptr) {
+    n = __builtin_amdgcn_readfirstlane(n);  // arguments come in VGPRs: loop bounds uniform
     // I0: the first i >= 1 that a[0] can drop
     const FltRec a0 = a[0];
     int I0 = n;
@@ -582,14 +583,19 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* 
                 if (jj < m0) tile = a[kidx[jj]];
             }
             const int jn = m0 - j0 < 64 ? m0 - j0 : 64;
+            // flt_can_drop and flt_sig as straight-line selects (short-circuit
+            // tests compiled to nested branches on exec)
+            const int32_t li = ai.end - ai.beg;
             for (int jl = 0; srch && jl < jn; ++jl) {
-                const FltRec aj{__builtin_amdgcn_readlane(tile.beg, jl), __builtin_amdgcn_readlane(tile.end, jl),
-                                __builtin_amdgcn_readlane(tile.w, jl), 0, -1};
+                const int32_t bj = __builtin_amdgcn_readlane(tile.beg, jl), ej = __builtin_amdgcn_readlane(tile.end, jl);
+                const int32_t wj = __builtin_amdgcn_readlane(tile.w, jl), lj = ej - bj;
                 const bool on = (srch >> lane) & 1;
-                const bool can = on && flt_can_drop(ai, aj, drop_ratio, msl);
-                const bool hit = can && flt_sig(ai, aj, mask_level);
-                if (hit) jstar = j0 + jl;
-                srch &= ~__ballot(on && (hit || !can));
+                const bool can = on & ((float)ai.w < (float)wj * drop_ratio) & (wj - ai.w >= msl << 1);
+                const int32_t b_max = bj > ai.beg ? bj : ai.beg, e_min = ej < ai.end ? ej : ai.end;
+                const int32_t min_l = li < lj ? li : lj;
+                const bool hit = can & (e_min > b_max) & ((float)(e_min - b_max) >= (float)min_l * mask_level);
+                jstar = hit ? j0 + jl : jstar;
+                srch &= ~__ballot(on & (hit | !can));
             }
         }
         uint64_t und = __ballot(valid && jstar < 0);
@@ -615,6 +621,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* 
     if (dbg && lane == 0) dbg[13] = __builtin_readcyclecounter();  // SMEM_CHAIN_DBG: the kept list's end
     // p2, 64 chains i at a time
     int nu = 0, m_run = 0;
+    uint32_t n_steps = 0, n_memb = 0;  // SMEM_CHAIN_DBG: p2's broadcast steps and U entries visited
     for (int b = 0; b < n; b += 64) {
         const int i = b + lane;
         int32_t bi = 0, ei = 0, ji = 0;
@@ -638,6 +645,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* 
         __builtin_amdgcn_wave_barrier();
         const int nb = n - b < 64 ? n - b : 64;
         int out = 0;
+        n_memb += (uint32_t)nu;
         for (int c = 0; c < nu; c += 64) {
             const int u = c + lane;
             const bool act = u < nu;
@@ -657,13 +665,30 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* 
                     t0 = o2 < t0 ? o2 : t0;
                 }
             }
-            for (int t = t0; t < nb; ++t) {
-                if ((t & 7) == 0 && !__ballot(act && hit < 0)) break;
-                const int32_t bt = __builtin_amdgcn_readlane(bi, t), et = __builtin_amdgcn_readlane(ei, t);
-                const int32_t jt = __builtin_amdgcn_readlane(ji, t);
-                if (act && hit < 0 && (uint32_t)(b + t) > oj && (jt < 0 || (int32_t)kp <= jt) &&
-                    flt_sig(FltRec{bt, et, 0, 0, 0}, rj, mask_level))
-                    hit = b + t;
+            // t0 uniform (readfirstlane): a loop on a VGPR counter compiled
+            // to a divergent loop, every condition a branch on exec (~420
+            // cycles a step on the giants' one wave per CU); now four steps
+            // of straight-line selects at a time (independent tests, one
+            // first-hit pick) -- the same test as flt_sig
+            t0 = __builtin_amdgcn_readfirstlane(t0);
+            const int32_t lj = rj.end - rj.beg;
+            for (int t = t0; t < nb; t += 4) {
+                if (!__ballot(act && hit < 0)) break;
+                n_steps += (uint32_t)(nb - t < 4 ? nb - t : 4);
+                int first = -1;
+#pragma unroll
+                for (int k = 3; k >= 0; --k) {
+                    const int tk = t + k < nb ? t + k : t;  // past the block: a repeat of step t
+                    const int32_t bt = __builtin_amdgcn_readlane(bi, tk), et = __builtin_amdgcn_readlane(ei, tk);
+                    const int32_t jt = __builtin_amdgcn_readlane(ji, tk);
+                    const int32_t jlim = jt < 0 ? INT32_MAX : jt, li = et - bt;
+                    const int32_t b_max = bt > rj.beg ? bt : rj.beg, e_min = et < rj.end ? et : rj.end;
+                    const int32_t min_l = li < lj ? li : lj;
+                    const bool sig = (e_min > b_max) & ((float)(e_min - b_max) >= (float)min_l * mask_level);
+                    const bool h = ((uint32_t)(b + tk) > oj) & ((int32_t)kp <= jlim) & sig;
+                    first = h ? b + tk : first;  // k descending: the lowest hitting step wins
+                }
+                hit = (act & (hit < 0)) ? first : hit;
             }
             if (hit >= 0) a[oj].p2 = hit;
             const bool keep = act && hit < 0;
@@ -677,6 +702,7 @@ __device__ int flt_drop_blocked(FltRec* a, uint32_t* kidx, int32_t* jst, uint4* 
         wave_fence();
         __builtin_amdgcn_wave_barrier();
     }
+    if (dbg && lane == 0) dbg[30] = n_steps, dbg[31] = n_memb;
     // compact the kept records (with their p2) to a[0 .. m): kidx[k] >= k, so
     // a chunk's loads never read a slot an earlier chunk stored, and its own
     // stores wait for its loads (their data); a kept prefix stays in place
@@ -1897,6 +1923,8 @@ __device__ __forceinline__ void wave_sync_mem() {
 // one partition of keys ky[s..t] (s < t) as ks_introsort makes it; returns the
 // pivot's final position.  tl / tr: the stopper positions by rank
 __device__ uint32_t key_partition_wave(uint32_t* ky, uint32_t s, uint32_t t, uint32_t* tl, uint32_t* tr, int lane) {
+    s = __builtin_amdgcn_readfirstlane(s);  // arguments come in VGPRs: loop bounds uniform
+    t = __builtin_amdgcn_readfirstlane(t);
     uint32_t k = s + ((t - s) >> 1) + 1;
     {
         const uint32_t wi = ky[s] >> 16, wj = ky[t] >> 16, wk = ky[k] >> 16;  // flt_lt(x, y) = x.w > y.w
@@ -1956,6 +1984,7 @@ __device__ uint32_t key_partition_wave(uint32_t* ky, uint32_t s, uint32_t t, uin
 }
 
 __device__ void wave_bitonic32(uint32_t* key, uint32_t npad, int lane) {
+    npad = __builtin_amdgcn_readfirstlane(npad);
     for (uint32_t k = 2; k <= npad; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             if (npad >= 64 * 2 * 8) bitonic_stage<8>(key, npad, k, j, lane);
@@ -1975,6 +2004,11 @@ __device__ void wave_bitonic32(uint32_t* key, uint32_t npad, int lane) {
 __device__ void flt_sort_wave(FltRec* a, uint32_t n, uint32_t lane_max, uint32_t* K, bool k_lds, FltRec* tmp,
                               uint32_t* small, uint32_t* stk, int lane, int wmin, int wmax, uint32_t* cnt,
                               uint32_t cnt_cap, uint64_t* dbg = nullptr) {
+    n = __builtin_amdgcn_readfirstlane(n);  // arguments come in VGPRs: loop bounds uniform
+    lane_max = __builtin_amdgcn_readfirstlane(lane_max);
+    wmin = __builtin_amdgcn_readfirstlane(wmin);
+    wmax = __builtin_amdgcn_readfirstlane(wmax);
+    cnt_cap = __builtin_amdgcn_readfirstlane(cnt_cap);
     if (n < 2) return;
     if (n == 2) {
         if (lane == 0 && flt_lt(a[1], a[0])) flt_swap(a, 0, 1);

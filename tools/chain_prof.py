@@ -64,6 +64,7 @@ def main():
                                            weights=int(x[5] - x[3]), sort=int(x[6] - x[5]), drop=int(x[7] - x[6]),
                                            kept=int(x[8]), tail=int(x[9] - x[7]), replay=int(x[10]), cluster_pass=int(x[11] - x[2]) if x[11] else 0,
                                            n_cand=int(x[12]), drop_kept=int(x[13] - x[6]) if x[13] > x[6] else None, in_lds=int(x[23]),
+                                           p2_steps=int(x[30]), p2_members=int(x[31]),
                                            combsort=[int(x[16]), int(x[17])], partitions=[int(x[18]), int(x[19])],
                                            sort_parts=int(x[20] - x[5]) if x[20] else None, n_small=int(x[21]),
                                            sort_small=int(x[22] - x[20]) if x[22] else None, sort_close=int(x[24] - x[22]) if x[24] else None,
