@@ -1480,7 +1480,7 @@ int smem_batch_chain(smem_batch_t* b, int64_t l_pac, const smem_chain_opt_t* opt
     if (const char* v = getenv("SMEM_CHAIN_GIANT_MIN")) P.giant_min = (uint32_t)std::max(0, atoi(v));
     P.cluster = getenv("SMEM_CHAIN_TREE_ONLY") ? 0 : 1;
     P.wave_sort = getenv("SMEM_CHAIN_SERIAL_SORT") ? 0 : 1;
-    P.sort_lane_max = 256;
+    P.sort_lane_max = 128;  // r7h: 128 vs 256, human-like 22.5-22.7 vs 22.5-23.4 ms, uniform 14.2-14.3 vs 14.3-14.5
     P.drop_blocked = getenv("SMEM_CHAIN_DROP_PRUNED") ? 0 : 1;
     // the replay's chain-record cache and the wave-batched big clusters are off by default: both
     // measured slower (filtered, 1M reads: uniform 14.7 -> 16.1-16.2 ms with both, human-like 26.2 ->
