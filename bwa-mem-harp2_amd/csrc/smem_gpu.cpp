@@ -612,8 +612,15 @@ static smem_gpu_t* gpu_handle(int device, uint64_t bwt_size, uint64_t primary, c
     // a variant this build does not have is ignored
     if (const char* v = getenv("SMEM_GPU_SEED_VARIANT")) {
         const int sv = atoi(v);
-        if (sv > 0 && smem_seed_variant_built(sv) && sv != 9 && sv != 23 && sv != 25) g->variant = sv;
+        // (not the variants that need more than the Occ64 index -- 3 / 4 the reference layout,
+        // 10 / 22 the Occ192 one, 23 the k-mer table, 9 / 25 the stamp buffer --: those only
+        // through smem_gpu_set_kernel_variant / their own setup)
+        if (sv > 0 && smem_seed_variant_built(sv) && sv != 3 && sv != 4 && sv != 9 && sv != 10 && sv != 22 &&
+            sv != 23 && sv != 25)
+            g->variant = sv;
     }
+    // the CU count before any async init starts (smem_gpu_grid_reads may read it at once)
+    if (hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) g->n_cu = 0;
     g->bwt_size = bwt_size;
     g->primary = primary;
     std::memcpy(g->L2, L2, sizeof(g->L2));
@@ -629,7 +636,7 @@ static int gpu_open(smem_gpu_t* g, const uint32_t* bwt) {
     HIP_TRY(hipSetDevice(g->device));
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, g->device));
-    g->n_cu = prop.multiProcessorCount;
+    if (g->n_cu <= 0) g->n_cu = prop.multiProcessorCount;  // (set by gpu_handle unless that query failed)
     const uint64_t bwt_size = g->bwt_size;
     // +16 words: a whole 64-B bucket can be loaded at the very end
     hipError_t e = hipMalloc(&g->d_bwt, (bwt_size + 16) * sizeof(uint32_t));
@@ -866,8 +873,11 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     b->cap_calls = (uint32_t)(max_len / 4 + 16);  // ~6 lists per 150 bp read; more -> overflow pass
     b->cap_list = (uint32_t)max_len + 2;   // forward/backward lists hold <= len+1 intervals
     const int want_lanes = g->n_cu * (g->lanes_per_cu > 0 ? g->lanes_per_cu : seed_lanes_per_cu(g->variant));
-    // seed_wp_kernel owns 32 reads per wave: two lanes per read cover a small batch
-    const int read_lanes = (int)std::min<int64_t>((int64_t)2 * max_reads + 255, INT32_MAX) / 256 * 256;
+    // seed_wp_kernel owns 24 reads per wave (variant 49): seed_lanes_per_read lanes per read
+    // give every read of a small batch an owner; batch_run_impl bounds each launch by b->lanes,
+    // the lanes the scratch below was sized for, whatever variant is set later
+    const int read_lanes =
+        (int)std::min<int64_t>((int64_t)seed_lanes_per_read(g->variant) * max_reads + 255, INT32_MAX) / 256 * 256;
     b->lanes = std::max(256, std::min(want_lanes, read_lanes));
     int rc = SMEM_OK;
     hipError_t e = hipSuccess;
@@ -2682,6 +2692,12 @@ int smem_gpu_set_max_active(smem_gpu_t* g, int n) {
     g->max_active = n > 0 ? n : 8;
     g->adm_cv.notify_all();
     return SMEM_OK;
+}
+
+int smem_gpu_get_max_active(const smem_gpu_t* g) {
+    if (!g) return SMEM_E_ARG;
+    std::lock_guard<std::mutex> lk(const_cast<smem_gpu_t*>(g)->adm_mu);
+    return g->max_active;
 }
 
 int smem_gpu_reserve_slots(smem_gpu_t* g, int n_slots, int reads_per_slot, int max_len) {

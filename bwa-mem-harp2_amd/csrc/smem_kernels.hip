@@ -2054,26 +2054,28 @@ __global__ void ovf_slot_kernel(const int32_t* __restrict__ items, int n_ovf, in
 }  // namespace smem
 
 // ------------------------------------------------------------ host launchers
-// The product build instantiates the default kernel (2; 0, 20 and 26 name it too),
-// its stamped diagnostic twin (9), the k-mer table variant (23), the claim-ahead
-// variant and its stamped twin (24, 25) and the priority A/B pair (27, 28).  The other
-// A/B variants measured in rounds 1-2 are compiled only with
-// SMEM_AB_VARIANTS (make AB=1): 14 instantiations of the kernel otherwise ship
-// in every library for numbers already recorded.
+// The product build instantiates the default kernel (seed_wp_kernel variant 49;
+// 0 names it too) and its k-mer table twin (54).  Every other seeding kernel
+// measured in rounds 1-5 (seed_kernel variants 2-31; the seed_wp_kernel shapes
+// and OPT-bit twins 40-62 other than 49 / 54) is compiled only
+// with SMEM_AB_VARIANTS (make AB=1): the library ships no kernel whose numbers
+// are already recorded.
 extern "C" int smem_seed_variant_built(int variant) {
-    if (variant >= 40 && variant <= 62) return 1;  // seed_wp_kernel
 #ifdef SMEM_AB_VARIANTS
-    return variant == 0 || (variant >= 2 && variant <= 31);
+    return variant == 0 || (variant >= 2 && variant <= 31) || (variant >= 40 && variant <= 62);
 #else
-    return variant == 0 || variant == 2 || variant == 9 || variant == 20 || variant == 23 || variant == 24 ||
-           variant == 25 || variant == 26 || variant == 27 || variant == 28 || variant == 29 || variant == 30 ||
-           variant == 31;
+    return variant == 0 || variant == 49 || variant == 54;
 #endif
 }
 
 extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int block, int variant, hipStream_t st) {
     switch (variant) {
-        // 9: the default (wave priority included) with cycle stamps
+#ifdef SMEM_AB_VARIANTS
+        // 2 (20 and 26 name it too): round 4's default seed_kernel -- Occ64, the two bucket slots per
+        // lane in registers, 11 list entries per lane in LDS (the forward list as a ring of its last 11
+        // pushes), wave priority raised from the top of an iteration until its loads are issued (PRIO 1)
+        case 2: case 20: case 26: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 9: variant 2 (wave priority included) with cycle stamps
         case 9: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, true, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
         // 23: the default with the k-mer table (P->kt)
         case 23: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, true>), dim3(grid), dim3(block), 0, st, *P); break;
@@ -2102,14 +2104,12 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 47: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 1, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 48: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 24, 1, 3, true>), dim3(grid), dim3(block), 0, st, *P); break;
         // 49-51: 4 blocks per CU: <24, 18>, <20, 22>, 44 without wave priority
-        case 49: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 50: hipLaunchKernelGGL((smem::seed_wp_kernel<20, 22, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 51: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 16, 0, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         // 52-53: 4 blocks per CU: <24, 20>, <28, 16>
         case 52: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 20, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
         case 53: hipLaunchKernelGGL((smem::seed_wp_kernel<28, 16, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
-        // 54-55: with the k-mer table (KT; smem_gpu_set_kmer_table, no table: plain): 49's shape, 40's shape
-        case 54: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 55: with the k-mer table (KT; smem_gpu_set_kmer_table, no table: plain), 40's shape
         case 55: hipLaunchKernelGGL((smem::seed_wp_kernel<32, 20, 1, 3, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         // 56-57: descriptors by start position (DPOS): 49's shape, and with the k-mer table
         case 56: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
@@ -2122,7 +2122,6 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 60: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 11>), dim3(grid), dim3(block), 0, st, *P); break;
         case 61: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 14>), dim3(grid), dim3(block), 0, st, *P); break;
         case 62: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, false, false, 7>), dim3(grid), dim3(block), 0, st, *P); break;
-#ifdef SMEM_AB_VARIANTS
         // 3: reference-layout buckets, cooperative fetch, lists in global memory;
         // 4: reference layout, per-lane fetch; 5: Occ64 with 12 list entries in
         // LDS at 2 blocks per CU; 6: Occ64, lists in global memory; 7: the
@@ -2149,12 +2148,11 @@ extern "C" hipError_t smem_launch_seed(const smem::SeedParams* P, int grid, int 
         case 21: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 4, 7, true, false, false, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
         case 22: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, true, true, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
 #endif
-        // default (2; 0, 20 and 26 name it too): Occ64, the two bucket slots per
-        // lane in registers, 11 list entries per lane in LDS (the forward list as
-        // a ring of its last 11 pushes), wave priority raised from the top of an
-        // iteration until its loads are issued (PRIO 1: busy 24.93 -> 24.44 ms
-        // uniform, 32.38 -> 31.88 ms human-like against variant 28)
-        default: hipLaunchKernelGGL((smem::seed_kernel<smem::FETCH_OCC64, false, 3, 11, true, false, false, true, false, true, false, false, 1>), dim3(grid), dim3(block), 0, st, *P); break;
+        // 54: the default's shape with the k-mer table (KT; smem_gpu_set_kmer_table, no table: plain)
+        case 54: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4, false, true>), dim3(grid), dim3(block), 0, st, *P); break;
+        // default (49; 0 names it): seed_wp_kernel<24 owners per wave, 18 LDS list entries per owner,
+        // wave priority, 4 blocks per CU> with every OPT bit
+        default: hipLaunchKernelGGL((smem::seed_wp_kernel<24, 18, 1, 4>), dim3(grid), dim3(block), 0, st, *P); break;
     }
     return hipGetLastError();
 }

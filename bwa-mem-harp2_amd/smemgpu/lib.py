@@ -34,7 +34,7 @@ EXPORTED = [
     "smem_gpu_seed_stream", "smem_batch_results_packed",
     "smem_gpu_load_pac", "smem_batch_chain2aln", "smem_batch_aln_results", "smem_ksw_align2",
     "smem_gpu_init_devices", "smem_gpu_parse_devices", "smem_gpu_collect_ex", "smem_batch_fetch_mask",
-    "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_kernel_id", "smem_gpu_fault",
+    "smem_gpu_reserve_slots", "smem_gpu_set_max_active", "smem_gpu_get_max_active", "smem_gpu_kernel_id", "smem_gpu_fault",
     "smem_batch_memory", "smem_gpu_memory", "smem_gpu_init_devices_async", "smem_gpu_wait_ready",
     "smem_gpu_open_async", "smem_gpu_load_sa_async", "smem_gpu_load_pac_async",
 ]
@@ -237,6 +237,7 @@ def load() -> C.CDLL:
     lib.smem_gpu_kernel_id.restype = C.c_char_p
     lib.smem_gpu_reserve_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
     lib.smem_gpu_set_max_active.argtypes = [C.c_void_p, C.c_int]
+    lib.smem_gpu_get_max_active.argtypes = [C.c_void_p]
     lib.smem_gpu_fault.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
     lib.smem_gpu_init_devices_async.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                                 P(C.c_uint64), C.c_void_p, C.c_void_p, C.c_int64]
@@ -518,6 +519,13 @@ class Gpu:
     def set_max_active(self, n: int) -> None:
         """Admission: at most n calls on the device at once (smem_gpu_set_max_active; 0 = default)."""
         _check(load().smem_gpu_set_max_active(self._h, n), "smem_gpu_set_max_active")
+
+    def max_active(self) -> int:
+        """The admission limit in force (smem_gpu_get_max_active)."""
+        rc = load().smem_gpu_get_max_active(self._h)
+        if rc < 0:
+            _check(rc, "smem_gpu_get_max_active")
+        return rc
 
     def memory(self) -> dict:
         """smem_gpu_memory: bytes of the resident index, of the kept batches (device / pinned)."""

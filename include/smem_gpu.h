@@ -221,6 +221,9 @@ int  smem_gpu_grid_reads(const smem_gpu_t *gpu);
  * others wait for a pair instead of being rejected.  Default 8, or
  * SMEM_GPU_MAX_ACTIVE at smem_gpu_init; 0 restores the default. */
 int  smem_gpu_set_max_active(smem_gpu_t *gpu, int n);
+/* The admission limit in force (what smem_gpu_set_max_active / SMEM_GPU_MAX_ACTIVE
+ * set): the batches a device runs at once, for a caller's batch plan. */
+int  smem_gpu_get_max_active(const smem_gpu_t *gpu);
 /* 0: the device has not faulted; 1: a HIP runtime failure faulted it (the
  * HIP runtime may also have printed its own diagnostics -- on a queue abort,
  * a dump of the queue's packets on stdout); 2: an injected sticky fault

@@ -140,6 +140,8 @@ def test_human_kmer_table(human, gpu_device):
     """Variant 23 with a 12-mer table at human size (34-bit table entries)."""
     from smemgpu import synth
     gpu = human["gpu"]
+    if not smemgpu.load().smem_seed_variant_built(23):
+        pytest.skip("A/B variant 23 is not in this build (make AB=1)")
     reads = synth.make_reads(human["codes"], 4_000, 150, seed=7, sub_rate=0.03, n_rate=0.001)
     gpu.set_kmer_table(12)
     try:
@@ -153,11 +155,13 @@ def test_human_kmer_table(human, gpu_device):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("variant", [40, 41, 54])
+@pytest.mark.parametrize("variant", [40, 41, 49, 54])
 def test_human_wp_kernel(human, variant):
     """seed_wp_kernel at human size: forward lists longer than the LDS lists
     (entries in the owner's arena, both list regions), 34-bit coordinates."""
     from smemgpu import synth
+    if not smemgpu.load().smem_seed_variant_built(variant):
+        pytest.skip(f"A/B variant {variant} is not in this build (make AB=1)")
     gpu = human["gpu"]
     gpu.set_variant(variant)
     if variant == 54:

@@ -157,8 +157,10 @@ def test_admission_bound_concurrent_workers(small, gpu_device):
         except Exception as e:  # surfaced below
             errs.append(e)
 
+    assert gpu.max_active() == 8  # the default (SMEM_GPU_MAX_ACTIVE unset)
     for limit, reps in ((4, 1), (2, 3)):
         gpu.set_max_active(limit)
+        assert gpu.max_active() == limit
         th = [threading.Thread(target=worker, args=(reps,)) for _ in range(6)]
         for t in th:
             t.start()
