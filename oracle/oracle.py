@@ -39,7 +39,9 @@ class Stats(C.Structure):
                                           "n_ext_u1_fwd", "n_ext_u1_bwd", "n_run_u1", "n_ext_fwd_k12")] + [
         ("n_ext_len", C.c_uint64 * 33), ("n_fwd_push", C.c_uint64), ("n_bwd_push_hi", C.c_uint64),
         ("n_bwd_read_hi", C.c_uint64), ("n_fwd_spill", C.c_uint64),
-        ("n_bwd_step", C.c_uint64), ("n_step_hist", C.c_uint64 * 17), ("n_bwd_task_hi", C.c_uint64)]
+        ("n_bwd_step", C.c_uint64), ("n_step_hist", C.c_uint64 * 17), ("n_bwd_task_hi", C.c_uint64),
+        ("n_tm_saved", C.c_uint64), ("n_tm_sa", C.c_uint64), ("n_tm_isa", C.c_uint64), ("n_tm_runs", C.c_uint64),
+        ("n_tm_bases", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if k in ("n_ext_len", "n_step_hist") else int(getattr(self, k))) for k, _ in self._fields_}

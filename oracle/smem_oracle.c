@@ -155,18 +155,21 @@ typedef struct {
 	orc_stats_t st;
 } worker_t;
 
-static void count_extend(const orc_bwt_t *b, const orc_intv_t *ik, int is_back, int used, orc_stats_t *st)
+/* returns the Occ64 bucket loads of the extend (0 when not used) */
+static int count_extend(const orc_bwt_t *b, const orc_intv_t *ik, int is_back, int used, orc_stats_t *st)
 {
 	uint64_t k = ik->x[!is_back] - 1, l = k + ik->x[2];
 	uint64_t kk = k - (k >= b->primary), ll = l - (l >= b->primary);
 	uint64_t nb = (k == (uint64_t)-1) ? 1 : 1 + ((kk >> 7) != (ll >> 7));
+	int nb64 = (k == (uint64_t)-1) ? 1 : 1 + ((kk >> 6) != (ll >> 6));
 	st->n_ext_ref++;
 	st->n_bkt_ref += nb;
 	if (used) {
 		st->n_ext++;
 		st->n_bkt += nb;
-		st->n_bkt64 += (k == (uint64_t)-1) ? 1 : 1 + ((kk >> 6) != (ll >> 6));
+		st->n_bkt64 += nb64;
 	}
+	return used ? nb64 : 0;
 }
 
 /* ------------------------------------------------------------ bwt_smem1 */
@@ -191,6 +194,10 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 	int i, j, c, ret;
 	uint64_t ik_prev2 = 0;
 	int had_u1 = 0, has_u1 = 0;
+	/* text-mode model: tm = ik came from a text compare (x1 unknown), tm_pos = its text
+	 * position is known; for the backward list's entry 0 (the only one that can have
+	 * size 1: sizes strictly grow along a list) p0_lazy = x0 unknown, p0_pos likewise */
+	int tm = 0, tm_pos = 0, p0_lazy = 0, p0_pos = 0, c0_lazy = 0, c0_pos = 0, in_run = 0;
 
 	mem->n = 0;
 	w->st.n_smem1++;
@@ -209,20 +216,29 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 		if (q[i] > 3) { iv_push(&w->fwd, &ik); break; }      /* ambiguous base */
 		c = 3 - q[i];
 		orc_extend(b, &ik, ok, 0);
-		count_extend(b, &ik, 0, 1, &w->st);
+		{
+			int nb64 = count_extend(b, &ik, 0, 1, &w->st);
+			if (ik.x[2] == 1) {  /* text mode: q[i] against the text after the occurrence */
+				w->st.n_tm_saved += nb64;
+				if (!tm_pos) { w->st.n_tm_sa++; tm_pos = 1; w->st.n_tm_runs++; }
+				w->st.n_tm_bases++;
+			}
+		}
 		w->st.n_ext_fwd++;
 		w->st.n_ext_len[i + 1 - x < 32 ? i + 1 - x : 32]++;
 		if (i - x <= 12) w->st.n_ext_fwd_k12++;
 		if (ik.x[2] == 1) { w->st.n_ext_u1_fwd++; if (i == x + 1 || ik_prev2 != 1) w->st.n_run_u1++; }
 		ik_prev2 = ik.x[2];
 		if (ok[c].x[2] != ik.x[2]) {
+			if (tm) w->st.n_tm_isa++;  /* the pushed interval's exact x1 */
 			iv_push(&w->fwd, &ik);
 			if (ok[c].x[2] < (uint64_t)min_intv) break;
 		}
+		tm = ik.x[2] == 1;
 		ik = ok[c];
 		ik.info = (uint64_t)(i + 1);
 	}
-	if (i == len) iv_push(&w->fwd, &ik);
+	if (i == len) { if (tm) w->st.n_tm_isa++; iv_push(&w->fwd, &ik); }
 	w->st.n_fwd_push += w->fwd.n;
 	if ((int)w->fwd.n > NL) w->st.n_fwd_spill += w->fwd.n - NL;  /* the LDS ring spills its oldest entries */
 	iv_reverse(&w->fwd);                 /* longest match first (software/bwt.c:806) */
@@ -231,9 +247,15 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 	/* backward extension of every surviving interval (software/bwt.c:810-829) */
 	prev->n = 0;
 	for (j = 0; j < (int)w->fwd.n; ++j) iv_push(prev, &w->fwd.a[j]);
+	/* prev[0] is the forward phase's last push: exact, at the forward run's text position
+	 * when the forward phase compared text (its x0 never changed) */
+	p0_lazy = 0;
+	p0_pos = w->fwd.n > 0 && w->fwd.a[0].x[2] == 1 && tm_pos;
+	in_run = p0_pos;
 	for (i = x - 1; i >= -1; --i) {
 		c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
 		curr->n = 0;
+		c0_lazy = c0_pos = 0;
 		had_u1 = has_u1; has_u1 = 0;
 		if (c >= 0) {
 			w->st.n_bwd_step++;
@@ -244,7 +266,15 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 			if (i < x - 1 && j >= NL) w->st.n_bwd_read_hi++;
 			if (c >= 0 && j >= NL) w->st.n_bwd_task_hi++;
 			orc_extend(b, p, ok, 1);
-			count_extend(b, p, 1, c >= 0, &w->st);
+			{
+				int nb64 = count_extend(b, p, 1, c >= 0, &w->st);
+				if (c >= 0 && p->x[2] == 1) {  /* text mode: q[i] against the base before the occurrence */
+					w->st.n_tm_saved += nb64;
+					if (!p0_pos) w->st.n_tm_sa++;
+					if (!in_run) w->st.n_tm_runs++;
+					w->st.n_tm_bases++;
+				}
+			}
 			if (c >= 0) { int sl = (int)(uint32_t)p->info - i; w->st.n_ext_len[sl < 32 ? sl : 32]++; }
 			if (c >= 0 && p->x[2] == 1) {
 				w->st.n_ext_u1_bwd++;
@@ -256,17 +286,24 @@ static int smem1(const orc_bwt_t *b, int len, const uint8_t *q, int x, int min_i
 				 * already kept at this i, or it is contained in the last one */
 				if (curr->n == 0 && (mem->n == 0 || (uint64_t)(i + 1) < mem->a[mem->n - 1].info >> 32)) {
 					orc_intv_t e = *p;
+					if (j == 0 && p0_lazy) w->st.n_tm_isa++;  /* the emitted SMEM's exact x0 */
 					e.info |= (uint64_t)(i + 1) << 32;
 					iv_push(mem, &e);
 				}
 			} else if (curr->n == 0 || ok[c].x[2] != curr->a[curr->n - 1].x[2]) {
 				if ((int)curr->n >= NL) w->st.n_bwd_push_hi++;
 				ok[c].info = p->info;
+				if (curr->n == 0) {  /* the new entry 0: lazy when a text compare made it */
+					c0_lazy = p->x[2] == 1;
+					c0_pos = p->x[2] == 1;
+				}
 				iv_push(curr, &ok[c]);
 			}
 		}
 		if (curr->n == 0) break;
 		t = curr; curr = prev; prev = t;
+		p0_lazy = c0_lazy; p0_pos = c0_pos;
+		in_run = p0_pos;
 	}
 	iv_reverse(mem);                     /* sorted by start (software/bwt.c:830) */
 	return ret;
@@ -406,6 +443,8 @@ static void add_stats(orc_stats_t *d, const orc_stats_t *s)
 	d->n_fwd_push += s->n_fwd_push; d->n_bwd_push_hi += s->n_bwd_push_hi; d->n_bwd_read_hi += s->n_bwd_read_hi;
 	d->n_fwd_spill += s->n_fwd_spill;
 	d->n_bwd_step += s->n_bwd_step; d->n_bwd_task_hi += s->n_bwd_task_hi;
+	d->n_tm_saved += s->n_tm_saved; d->n_tm_sa += s->n_tm_sa; d->n_tm_isa += s->n_tm_isa;
+	d->n_tm_runs += s->n_tm_runs; d->n_tm_bases += s->n_tm_bases;
 	{ int k; for (k = 0; k < 17; ++k) d->n_step_hist[k] += s->n_step_hist[k]; }
 }
 

@@ -65,6 +65,15 @@ typedef struct {
 	uint64_t n_bwd_step;    /* backward steps with a base to extend by (c >= 0, software/bwt.c:812) */
 	uint64_t n_step_hist[17]; /* those steps by prev->n: 1..15, 16 = 16 or more */
 	uint64_t n_bwd_task_hi; /* backward extends (c >= 0, any step) of prev[j], j >= NL */
+	/* the unique-interval text mode, modelled (tools/text_mode_model.py): an
+	 * extend whose input has x2 == 1 decided by comparing the read with the reference text
+	 * instead of by Occ64 buckets; a full SA and ISA resident give the text position and the
+	 * exact x0 / x1 of a text-mode interval when it is pushed or emitted */
+	uint64_t n_tm_saved;    /* Occ64 bucket loads (n_bkt64's count) of those extends */
+	uint64_t n_tm_sa;       /* SA loads: a size-1 interval's text position, once per run */
+	uint64_t n_tm_isa;      /* ISA loads: exact x1 (forward push) / x0 (backward emit) of a text-mode result */
+	uint64_t n_tm_runs;     /* runs of text compares (each starts a 16-B .pac block load) */
+	uint64_t n_tm_bases;    /* bases compared against the text */
 } orc_stats_t;
 
 orc_bwt_t *orc_bwt_load(const char *fn);
