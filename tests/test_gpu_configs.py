@@ -138,6 +138,7 @@ def test_human_c5_5pct(human):
 @pytest.mark.timeout(900)
 def test_human_kmer_table(human, gpu_device):
     """Variant 23 with a 12-mer table at human size (34-bit table entries)."""
+    import smemgpu
     from smemgpu import synth
     gpu = human["gpu"]
     if not smemgpu.load().smem_seed_variant_built(23):
@@ -159,6 +160,7 @@ def test_human_kmer_table(human, gpu_device):
 def test_human_wp_kernel(human, variant):
     """seed_wp_kernel at human size: forward lists longer than the LDS lists
     (entries in the owner's arena, both list regions), 34-bit coordinates."""
+    import smemgpu
     from smemgpu import synth
     if not smemgpu.load().smem_seed_variant_built(variant):
         pytest.skip(f"A/B variant {variant} is not in this build (make AB=1)")

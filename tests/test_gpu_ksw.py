@@ -16,11 +16,15 @@ from tests import golden_data
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["wave", "g16", "lane"], autouse=True)
+@pytest.fixture(params=["wave", "wave_unsorted", "g16", "lane"], autouse=True)
 def ksw_kernel(request, monkeypatch):
-    """Every test on each kernel: one problem per wave, four per wave on
-    16-lane groups (SMEM_KSW_G16, kswd::extend_group16), and one per lane
-    (SMEM_KSW_LANE, kswl::extend_lane, with its fallbacks to one per wave)."""
+    """Every test on each kernel: one problem per wave (the problems in
+    query-length order, the default, and in the caller's order:
+    SMEM_KSW_SORT=0), four per wave on 16-lane groups (SMEM_KSW_G16,
+    kswd::extend_group16), and one per lane (SMEM_KSW_LANE, kswl::extend_lane,
+    with its fallbacks to one per wave)."""
+    if request.param == "wave_unsorted":
+        monkeypatch.setenv("SMEM_KSW_SORT", "0")
     if request.param == "g16":
         monkeypatch.setenv("SMEM_KSW_G16", "1")
     if request.param == "lane":
