@@ -268,6 +268,11 @@ static int seed_owners_per_wave(int variant) {
 }
 // lanes a launch gives each read so that every owner of a small batch's grid has one
 static int seed_lanes_per_read(int variant) { return (64 + seed_owners_per_wave(variant) - 1) / seed_owners_per_wave(variant); }
+// list arenas a launch of `lanes` lanes addresses (2 x cap_list packed entries each): seed_wp_kernel
+// one per owner (OWN a wave), seed_kernel one per lane
+static size_t seed_arenas(int variant, int lanes) {
+    return variant >= 40 ? (size_t)(lanes / 64) * (size_t)seed_owners_per_wave(variant) : (size_t)lanes;
+}
 
 struct smem_gpu {
     int device = 0;
@@ -895,7 +900,7 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     if (e == hipSuccess) e = b->d_ovf_items.ensure(R);
     if (e == hipSuccess) e = b->d_ovf_items2.ensure(R);
     if (e == hipSuccess) e = b->d_ovf_slot.ensure(R);
-    if (e == hipSuccess) e = b->d_scratch.ensure((size_t)b->lanes * 2 * b->cap_list);  // 2 packed lists per lane
+    if (e == hipSuccess) e = b->d_scratch.ensure(seed_arenas(g->variant, b->lanes) * 2 * b->cap_list);  // 2 packed lists
     if (e == hipSuccess) e = b->d_sz_intv.ensure(R);
     if (e == hipSuccess) e = b->d_sz_calls.ensure(R);
     if (e == hipSuccess) e = b->d_intv_off.ensure(R + 1);
@@ -1025,6 +1030,9 @@ static int batch_run_impl(smem_batch_t* b, const smem_opt_t* opt) {
     const int lanes = std::min(b->lanes, std::max(256, (n * seed_lanes_per_read(g->variant) + 255) / 256 * 256));
     const int grid = lanes / 256;
     b->stats.grid = grid;
+    // (a variant set after smem_batch_create may address more arenas than the batch was made for)
+    HIP_TRY(b->d_scratch.ensure(seed_arenas(g->variant, b->lanes) * 2 * b->cap_list));
+    P.scratch = b->d_scratch.p;
     HIP_TRY(hipMemsetAsync(b->d_ctr.p, 0, 8 * sizeof(int32_t), b->st));
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
     if (g->variant == 23 && !g->d_kt) return fail(SMEM_E_ARG, "smem_batch_run: variant 23 needs smem_gpu_set_kmer_table");
@@ -1984,7 +1992,9 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
     }
     smem::CandParams C{};
     if (n_heavy && P.lane_on) {  // the walk's scratch (its chains were prepared by the lane path)
-        HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+        // the bin hash (0.54 GB at 256 CUs) only serves a walk without the candidate index
+        // (aln_heavy_kernel: `hashed` needs !indexed)
+        if (!aln_cand_on()) HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
         HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.ht = H.ht.p, P.rnext = H.rnext.p;
         if (aln_cand_on()) {
@@ -2605,7 +2615,7 @@ static int batch_prealloc(smem_batch_t* b) {
     HIP_TRY(H.hscnt.grow(R));
     HIP_TRY(H.hoff.grow(R + 1));
     HIP_TRY(H.rnext.grow(ns));
-    HIP_TRY(H.ht.grow((size_t)b->g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+    // (H.ht, the walk's bin hash, is grown by run_aln only for a walk without the candidate index)
     HIP_TRY(b->d_aln_out.grow(R * 4));
     HIP_TRY(b->h_aln_regoff.grow(R + 1));
     HIP_TRY(b->h_aln_regs.grow(R * 4));  // pinned: the regions fetched (~3 per read)
@@ -2689,6 +2699,20 @@ int smem_gpu_memory(smem_gpu_t* g, uint64_t* index_bytes, uint64_t* batch_bytes,
         for (auto& kv : g->per_thread) add(kv.second);
         for (auto* b : g->slots) add(b);
         for (auto* b : g->stream_pool) add(b);
+        // SMEM_GPU_MEMORY_DETAIL=1: the first slot's device buffers of >= 8 MB, by their place in
+        // batch_bufs' visit order (a diagnostic of the per-slot footprint)
+        if (getenv("SMEM_GPU_MEMORY_DETAIL") && !g->slots.empty() && g->slots[0]) {
+            int k = 0;
+            uint64_t mx = 0;
+            std::string line;
+            batch_bufs(g->slots[0], [&](auto& x) {
+                if (x.bytes() >= (8ull << 20)) line += " #" + std::to_string(k) + ":" + std::to_string(x.bytes() >> 20) + "M";
+                mx += x.bytes();
+                ++k;
+            }, [](auto&) {});
+            fprintf(stderr, "[M::smem_gpu_memory] device %d slot 0 (max_reads %d): %.3f GB;%s\n", g->device,
+                    g->slots[0]->max_reads, mx / 1e9, line.c_str());
+        }
     }
     if (index_bytes) *index_bytes = ix;
     if (batch_bytes) *batch_bytes = d;

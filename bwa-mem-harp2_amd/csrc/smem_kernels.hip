@@ -1398,8 +1398,11 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     const int me = (int)(threadIdx.x & 63);
     const uint64_t wave_g = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);  // lane 0's global index
     const uint32_t cap = P.cap_list;
-    // an owner's arena: [0, cap) the forward list beyond the ring, [cap, 2 cap) curr / prev beyond NL
-    PIntv* __restrict__ bp = reinterpret_cast<PIntv*>(P.scratch + (wave_g + (uint64_t)me) * 2ull * cap);
+    // an owner's arena: [0, cap) the forward list beyond the ring, [cap, 2 cap) curr / prev beyond NL;
+    // one per owner (OWN a wave, numbered from wown), not per lane: the batch's scratch is 64 / OWN
+    // times smaller (smem_gpu.cpp seed_arenas)
+    const uint64_t wown = (wave_g >> 6) * (uint64_t)OWN;
+    PIntv* __restrict__ bp = reinterpret_cast<PIntv*>(P.scratch + (wown + (uint64_t)(me < OWN ? me : 0)) * 2ull * cap);
 
     int phase = me < OWN ? P_FETCH : P_EXIT;  // lanes >= OWN only execute extends
     int item = -1, len = 0;
@@ -1786,7 +1789,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             } else if constexpr (OPT & 2) {
                 far = true;
             } else {
-                const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wown + o) * 2ull * cap);
                 const uint32_t at = w0.z + jj;
                 ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
             }
@@ -1798,7 +1801,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
                     } else if constexpr (OPT & 2) {
                         far2 = true;
                     } else {
-                        const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+                        const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wown + o) * 2ull * cap);
                         const uint32_t at = w0.z + jj + 1;
                         ent2 = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
                     }
@@ -1811,7 +1814,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
         // wave-uniform branch that waits for them itself -- a wait at the join would run every
         // iteration, and one vmcnt counts the owners' result stores too (their acks, every iteration)
         if (OPT & 2 && __builtin_expect(__any(far || far2), 0)) {
-            const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+            const PIntv* obp = reinterpret_cast<const PIntv*>(P.scratch + (wown + o) * 2ull * cap);
             if (far) {
                 const uint32_t at = w0.z + jj;
                 ent = *reinterpret_cast<const uint4*>(obp + (at < 2 * cap ? at : 0u));
@@ -1938,7 +1941,7 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
             const uint32_t pf = L->tabP[s];
             const uint64_t before = (1ull << me) - 1ull & ~((1ull << pf) - 1ull);
             const uint32_t kr = (uint32_t)(__popcll(kmask & before) + __popcll(kmask2 & before));
-            PIntv* obp = reinterpret_cast<PIntv*>(P.scratch + (wave_g + o) * 2ull * cap);
+            PIntv* obp = reinterpret_cast<PIntv*>(P.scratch + (wown + o) * 2ull * cap);
             if (keep) {
                 const uint32_t idx = w0.y + kr;
                 const uint4 e = pack_p(na, nb, ns, p_end(ent));
