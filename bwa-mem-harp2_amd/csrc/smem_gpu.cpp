@@ -271,7 +271,12 @@ static int seed_lanes_per_read(int variant) { return (64 + seed_owners_per_wave(
 // list arenas a launch of `lanes` lanes addresses (2 x cap_list packed entries each): seed_wp_kernel
 // one per owner (OWN a wave), seed_kernel one per lane
 static size_t seed_arenas(int variant, int lanes) {
+#ifdef SMEM_WP_ARENA_PER_LANE
+    (void)variant;
+    return (size_t)lanes;
+#else
     return variant >= 40 ? (size_t)(lanes / 64) * (size_t)seed_owners_per_wave(variant) : (size_t)lanes;
+#endif
 }
 
 struct smem_gpu {

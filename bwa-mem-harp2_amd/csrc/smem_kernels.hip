@@ -1401,8 +1401,13 @@ __global__ __launch_bounds__(256, WPE) void seed_wp_kernel(SeedParams P) {
     // an owner's arena: [0, cap) the forward list beyond the ring, [cap, 2 cap) curr / prev beyond NL;
     // one per owner (OWN a wave, numbered from wown), not per lane: the batch's scratch is 64 / OWN
     // times smaller (smem_gpu.cpp seed_arenas)
+#ifdef SMEM_WP_ARENA_PER_LANE  // (A/B: round 5's one arena per lane)
+    const uint64_t wown = wave_g;
+    PIntv* __restrict__ bp = reinterpret_cast<PIntv*>(P.scratch + (wown + (uint64_t)me) * 2ull * cap);
+#else
     const uint64_t wown = (wave_g >> 6) * (uint64_t)OWN;
     PIntv* __restrict__ bp = reinterpret_cast<PIntv*>(P.scratch + (wown + (uint64_t)(me < OWN ? me : 0)) * 2ull * cap);
+#endif
 
     int phase = me < OWN ? P_FETCH : P_EXIT;  // lanes >= OWN only execute extends
     int item = -1, len = 0;

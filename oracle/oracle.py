@@ -78,6 +78,9 @@ def load() -> C.CDLL:
         lib.orc_seed_timed.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.POINTER(OptT), C.c_int,
                                        C.POINTER(Stats)]
         lib.orc_seed_timed.restype = C.c_double
+        lib.orc_seed_trace.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.POINTER(OptT), C.c_void_p,
+                                       C.c_uint64, C.c_void_p]
+        lib.orc_seed_trace.restype = C.c_int64
         lib.orc_free.argtypes = [C.c_void_p]
         lib.orc_free.restype = None
         lib.orc_occ4.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
@@ -228,6 +231,28 @@ def seed(index: OracleIndex, codes: np.ndarray, offs: np.ndarray, threads: int =
     data = C.string_at(out, out_len.value)
     lib.orc_free(out)
     return data, {"n_intv": n_intv[:n], "n_calls": n_calls[:n], "bytes": nbytes[:n]}, st.as_dict()
+
+
+def seed_trace(index: OracleIndex, codes: np.ndarray, offs: np.ndarray, **opt):
+    """Occ64 bucket index of every load the GPU seeding kernel makes, in
+    extend order (bit 31: an extend's second bucket), and the per-read
+    offsets into it (orc_seed_trace; for tools/replay_ceiling.py)."""
+    lib = load()
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    n = offs.size - 1
+    o = _opt(**opt)
+    roff = np.zeros(n + 1, dtype=np.uint64)
+    cap = max(1, int(3000 * n))
+    while True:
+        buf = np.zeros(cap, dtype=np.uint32)
+        tot = lib.orc_seed_trace(index._h, n, codes.ctypes.data, offs.ctypes.data, C.byref(o), buf.ctypes.data,
+                                 cap, roff.ctypes.data)
+        if tot < 0:
+            raise RuntimeError("orc_seed_trace failed")
+        if tot <= cap:
+            return buf[:tot], roff
+        cap = int(tot)
 
 
 def seed_stats(index: OracleIndex, codes, offs, threads: int = 1, **opt):

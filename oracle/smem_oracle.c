@@ -155,6 +155,17 @@ typedef struct {
 	orc_stats_t st;
 } worker_t;
 
+/* orc_seed_trace: the Occ64 bucket index of every load the GPU kernel makes,
+ * in extend order (bit 31: the second bucket of the same extend) */
+typedef struct { uint32_t *p; uint64_t n, cap; } trace_t;
+static __thread trace_t *g_trace;
+
+static void trace_put(uint32_t v)
+{
+	if (g_trace->n < g_trace->cap) g_trace->p[g_trace->n] = v;
+	g_trace->n++;
+}
+
 /* returns the Occ64 bucket loads of the extend (0 when not used) */
 static int count_extend(const orc_bwt_t *b, const orc_intv_t *ik, int is_back, int used, orc_stats_t *st)
 {
@@ -168,6 +179,13 @@ static int count_extend(const orc_bwt_t *b, const orc_intv_t *ik, int is_back, i
 		st->n_ext++;
 		st->n_bkt += nb;
 		st->n_bkt64 += nb64;
+		if (g_trace) {
+			if (k == (uint64_t)-1) trace_put((uint32_t)(ll >> 6));
+			else {
+				trace_put((uint32_t)(kk >> 6));
+				if (nb64 == 2) trace_put((uint32_t)(ll >> 6) | 0x80000000u);
+			}
+		}
 	}
 	return used ? nb64 : 0;
 }
@@ -489,6 +507,30 @@ int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const in
 	}
 	free(jobs); free(tid);
 	return 0;
+}
+
+/* The Occ64 bucket trace of seeding reads [0, n_reads) on one thread (a
+ * replay input: tools/replay_ceiling.hip); read r's loads are
+ * out[read_off[r] .. read_off[r + 1]).  Returns the total, which may exceed
+ * cap (then only the first cap were written). */
+int64_t orc_seed_trace(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,
+		const orc_opt_t *opt, uint32_t *out, uint64_t cap, uint64_t *read_off)
+{
+	job_t jb;
+	trace_t tr = {out, 0, cap};
+	int64_t r;
+	memset(&jb, 0, sizeof(jb));
+	jb.b = b; jb.codes = codes; jb.offs = offs; jb.opt = opt;
+	g_trace = &tr;
+	for (r = 0; r < n_reads; ++r) {
+		read_off[r] = tr.n;
+		jb.beg = r; jb.end = r + 1;
+		seed_range(&jb);
+	}
+	read_off[n_reads] = tr.n;
+	g_trace = 0;
+	free_worker(&jb.w);
+	return (int64_t)tr.n;
 }
 
 double orc_seed_timed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,

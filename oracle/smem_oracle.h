@@ -100,6 +100,11 @@ int orc_seed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const in
 		orc_stats_t *stats);
 
 /* timed variant for the CPU baseline: seeds reads, returns wall seconds */
+/* every Occ64 bucket load of the GPU kernel in extend order (bit 31: the
+ * extend's second bucket), read r's at out[read_off[r] .. read_off[r+1]);
+ * one thread; returns the total (> cap: truncated) */
+int64_t orc_seed_trace(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,
+		const orc_opt_t *opt, uint32_t *out, uint64_t cap, uint64_t *read_off);
 double orc_seed_timed(const orc_bwt_t *b, int64_t n_reads, const uint8_t *codes, const int64_t *offs,
 		const orc_opt_t *opt, int n_threads, orc_stats_t *stats);
 

@@ -139,7 +139,13 @@ def test_cpu_fallback_sam_identical(indexed, g, kind):
 def _same(got, want):
     assert len(got) == len(want)
     bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
-    assert not bad, f"{len(bad)} SAM lines differ, first: {got[bad[0]][:200]} vs {want[bad[0]][:200]}"
+    if bad:
+        def fields(i):  # the fields that differ (SEQ / QUAL cut short)
+            a, b = got[i].split("\t"), want[i].split("\t")
+            return [(k, x[:60], y[:60]) for k, (x, y) in enumerate(zip(a, b)) if x != y] + \
+                [("n_fields", len(a), len(b))] * (len(a) != len(b))
+        detail = "; ".join(f"{got[i].split(chr(9))[0]}: {fields(i)}" for i in bad[:6])
+        raise AssertionError(f"{len(bad)} SAM lines differ (lines {bad[:12]}): {detail}")
 
 
 GPU_MODES = {
