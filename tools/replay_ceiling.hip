@@ -17,7 +17,7 @@
 // `reps` times (replica k of read r claimed ~k x n_reads later: far beyond any
 // cache's reuse distance).
 //
-//   hipcc --offload-arch=gfx950 -O3 -o tools/replay_ceiling tools/replay_ceiling.hip
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/replay_ceiling tools/replay_ceiling.hip
 //   tools/replay_ceiling <trace.bin> <table_buckets> <waves_per_cu> [reps=4] [uniform=0]
 //
 // trace.bin: u64 n_reads, u64 n_loads, u64 read_off[n_reads + 1], u32 loads[n_loads]

@@ -8,7 +8,7 @@ uniformly (the random-gather ceiling at the same occupancy and chain shape).
     python tools/replay_ceiling.py [--genome-profile human] [--reads 200000] [--waves 12,15,16] [--out f.json]
 
 Needs bench.py's cache of the index (run bench.py first in the same gpurun call)
-and tools/replay_ceiling built (hipcc --offload-arch=gfx950 -O3 -o tools/replay_ceiling
+and tools/replay_ceiling built (hipcc --offload-arch=gfx950 -O3 -o tools/bin/replay_ceiling
 tools/replay_ceiling.hip).
 """
 import argparse
@@ -77,7 +77,7 @@ def main():
         fh.write(roff.tobytes())
         fh.write(loads.astype(np.uint32).tobytes())
     del loads
-    exe = os.path.join(ROOT, "tools", "replay_ceiling")
+    exe = os.path.join(ROOT, "tools", "bin", "replay_ceiling")
     rep = {"reads": r.n, "genome_profile": a.genome_profile, "sub": a.sub, "n_buckets": n_buckets, "runs": []}
     for w in [int(x) for x in a.waves.split(",") if x]:
         for uni in (0, 1):
