@@ -1048,7 +1048,7 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
         if ((threadIdx.x & 63) == 0) h = atomicAdd(&P.ctr[KC > 4 ? 13 : 3], 1u);
         h = (uint32_t)uni((int)h);
         if (h >= nh) break;
-        const int r = uni(P.heavy[h]);
+        const int r = uni(P.heavy[P.horder ? P.horder[h] : h]);
         if ((uni((int)(P.offs[r + 1] - P.offs[r])) > 256) == (KC > 4)) {
             if constexpr (INL) heavy_read_walk_body<KC, true>(P, r);
             else heavy_read_walk<KC>(P, r);
@@ -1056,6 +1056,33 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
     }
 }
 
+
+// The walk's claim order: a counting sort of the heavy reads by the bit length
+// of their seeds + chains, longest first (one block; the reads of a bucket in
+// any order -- each read's walk is independent of the others').  A read of
+// thousands of seeds claimed late was the walk's tail.
+__global__ __launch_bounds__(1024) void aln_heavy_order_kernel(AlnParams P, uint32_t nh, uint32_t* horder) {
+    __shared__ uint32_t cnt[64];
+    const uint32_t t = threadIdx.x;
+    if (t < 64) cnt[t] = 0;
+    __syncthreads();
+    auto bucket = [&](uint32_t h) -> uint32_t {
+        const uint64_t w = P.hcnt[h] + P.hscnt[h];
+        return 63u - (uint32_t)__builtin_clzll(w | 1ull);  // 0..63; the larger first below
+    };
+    for (uint32_t h = t; h < nh; h += blockDim.x) atomicAdd(&cnt[bucket(h)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t o = 0;
+        for (int b = 63; b >= 0; --b) {
+            const uint32_t c = cnt[b];
+            cnt[b] = o;
+            o += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t h = t; h < nh; h += blockDim.x) horder[atomicAdd(&cnt[bucket(h)], 1u)] = h;
+}
 
 // ---- the heavy walk's candidate index (AlnParams::cand_*) ----
 // Every region a heavy read's walk can make is known before the walk: its
@@ -1599,16 +1626,21 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
     if (!(parts & 2)) return hipGetLastError();
     // the walk kernels use the per-wave hash tables in turn (same stream);
     // walk_guard != 0: the inlined, guarded walk (diagnostic)
+    const int wb = n_cu * (int)(P->walk_wpc ? P->walk_wpc : smem::ALN_WALK_WAVES) / 4;  // blocks of 4 waves
     if (P->walk_guard) {
-        hipLaunchKernelGGL((smem::aln_heavy_kernel<4, true>), dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
-        if (long_reads)
-            hipLaunchKernelGGL((smem::aln_heavy_kernel<16, true>), dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0,
-                               st, *P);
+        hipLaunchKernelGGL((smem::aln_heavy_kernel<4, true>), dim3(wb), dim3(256), 0, st, *P);
+        if (long_reads) hipLaunchKernelGGL((smem::aln_heavy_kernel<16, true>), dim3(wb), dim3(256), 0, st, *P);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
-    if (long_reads)
-        hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(n_cu * smem::ALN_WALK_WAVES / 4), dim3(256), 0, st, *P);
+    hipLaunchKernelGGL(smem::aln_heavy_kernel<4>, dim3(wb), dim3(256), 0, st, *P);
+    if (long_reads) hipLaunchKernelGGL(smem::aln_heavy_kernel<16>, dim3(wb), dim3(256), 0, st, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t smem_launch_aln_heavy_order(const smem::AlnParams* P, uint32_t n_heavy, uint32_t* horder,
+                                                  hipStream_t st) {
+    if (!n_heavy) return hipSuccess;
+    hipLaunchKernelGGL(smem::aln_heavy_order_kernel, dim3(1), dim3(1024), 0, st, *P, n_heavy, horder);
     return hipGetLastError();
 }
 

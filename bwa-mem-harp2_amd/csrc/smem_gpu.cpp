@@ -354,6 +354,7 @@ static void gpu_wait(smem_gpu_t* g) {
 // scratch of the heavy-read path of chains -> regions
 struct AlnHeavyBufs {
     DevBuf<int32_t> heavy;
+    DevBuf<uint32_t> horder;
     DevBuf<uint64_t> hcnt, hoff, hscnt;
     DevBuf<int64_t> span;
     DevBuf<uint64_t> ht;
@@ -374,7 +375,7 @@ struct AlnHeavyBufs {
     template <class F>
     void each(F&& f) {
         f(ckey); f(ckey2); f(coff); f(ccnt); f(cval); f(cval2); f(cq); f(cpos_s); f(cpos_c); f(chord); f(chmax);
-        f(crb); f(cre); f(cmade); f(ctmp); f(crng); f(heavy); f(hcnt); f(hoff); f(hscnt); f(span); f(ht); f(rnext);
+        f(crb); f(cre); f(cmade); f(ctmp); f(crng); f(heavy); f(horder); f(hcnt); f(hoff); f(hscnt); f(span); f(ht); f(rnext);
         f(pre); f(pre_short); f(loc); f(short_ok); f(pre_ok); f(tmp); f(tasks); f(torder); f(lq); f(tfail); f(sdec);
         f(chain_read); f(swlist); f(htasks); f(htorder); f(hlq); f(htfail);
     }
@@ -883,11 +884,13 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
     b->cap_calls = (uint32_t)(max_len / 4 + 16);  // ~6 lists per 150 bp read; more -> overflow pass
     b->cap_list = (uint32_t)max_len + 2;   // forward/backward lists hold <= len+1 intervals
     const int want_lanes = g->n_cu * (g->lanes_per_cu > 0 ? g->lanes_per_cu : seed_lanes_per_cu(g->variant));
-    // seed_wp_kernel owns 24 reads per wave (variant 49): seed_lanes_per_read lanes per read
-    // give every read of a small batch an owner; batch_run_impl bounds each launch by b->lanes,
-    // the lanes the scratch below was sized for, whatever variant is set later
-    const int read_lanes =
-        (int)std::min<int64_t>((int64_t)seed_lanes_per_read(g->variant) * max_reads + 255, INT32_MAX) / 256 * 256;
+    // a persistent grid of at most one lane per read: a batch under a full grid (the binding's
+    // worker batches) runs beside the device's other admitted batches, which fill
+    // the CUs its grid leaves, and each lane of the grid costs list-arena scratch (one arena per
+    // owner, 2 x cap_list entries: 9 KB per read at 3 lanes a read and 256-bp slots).  Owners
+    // (24 a wave) then take 2.7 reads each in turn.  batch_run_impl bounds each launch by
+    // b->lanes, the lanes the scratch below was sized for, whatever variant is set later.
+    const int read_lanes = (int)std::min<int64_t>((int64_t)max_reads + 255, INT32_MAX) / 256 * 256;
     b->lanes = std::max(256, std::min(want_lanes, read_lanes));
     int rc = SMEM_OK;
     hipError_t e = hipSuccess;
@@ -1895,6 +1898,18 @@ static bool aln_cand_on() {
     const char* e = getenv("SMEM_ALN_CAND");
     return !e || atoi(e) != 0;
 }
+// the heavy walk's waves per CU (SMEM_ALN_WALK_WAVES; aln_heavy_kernel takes 132 VGPRs: at most
+// 12) and its claim order (SMEM_ALN_WALK_ORDER=0: the classify kernel's order instead of the
+// reads with the most seeds + chains first)
+static uint32_t aln_walk_wpc() {
+    const char* e = getenv("SMEM_ALN_WALK_WAVES");
+    const int v = e ? atoi(e) : smem::ALN_WALK_WAVES;
+    return (uint32_t)std::max(4, std::min(16, v / 4 * 4));
+}
+static bool aln_walk_order() {
+    const char* e = getenv("SMEM_ALN_WALK_ORDER");
+    return !(e && atoi(e) == 0);
+}
 // SMEM_ALN_LANE=0: no regions computed ahead one seed per lane (the walks
 // extend every seed one wave per problem, round-2 style)
 static bool aln_lane_on() {
@@ -1995,11 +2010,18 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(hipStreamSynchronize(st));
         n_heavy = (uint32_t)hs[0];
     }
+    P.walk_wpc = aln_walk_wpc();
+    P.horder = nullptr;
+    if (n_heavy && aln_walk_order()) {
+        HIP_TRY(H.horder.grow(n_heavy));
+        HIP_TRY(smem_launch_aln_heavy_order(&P, n_heavy, H.horder.p, st));
+        P.horder = H.horder.p;
+    }
     smem::CandParams C{};
     if (n_heavy && P.lane_on) {  // the walk's scratch (its chains were prepared by the lane path)
         // the bin hash (0.54 GB at 256 CUs) only serves a walk without the candidate index
         // (aln_heavy_kernel: `hashed` needs !indexed)
-        if (!aln_cand_on()) HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+        if (!aln_cand_on()) HIP_TRY(H.ht.grow((size_t)g->n_cu * P.walk_wpc * smem::ALN_HT));
         HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.ht = H.ht.p, P.rnext = H.rnext.p;
         if (aln_cand_on()) {
@@ -2050,7 +2072,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.pre_short.grow(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(H.short_ok.grow(std::max<uint64_t>(n_chains, 1)));
         HIP_TRY(H.span.grow(2 * std::max<uint64_t>(n_chains, 1)));
-        HIP_TRY(H.ht.grow((size_t)g->n_cu * smem::ALN_WALK_WAVES * smem::ALN_HT));
+        HIP_TRY(H.ht.grow((size_t)g->n_cu * P.walk_wpc * smem::ALN_HT));
         HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.hoff = H.hoff.p, P.pre = H.pre.p, P.loc = H.loc.p, P.pre_ok = H.pre_ok.p, P.pre_short = H.pre_short.p;
         P.short_ok = H.short_ok.p, P.span = H.span.p, P.ht = H.ht.p, P.rnext = H.rnext.p;
