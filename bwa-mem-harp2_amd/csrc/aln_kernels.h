@@ -32,11 +32,15 @@ struct RegTask {
 // the lane path's queue words (AlnParams::lq)
 constexpr int LQ_NTASK = 0;     // tasks listed
 constexpr int LQ_NSW = 1;       // heavy chains listed for mem_chain2aln_short's SW
-constexpr int LQ_BOUNDS = 8;    // [10] queue q = order[bounds[q] .. bounds[q + 1]): pass lengths 16q + 1 .. 16q + 16
-constexpr int LQ_HEADS = 24;    // [8] claim counters
-constexpr int LQ_HIST = 32;     // [130] tasks per pass length (0..128, longer), then cursors
+constexpr int LQ_QUEUES = 9;    // 16-column queues: pass lengths 1 .. 144 (LQ_MAXQ)
+constexpr int LQ_MAXQ = 16 * LQ_QUEUES;
+constexpr int LQ_BOUNDS = 8;    // [LQ_QUEUES + 1] queue q = order[bounds[q] .. bounds[q + 1]): lengths 16q + 1 .. 16q + 16
+constexpr int LQ_HEADS = 24;    // [LQ_QUEUES] claim counters
+constexpr int LQ_HIST = 40;     // [LQ_BUCKETS] tasks per pass length (0..LQ_MAXQ, longer), then cursors
+constexpr int LQ_BUCKETS = LQ_MAXQ + 2;
 constexpr int LQ_WORDS = 192;
-constexpr int LQ_BUCKETS = 130;
+static_assert(LQ_BOUNDS + LQ_QUEUES + 1 <= LQ_HEADS && LQ_HEADS + LQ_QUEUES <= LQ_HIST &&
+              LQ_HIST + LQ_BUCKETS <= LQ_WORDS, "lane queue words");
 
 struct AlnParams {
     // reads (nt4 codes, 4 = N) and the chains smem_batch_chain wrote
@@ -93,7 +97,7 @@ struct AlnParams {
     uint32_t lane_on;
     RegTask* tasks;           // [n_seeds + n_chains]
     uint32_t* torder;         // [n_seeds + n_chains] the tasks in pass order (by the pass's query length)
-    uint8_t* tfail;           // [n_seeds + n_chains] 1: left to the walk (query past 128 columns, or scores past 16 bits)
+    uint8_t* tfail;           // [n_seeds + n_chains] 1: left to the walk (query past LQ_MAXQ columns, or scores past 16 bits)
     uint8_t* sdec;            // [n_chains] light chains: 1 when mem_chain2aln_short declines before its SW
     uint32_t* lq;             // [LQ_WORDS] the lane path's counters, queue bounds and histogram
     uint32_t* chain_read;     // [n_chains] the read of each chain, bit 31: a heavy read

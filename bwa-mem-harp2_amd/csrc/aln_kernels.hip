@@ -1334,7 +1334,7 @@ __global__ __launch_bounds__(256) void aln_heavy_sw_kernel(AlnParams P) {
 }
 
 // the query length of task t's extension in pass `side` (0 left, 1 right);
-// LQ_BUCKETS - 1: not run by the lanes (longer than 128, or failed before)
+// LQ_BUCKETS - 1: not run by the lanes (longer than LQ_MAXQ, or failed before)
 __device__ __forceinline__ int task_key(const AlnParams& P, uint32_t t, int side) {
     const RegTask T = P.tasks[t];
     const SeedRec s = P.seeds[P.chains[T.c].seed_off + T.si];
@@ -1345,7 +1345,7 @@ __device__ __forceinline__ int task_key(const AlnParams& P, uint32_t t, int side
         if (P.tfail[t]) return LQ_BUCKETS - 1;
         q = (int)(P.offs[T.r + 1] - P.offs[T.r]) - s.qbeg - s.len;
     }
-    return q <= 128 ? q : LQ_BUCKETS - 1;
+    return q <= LQ_MAXQ ? q : LQ_BUCKETS - 1;
 }
 
 // counting sort of the tasks by the pass's query length: block histograms in
@@ -1375,12 +1375,12 @@ __global__ __launch_bounds__(64) void aln_task_scan_kernel(AlnParams P) {
     }
     for (int k = 0; k < LQ_BUCKETS; ++k) P.lq[LQ_HIST + k] = c[k];
     P.lq[LQ_BOUNDS] = 0;
-    for (int q = 1; q <= 8; ++q) P.lq[LQ_BOUNDS + q] = c[16 * q + 1];
-    for (int q = 0; q < 8; ++q) P.lq[LQ_HEADS + q] = 0;
+    for (int q = 1; q <= LQ_QUEUES; ++q) P.lq[LQ_BOUNDS + q] = c[16 * q + 1];
+    for (int q = 0; q < LQ_QUEUES; ++q) P.lq[LQ_HEADS + q] = 0;
 }
 
 // the tasks in pass order (a block reserves its share of each length with one
-// global add); tasks past 128 columns are marked failed (left to the walk)
+// global add); tasks past LQ_MAXQ columns are marked failed (left to the walk)
 __global__ __launch_bounds__(256) void aln_task_scatter_kernel(AlnParams P, int side) {
     __shared__ uint32_t h[LQ_BUCKETS], base[LQ_BUCKETS];
     const uint32_t n = P.lq[LQ_NTASK];
@@ -1486,7 +1486,10 @@ struct RegionPol {
 };
 
 // KCOL-column lane engine over the pass's queues of query lengths up to KCOL
-// (32: queues 0-1, 64: 2-3, 128: 4-7)
+// (32: queues 0-1, 64: 2-3, 144: 4-8).  The top tier is 144 columns, not 128:
+// a 150-bp read's seeds near its ends make extensions of 129-131 columns (2.8 %
+// of the human-like profile's tasks), which one wave each took 6.2 ms of the
+// heavy reads' critical path (profiles/r06/aln/s6d_human_kernel_stats.csv).
 template <int KCOL>
 __global__ __launch_bounds__(256, KCOL > 64 ? 2 : 4) void aln_region_lane_kernel(AlnParams P, int side) {
     __shared__ uint32_t stab[10];
@@ -1494,11 +1497,12 @@ __global__ __launch_bounds__(256, KCOL > 64 ? 2 : 4) void aln_region_lane_kernel
     if (threadIdx.x < 5) kswl::row_scores(P.mat, threadIdx.x, stab[2 * threadIdx.x], stab[2 * threadIdx.x + 1]);
     __syncthreads();
     RegionPol pol{&P, side, P.top};
-    kswl::lane_engine<KCOL, 8>(pol, P.lq + LQ_BOUNDS, P.lq + LQ_HEADS, KCOL == 32 ? 0 : KCOL / 32, KCOL / 16, stab,
+    kswl::lane_engine<KCOL, 8>(pol, P.lq + LQ_BOUNDS, P.lq + LQ_HEADS, KCOL == 32 ? 0 : KCOL == 64 ? 2 : 4,
+                               KCOL == 32 ? 2 : KCOL == 64 ? 4 : LQ_QUEUES, stab,
                                qsl[threadIdx.x >> 6], P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
 }
 
-// the tasks the lanes left (a query past 128 columns, scores past 16 bits):
+// the tasks the lanes left (a query past LQ_MAXQ columns, scores past 16 bits):
 // the whole region one wave per task, as the heavy chain tasks did (left to
 // the walks, they made the human-like profile's heavy walk 4x slower)
 template <int KC>
@@ -1697,7 +1701,7 @@ extern "C" hipError_t smem_launch_aln_passes(const smem::AlnParams* P, int n_cu,
         hipLaunchKernelGGL(smem::aln_task_scatter_kernel, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<32>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<64>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
-        hipLaunchKernelGGL(smem::aln_region_lane_kernel<128>, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_region_lane_kernel<smem::LQ_MAXQ>, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
     }
     hipLaunchKernelGGL(smem::aln_region_cov_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
     hipLaunchKernelGGL(smem::aln_region_rest_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
