@@ -16,7 +16,9 @@
 // mode 5: mode 4 plus argv[8] lane-private cache-hit loads per round;
 // mode 6: the Occ64 fetch, 2 random 32-B buckets per lane (2 x 16-B chunks each);
 // mode 7: k-mer interval table probes, 2 random 16-B entries per lane (64-bit
-//         indices: tables past 64 GB).
+//         indices: tables past 64 GB);
+// mode 8: argv[6] random 32-B buckets per lane per round into registers, no LDS
+//         (gather_regs, below: the occupancy asked for is the occupancy run).
 // Every round waits for its data (vmcnt(0)) before the next, like the
 // kernel; addresses are independent so only bandwidth/queueing limit it.
 #include <hip/hip_runtime.h>
@@ -154,6 +156,31 @@ __global__ __launch_bounds__(256) void gather(const uint4* __restrict__ tab, uin
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// mode 8 (round 6): NB random 32-B buckets per lane per round (argv[6], 1..16) into
+// registers (2 x global_load_dwordx4 each), no LDS: the other modes' 64-KB LDS image
+// allowed at most 2 blocks (8 waves) per CU whatever waves_per_cu asked for, so
+// their "12 waves/CU" ceiling ran at 8.  This one runs the asked occupancy and
+// the asked memory-level parallelism (waves x lanes x NB outstanding buckets).
+template <int NB>
+__global__ __launch_bounds__(256) void gather_regs(const uint4* __restrict__ tab, uint64_t n_buckets, int iters,
+                                                   uint32_t* __restrict__ sink) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t seed = (blockIdx.x * 4 + w) * 0x9E3779B9u + lane * 0x85EBCA6Bu;
+    uint32_t acc = 0;
+    for (int it = 0; it < iters; ++it) {
+        uint4 a[2 * NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint32_t bk = mix(seed + it * NB + b) % n_buckets;
+            a[2 * b] = tab[(uint64_t)bk * 2];
+            a[2 * b + 1] = tab[(uint64_t)bk * 2 + 1];
+        }
+#pragma unroll
+        for (int b = 0; b < 2 * NB; ++b) acc ^= a[b].x ^ a[b].w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const size_t mb = argc > 1 ? atol(argv[1]) : 1000;
     const int wpc = argc > 2 ? atoi(argv[2]) : 12;
@@ -171,13 +198,13 @@ int main(int argc, char** argv) {
         CHECK(hipMalloc(&tab, bytes));
     CHECK(hipMalloc(&sink, 4));
     CHECK(hipMemset(tab, 1, bytes));
-    const int bsz = mode == 7 ? 16 : (mode == 2 || mode == 6) ? 32 : 64;
+    const int bsz = mode == 7 ? 16 : (mode == 2 || mode == 6 || mode == 8) ? 32 : 64;
     // argv[5]: restrict the addresses to the first N buckets (e.g. 256 = L1-resident)
     uint64_t n_buckets = bytes / bsz;
     if (mode != 7 && n_buckets > 0xffffffffull) n_buckets = 0xffffffffull;
     if (argc > 5 && atol(argv[5]) > 0 && (uint64_t)atol(argv[5]) < n_buckets) n_buckets = (uint64_t)atol(argv[5]);
     const int grid = prop.multiProcessorCount * wpc / 4;
-    int active = argc > 6 ? atoi(argv[6]) : 64;  // mode 4: lanes that fetch
+    int active = argc > 6 ? atoi(argv[6]) : (mode == 8 ? 2 : 64);  // mode 4: lanes that fetch; mode 8: buckets per lane
     if (active < 1 || active > 64) active = 64;
     const int extra = argc > 8 ? atoi(argv[8]) : 0;  // mode 5: extra lane-private loads per round
     hipEvent_t e0, e1;
@@ -193,11 +220,22 @@ int main(int argc, char** argv) {
         if (mode == 5) hipLaunchKernelGGL(gather<5>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
         if (mode == 6) hipLaunchKernelGGL(gather<6>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
         if (mode == 7) hipLaunchKernelGGL(gather<7>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink, active, extra);
+        if (mode == 8) {
+            switch (active) {
+                case 1: hipLaunchKernelGGL(gather_regs<1>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink); break;
+                case 2: hipLaunchKernelGGL(gather_regs<2>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink); break;
+                case 4: hipLaunchKernelGGL(gather_regs<4>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink); break;
+                case 8: hipLaunchKernelGGL(gather_regs<8>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink); break;
+                default: hipLaunchKernelGGL(gather_regs<16>, dim3(grid), dim3(256), 0, 0, tab, n_buckets, iters, sink); break;
+            }
+        }
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
-        const double nbk = (double)grid * 4 * iters * ((mode == 4 || mode == 6 || mode == 7) ? 2 * active : 128);  // buckets fetched
+        const double nbk = (double)grid * 4 * iters *
+                           (mode == 8 ? 64.0 * (active == 1 || active == 2 || active == 4 || active == 8 ? active : 16)
+                                      : (mode == 4 || mode == 6 || mode == 7) ? 2 * active : 128);  // buckets fetched
         printf("{\"table_MB\": %zu, \"waves_per_cu\": %d, \"mode\": %d, \"bucket_B\": %d, \"ms\": %.3f, "
                "\"Gbuckets_per_s\": %.2f, \"TB_per_s\": %.3f, \"active\": %d, \"us_per_round\": %.3f}\n",
                mb, wpc, mode, bsz, ms, nbk / ms * 1e-6, nbk * bsz / ms * 1e-9, active, ms * 1e3 / iters);
