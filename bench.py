@@ -81,10 +81,13 @@ CONFIGS = {
     "c3": dict(read_len=150, sub=0.02, k=19, pairs=True, stream_reads=25_000_000,
                what="C3 on one GPU: its shard of 100M x 150 bp PE on 8 GPUs = 12.5M pairs, insert N(500, 50), "
                     "mates interleaved in one chunk"),
-    "c4": dict(read_len=250, sub=0.02, k=19, pairs=False, stream_reads=10_000_000,
-               what="C4: 10M x 250 bp, min-seed-len 19 with re-seeding"),
-    "c5": dict(read_len=150, sub=0.05, k=19, pairs=False, stream_reads=10_000_000,
-               what="C5: 10M x 150 bp at 5 % substitutions"),
+    # c4 / c5 stream in 1M-read chunks with 4 workers: their reads carry ~1.7x the intervals of
+    # c2's, and 2M-read chunks (1.7 GB of pinned results each) fetched at 10-15 GB/s instead of
+    # 30 (profiles/r06/stream/stream_c5.jsonl: 15.8 -> 32.5 M reads/s)
+    "c4": dict(read_len=250, sub=0.02, k=19, pairs=False, stream_reads=10_000_000, stream_chunk=1 << 20,
+               stream_workers=4, what="C4: 10M x 250 bp, min-seed-len 19 with re-seeding"),
+    "c5": dict(read_len=150, sub=0.05, k=19, pairs=False, stream_reads=10_000_000, stream_chunk=1 << 20,
+               stream_workers=4, what="C5: 10M x 150 bp at 5 % substitutions"),
 }
 
 
@@ -115,9 +118,10 @@ def parse(argv=None):
     p.add_argument("--stream-reads", type=int, default=None,
                    help="reads per GPU pushed through the streaming path (default: the config's; 0: the resident "
                         "reads; -1: no streaming leg)")
-    p.add_argument("--stream-chunk", type=int, default=1 << 21,
-                   help="reads per streamed chunk (2M: 0.93 of the resident rate vs 0.86-0.88 at 1M, profiles/r04/stream)")
-    p.add_argument("--stream-workers", type=int, default=3)
+    p.add_argument("--stream-chunk", type=int, default=None,
+                   help="reads per streamed chunk (default: the config's; c2 / c3 2M: 0.93 of the resident rate vs "
+                        "0.86-0.88 at 1M, profiles/r04/stream; c4 / c5 1M)")
+    p.add_argument("--stream-workers", type=int, default=None, help="streaming workers (default: the config's, 3 or 4)")
     p.add_argument("--stream-packed", type=int, default=1, help="1: 16-B wire entries (SMEM_STREAM_PACKED)")
     p.add_argument("--stream-passes", type=int, default=3, help="timed streaming passes; the median is reported")
     p.add_argument("--side-stages", type=int, default=1, help="0: skip the sa / chain / sw side reports")
@@ -150,6 +154,10 @@ def parse(argv=None):
     a.pairs = cfg["pairs"]
     if a.stream_reads is None:
         a.stream_reads = cfg["stream_reads"]
+    if a.stream_chunk is None:
+        a.stream_chunk = cfg.get("stream_chunk", 1 << 21)
+    if a.stream_workers is None:
+        a.stream_workers = cfg.get("stream_workers", 3)
     if a.traffic_json is None:
         a.traffic_json = traffic_path(a.genome_profile)
     return a
