@@ -77,9 +77,15 @@ struct AlnParams {
     uint32_t light_claims;    // aln_kernel: work-queue claims per wave before it exits (0: until the queue is empty)
     uint32_t walk_guard;      // != 0: the inlined walk, at most this many loop iterations per read (ctr[15] counts trips)
     int32_t* heavy;           // [n_reads] heavy read ids (ctr[2] of them, any order)
-    const uint32_t* horder;   // [n_heavy] the walk's claim order over heavy[] (most seeds + chains first), or
-                              // nullptr: heavy[] order (smem_launch_aln_heavy_order)
     uint32_t walk_wpc;        // the walk's waves per CU (aln_heavy_kernel grid; 0: ALN_WALK_WAVES)
+    uint32_t walk_waves;      // != 0: the walk's grid in waves (the giant reads' walk: one wave each)
+    // The giant split (smem_launch_aln_heavy_split): the heaviest heavy reads (rgiant[r] = 1;
+    // chain_read bit 30) get their own task list and candidate index, and their passes and walk
+    // run on a stream of their own from the start -- a tandem-repeat read's walk, ~20 ms on one
+    // wave, then overlaps the other heavy and light reads' passes instead of ending the stage.
+    const uint8_t* rgiant;    // [n_reads] 1: a giant read (nullptr: no split)
+    RegTask* gtasks;          // [n_seeds] the giant reads' chain tasks (glq[LQ_NTASK] of them)
+    uint32_t* glq;            // [LQ_WORDS] their lane queues (as lq)
     uint64_t* hcnt;           // [n_reads] their chain counts, then
     uint64_t* hoff;           // [n_heavy + 1] prefix: chain task t of the heavy reads
     uint64_t* hscnt;          // [n_reads] their seed counts
@@ -169,9 +175,12 @@ hipError_t smem_launch_aln_write(const smem::AlnParams* P, hipStream_t st);
 hipError_t smem_launch_aln_classify(const smem::AlnParams* P, hipStream_t st);
 // parts: 1 the chain tasks, 2 the walk, 3 both
 hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, int long_reads, int parts, hipStream_t st);
-// the heavy walk's claim order (P->horder, n_heavy entries): reads by log2 of their seeds + chains,
-// most first, so that no long read starts last (the walk's tail)
-hipError_t smem_launch_aln_heavy_order(const smem::AlnParams* P, uint32_t n_heavy, uint32_t* horder, hipStream_t st);
+// the giant split: P->heavy / hcnt / hscnt (n_heavy of them) copied into heavy2 / hcnt2 / hscnt2
+// in the same bucket order (seeds + chains, most first); the first n_giant of them marked in
+// rgiant (cleared for every read first); ctr_g[2] = n_giant, ctr_r[2] = n_heavy - n_giant
+hipError_t smem_launch_aln_heavy_split(const smem::AlnParams* P, uint32_t n_heavy, uint32_t n_giant, int32_t* heavy2,
+                                       uint64_t* hcnt2, uint64_t* hscnt2, uint8_t* rgiant, uint32_t* ctr_g,
+                                       uint32_t* ctr_r, hipStream_t st);
 // the candidate index: slot counts per heavy read (hcnt + hscnt) into cnt[n_heavy];
 // then (C.off scanned, C.m slots) fill, sort, place and every heavy seed's range;
 // tmp / tmp_bytes: the sort's scratch (tmp nullptr: *tmp_bytes is set, nothing runs)

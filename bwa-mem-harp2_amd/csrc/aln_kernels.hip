@@ -1048,7 +1048,7 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
         if ((threadIdx.x & 63) == 0) h = atomicAdd(&P.ctr[KC > 4 ? 13 : 3], 1u);
         h = (uint32_t)uni((int)h);
         if (h >= nh) break;
-        const int r = uni(P.heavy[P.horder ? P.horder[h] : h]);
+        const int r = uni(P.heavy[h]);
         if ((uni((int)(P.offs[r + 1] - P.offs[r])) > 256) == (KC > 4)) {
             if constexpr (INL) heavy_read_walk_body<KC, true>(P, r);
             else heavy_read_walk<KC>(P, r);
@@ -1057,18 +1057,20 @@ __global__ __launch_bounds__(256) void aln_heavy_kernel(AlnParams P) {
 }
 
 
-// The walk's claim order: a counting sort of the heavy reads by the bit length
-// of their seeds + chains, longest first (one block; the reads of a bucket in
-// any order -- each read's walk is independent of the others').  A read of
-// thousands of seeds claimed late was the walk's tail.
-__global__ __launch_bounds__(1024) void aln_heavy_order_kernel(AlnParams P, uint32_t nh, uint32_t* horder) {
+// The giant split: the heavy list copied in the same bucket order (seeds +
+// chains, most first), its first n_giant reads marked giant.  (One block; the
+// reads of a bucket in any order.)
+__global__ __launch_bounds__(1024) void aln_heavy_split_kernel(AlnParams P, uint32_t nh, uint32_t ng, int32_t* heavy2,
+                                                               uint64_t* hcnt2, uint64_t* hscnt2, uint8_t* rgiant,
+                                                               uint32_t* ctr_g, uint32_t* ctr_r) {
     __shared__ uint32_t cnt[64];
     const uint32_t t = threadIdx.x;
     if (t < 64) cnt[t] = 0;
+    for (int r = (int)t; r < P.n_reads; r += (int)blockDim.x) rgiant[r] = 0;
     __syncthreads();
     auto bucket = [&](uint32_t h) -> uint32_t {
         const uint64_t w = P.hcnt[h] + P.hscnt[h];
-        return 63u - (uint32_t)__builtin_clzll(w | 1ull);  // 0..63; the larger first below
+        return 63u - (uint32_t)__builtin_clzll(w | 1ull);
     };
     for (uint32_t h = t; h < nh; h += blockDim.x) atomicAdd(&cnt[bucket(h)], 1u);
     __syncthreads();
@@ -1079,9 +1081,18 @@ __global__ __launch_bounds__(1024) void aln_heavy_order_kernel(AlnParams P, uint
             cnt[b] = o;
             o += c;
         }
+        ctr_g[2] = ng;
+        ctr_r[2] = nh - ng;
     }
     __syncthreads();
-    for (uint32_t h = t; h < nh; h += blockDim.x) horder[atomicAdd(&cnt[bucket(h)], 1u)] = h;
+    for (uint32_t h = t; h < nh; h += blockDim.x) {
+        const uint32_t pos = atomicAdd(&cnt[bucket(h)], 1u);
+        const int32_t r = P.heavy[h];
+        heavy2[pos] = r;
+        hcnt2[pos] = P.hcnt[h];
+        hscnt2[pos] = P.hscnt[h];
+        if (pos < ng) rgiant[r] = 1;
+    }
 }
 
 // ---- the heavy walk's candidate index (AlnParams::cand_*) ----
@@ -1110,8 +1121,9 @@ __global__ __launch_bounds__(256) void aln_cand_fill_kernel(AlnParams P, CandPar
          c += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t cr = P.chain_read[c];
         if (!(cr & 0x80000000u)) continue;
-        const int r = (int)(cr & 0x7FFFFFFFu);
+        const int r = (int)(cr & 0x3FFFFFFFu);
         const uint32_t h = C.hord[r];
+        if (h == 0xFFFFFFFFu) continue;  // a heavy read of the other instance (giant split)
         const uint64_t base = C.off[h], s0 = P.seed_off[r], ns = P.seed_off[r + 1] - s0;
         const uint64_t c0 = P.chain_off[r];
         const uint64_t hk = 0;  // the segments are the reads' slots: keys are rb alone
@@ -1233,7 +1245,7 @@ __global__ __launch_bounds__(256) void aln_chain_read_kernel(AlnParams P) {
         const uint64_t c0 = P.chain_off[r], c1 = P.chain_off[r + 1];
         const bool heavy =
             P.heavy_min && (c1 - c0 >= P.heavy_min || P.seed_off[r + 1] - P.seed_off[r] >= P.heavy_seeds);
-        const uint32_t v = (uint32_t)r | (heavy ? 0x80000000u : 0u);
+        const uint32_t v = (uint32_t)r | (heavy ? 0x80000000u : 0u) | (heavy && P.rgiant && P.rgiant[r] ? 0x40000000u : 0u);
         for (uint64_t c = c0; c < c1; ++c) P.chain_read[c] = v;
     }
 }
@@ -1252,7 +1264,8 @@ __global__ __launch_bounds__(256) void aln_chain_prep_kernel(AlnParams P, uint32
     const int64_t l2 = P.l_pac << 1;
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n_chains; c += gridDim.x * blockDim.x) {
         const uint32_t rv = P.chain_read[c];
-        const uint32_t r = rv & 0x7fffffffu;
+        const uint32_t r = rv & 0x3fffffffu;
+        const bool giant = (rv >> 30 & 1u) != 0;
         const bool heavy = (rv >> 31) != 0;
         const OutChain ch = P.chains[c];
         P.sdec[c] = 0;
@@ -1300,8 +1313,17 @@ __global__ __launch_bounds__(256) void aln_chain_prep_kernel(AlnParams P, uint32
         if (!heavy) {
             if (decline) P.tasks[atomicAdd(&P.lq[LQ_NTASK], 1u)] = RegTask{c, r, (uint32_t)top};
         } else if (decline) {
-            const uint32_t base = atomicAdd(&P.hlq[LQ_NTASK], (uint32_t)ch.n);
-            for (int i = 0; i < ch.n; ++i) P.htasks[base + i] = RegTask{c, r, (uint32_t)i};
+            // one atomic per list at a uniform address (the compiler's atomic optimizer
+            // folds a wave's into one; at a per-lane selected address it cannot:
+            // 37 ms instead of 0.9 for the human-like profile's 3.2 M heavy chains)
+            RegTask* const tl = giant ? P.gtasks : P.htasks;
+            const uint32_t n = (uint32_t)ch.n;
+            uint32_t base = atomicAdd(&P.hlq[LQ_NTASK], giant ? 0u : n);
+            if (P.glq) {
+                const uint32_t bg = atomicAdd(&P.glq[LQ_NTASK], giant ? n : 0u);
+                base = giant ? bg : base;
+            }
+            for (int i = 0; i < ch.n; ++i) tl[base + i] = RegTask{c, r, (uint32_t)i};
         } else {
             P.swlist[atomicAdd(&P.hlq[LQ_NSW], 1u)] = c;
         }
@@ -1316,7 +1338,9 @@ __global__ __launch_bounds__(256) void aln_heavy_sw_kernel(AlnParams P) {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t k = wave; k < n; k += n_waves) {
         const uint32_t c = (uint32_t)uni((int)P.swlist[k]);
-        const uint32_t r = (uint32_t)uni((int)(P.chain_read[c] & 0x7fffffffu));
+        const uint32_t rv = (uint32_t)uni((int)P.chain_read[c]);
+        const uint32_t r = rv & 0x3fffffffu;
+        const bool giant = (rv >> 30 & 1u) != 0;
         const uint64_t q0 = P.offs[r];
         const int L = uni((int)(P.offs[r + 1] - q0));
         OutChain ch = P.chains[c];
@@ -1325,10 +1349,11 @@ __global__ __launch_bounds__(256) void aln_heavy_sw_kernel(AlnParams P) {
         const int ok = chain_short(P, P.codes + q0, L, S, ch.n, P.pre_short + c, lane, P.ctr + 12) == 0;
         if (lane == 0) P.short_ok[c] = (uint8_t)ok;
         if (!ok) {
+            RegTask* const tl = giant ? P.gtasks : P.htasks;
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&P.hlq[LQ_NTASK], (uint32_t)ch.n);
+            if (lane == 0) base = atomicAdd(&(giant ? P.glq : P.hlq)[LQ_NTASK], (uint32_t)ch.n);
             base = (uint32_t)uni((int)base);
-            for (int i = lane; i < ch.n; i += 64) P.htasks[base + i] = RegTask{c, r, (uint32_t)i};
+            for (int i = lane; i < ch.n; i += 64) tl[base + i] = RegTask{c, r, (uint32_t)i};
         }
     }
 }
@@ -1641,7 +1666,8 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
     if (!(parts & 2)) return hipGetLastError();
     // the walk kernels use the per-wave hash tables in turn (same stream);
     // walk_guard != 0: the inlined, guarded walk (diagnostic)
-    const int wb = n_cu * (int)(P->walk_wpc ? P->walk_wpc : smem::ALN_WALK_WAVES) / 4;  // blocks of 4 waves
+    const int wb = P->walk_waves ? (int)(P->walk_waves + 3) / 4  // blocks of 4 waves
+                                 : n_cu * (int)(P->walk_wpc ? P->walk_wpc : smem::ALN_WALK_WAVES) / 4;
     if (P->walk_guard) {
         hipLaunchKernelGGL((smem::aln_heavy_kernel<4, true>), dim3(wb), dim3(256), 0, st, *P);
         if (long_reads) hipLaunchKernelGGL((smem::aln_heavy_kernel<16, true>), dim3(wb), dim3(256), 0, st, *P);
@@ -1652,10 +1678,11 @@ extern "C" hipError_t smem_launch_aln_heavy(const smem::AlnParams* P, int n_cu, 
     return hipGetLastError();
 }
 
-extern "C" hipError_t smem_launch_aln_heavy_order(const smem::AlnParams* P, uint32_t n_heavy, uint32_t* horder,
-                                                  hipStream_t st) {
-    if (!n_heavy) return hipSuccess;
-    hipLaunchKernelGGL(smem::aln_heavy_order_kernel, dim3(1), dim3(1024), 0, st, *P, n_heavy, horder);
+extern "C" hipError_t smem_launch_aln_heavy_split(const smem::AlnParams* P, uint32_t n_heavy, uint32_t n_giant,
+                                                  int32_t* heavy2, uint64_t* hcnt2, uint64_t* hscnt2, uint8_t* rgiant,
+                                                  uint32_t* ctr_g, uint32_t* ctr_r, hipStream_t st) {
+    hipLaunchKernelGGL(smem::aln_heavy_split_kernel, dim3(1), dim3(1024), 0, st, *P, n_heavy, n_giant, heavy2, hcnt2,
+                       hscnt2, rgiant, ctr_g, ctr_r);
     return hipGetLastError();
 }
 

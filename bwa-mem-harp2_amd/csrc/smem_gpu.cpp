@@ -10,6 +10,11 @@
 //     device buffers, so concurrent kt_for_batch workers never wait on a
 //     manager and never get rejected.
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -310,13 +315,15 @@ struct smem_gpu {
     // software/fastmap.c:320-429, which let one worker batch at a time onto
     // the FPGA and turned the others away): every entry point that runs work
     // on the device leases one of at most max_active stream pairs (a normal
-    // and a low-priority stream) for the duration of the call; more
+    // and a low-priority stream, plus a third normal one for chains -> regions'
+    // giant reads, smem_batch_chain2aln) for the duration of the call; more
     // concurrent calls wait for a pair.  So a device never carries more than
-    // 2 x max_active streams, however many kt_for_batch workers share it.
+    // 3 x max_active streams, however many kt_for_batch workers share it.
     int max_active = 8;
     std::mutex adm_mu;
     std::condition_variable adm_cv;
     std::vector<std::pair<hipStream_t, hipStream_t>> pairs;
+    std::vector<hipStream_t> thirds;  // pairs[k]'s third stream
     std::vector<int> free_pairs;
     int n_leased = 0;
     // a HIP runtime failure seen by any call: every later call fails at once
@@ -353,9 +360,15 @@ static void gpu_wait(smem_gpu_t* g) {
 
 // scratch of the heavy-read path of chains -> regions
 struct AlnHeavyBufs {
-    DevBuf<int32_t> heavy;
-    DevBuf<uint32_t> horder;
-    DevBuf<uint64_t> hcnt, hoff, hscnt;
+    DevBuf<int32_t> heavy, heavy2;
+    DevBuf<uint64_t> hcnt, hoff, hscnt, hcnt2, hscnt2;
+    // the giant split: read flags, the giants' walk counters, task list and lane queues, their
+    // candidate index's segments
+    DevBuf<uint8_t> rgiant, gtfail;
+    DevBuf<uint32_t> gctr, gtorder, glq, chord_g;
+    DevBuf<smem::RegTask> gtasks;
+    DevBuf<uint64_t> ccnt_g, coff_g;
+    DevBuf<uint8_t> ctmp_g;
     DevBuf<int64_t> span;
     DevBuf<uint64_t> ht;
     DevBuf<int32_t> rnext;
@@ -375,7 +388,8 @@ struct AlnHeavyBufs {
     template <class F>
     void each(F&& f) {
         f(ckey); f(ckey2); f(coff); f(ccnt); f(cval); f(cval2); f(cq); f(cpos_s); f(cpos_c); f(chord); f(chmax);
-        f(crb); f(cre); f(cmade); f(ctmp); f(crng); f(heavy); f(horder); f(hcnt); f(hoff); f(hscnt); f(span); f(ht); f(rnext);
+        f(crb); f(cre); f(cmade); f(ctmp); f(crng); f(heavy); f(heavy2); f(hcnt2); f(hscnt2); f(rgiant); f(gtfail);
+        f(gctr); f(gtorder); f(glq); f(chord_g); f(gtasks); f(ccnt_g); f(coff_g); f(ctmp_g); f(hcnt); f(hoff); f(hscnt); f(span); f(ht); f(rnext);
         f(pre); f(pre_short); f(loc); f(short_ok); f(pre_ok); f(tmp); f(tasks); f(torder); f(lq); f(tfail); f(sdec);
         f(chain_read); f(swlist); f(htasks); f(htorder); f(hlq); f(htfail);
     }
@@ -394,7 +408,8 @@ struct smem_batch {
     // reads' kernels on st, joined by ev_join (created on first use)
     // (chaining: the heavy reads' second tier on st2, forked by ev_fork)
     hipStream_t st2 = nullptr;
-    hipEvent_t ev_join = nullptr, ev_fork = nullptr;
+    hipStream_t st3 = nullptr;  // chains -> regions: the giant reads' passes and walk (ev_giant joins them)
+    hipEvent_t ev_join = nullptr, ev_fork = nullptr, ev_giant = nullptr;
     int max_reads = 0, max_len = 0;
     uint64_t max_bases = 0;
     uint32_t cap_intv = 0, cap_calls = 0, cap_list = 0;
@@ -504,7 +519,7 @@ static int gpu_check(smem_gpu_t* g) {
 struct DeviceCall {
     smem_gpu_t* g;
     int pair = -1;
-    hipStream_t st = nullptr, st2 = nullptr;
+    hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;
     int rc = SMEM_OK;
     explicit DeviceCall(smem_gpu_t* g_) : g(g_) {
         g_err[0] = 0;
@@ -530,28 +545,33 @@ struct DeviceCall {
             pair = g->free_pairs.back();
             g->free_pairs.pop_back();
         } else {
-            hipStream_t a = nullptr, b = nullptr;
+            hipStream_t a = nullptr, b = nullptr, c = nullptr;
             int least = 0, greatest = 0;
             e = hipStreamCreateWithFlags(&a, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
             if (e == hipSuccess) e = hipStreamCreateWithPriority(&b, hipStreamNonBlocking, least);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking);
             if (e != hipSuccess) {
                 if (a) (void)hipStreamDestroy(a);
+                if (b) (void)hipStreamDestroy(b);
                 rc = fail(SMEM_E_DEVICE, "admission: hipStreamCreate", e);
                 g->adm_cv.notify_one();
                 return;
             }
             g->pairs.emplace_back(a, b);
+            g->thirds.push_back(c);
             pair = (int)g->pairs.size() - 1;
         }
         ++g->n_leased;
         st = g->pairs[(size_t)pair].first;
         st2 = g->pairs[(size_t)pair].second;
+        st3 = g->thirds[(size_t)pair];
     }
     DeviceCall(const DeviceCall&) = delete;
     DeviceCall& operator=(const DeviceCall&) = delete;
     ~DeviceCall() {
         if (pair >= 0) {
+            (void)hipStreamSynchronize(st3);
             (void)hipStreamSynchronize(st2);
             (void)hipStreamSynchronize(st);
             std::lock_guard<std::mutex> lk(g->adm_mu);
@@ -570,9 +590,9 @@ struct DeviceCall {
 struct BatchCall : DeviceCall {
     smem_batch_t* b;
     explicit BatchCall(smem_batch_t* b_) : DeviceCall(b_->g), b(b_) {
-        if (rc == SMEM_OK) b->st = st, b->st2 = st2;
+        if (rc == SMEM_OK) b->st = st, b->st2 = st2, b->st3 = st3;
     }
-    ~BatchCall() { b->st = b->st2 = nullptr; }
+    ~BatchCall() { b->st = b->st2 = b->st3 = nullptr; }
 };
 
 extern "C" {
@@ -814,6 +834,7 @@ void smem_batch_destroy(smem_batch_t* b) {
         if (ev) (void)hipEventDestroy(ev);
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+    if (b->ev_giant) (void)hipEventDestroy(b->ev_giant);
     delete b;
 }
 
@@ -855,6 +876,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
         (void)hipStreamDestroy(p.first);
         (void)hipStreamDestroy(p.second);
     }
+    for (auto c : g->thirds) (void)hipStreamDestroy(c);
     if (g->sa_ready) (void)hipEventDestroy(g->sa_ready);
     if (g->init_st) (void)hipStreamDestroy(g->init_st);
     if (getenv("SMEM_GPU_TIMES"))
@@ -1899,16 +1921,19 @@ static bool aln_cand_on() {
     return !e || atoi(e) != 0;
 }
 // the heavy walk's waves per CU (SMEM_ALN_WALK_WAVES; aln_heavy_kernel takes 132 VGPRs: at most
-// 12) and its claim order (SMEM_ALN_WALK_ORDER=0: the classify kernel's order instead of the
-// reads with the most seeds + chains first)
+// 12; 4, 8 and 12 measured the same, profiles/r06/aln/s6e_walk_ab.log: the walk's end is its
+// longest reads, hence the giant split)
 static uint32_t aln_walk_wpc() {
     const char* e = getenv("SMEM_ALN_WALK_WAVES");
     const int v = e ? atoi(e) : smem::ALN_WALK_WAVES;
     return (uint32_t)std::max(4, std::min(16, v / 4 * 4));
 }
-static bool aln_walk_order() {
-    const char* e = getenv("SMEM_ALN_WALK_ORDER");
-    return !(e && atoi(e) == 0);
+// the giant split's reads (SMEM_ALN_GIANTS, default 128; 0: off): the heaviest heavy reads by
+// seeds + chains (a read of ~10k seeds walks ~10 ms on its wave; the human-like profile's 1M reads
+// hold dozens), their passes and walk on the batch's third stream from the start
+static uint32_t aln_giants() {
+    const char* e = getenv("SMEM_ALN_GIANTS");
+    return e ? (uint32_t)std::max(0, atoi(e)) : 128u;
 }
 // SMEM_ALN_LANE=0: no regions computed ahead one seed per lane (the walks
 // extend every seed one wave per problem, round-2 style)
@@ -1958,7 +1983,7 @@ static int aln_guard_check(const smem::AlnParams& P, hipStream_t st, uint64_t* h
 // pageable or stack memory: a copy must not outlive the call's frame)
 static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_t n_seeds, bool long_reads,
                    AlnHeavyBufs& H, uint64_t* hs, hipStream_t st, hipStream_t st2 = nullptr,
-                   hipEvent_t ev_join = nullptr) {
+                   hipEvent_t ev_join = nullptr, hipStream_t st3 = nullptr, hipEvent_t ev_giant = nullptr) {
     const int n = P.n_reads;
     P.heavy_min = aln_heavy_min();
     P.heavy_seeds = aln_heavy_seeds();
@@ -2011,13 +2036,32 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         n_heavy = (uint32_t)hs[0];
     }
     P.walk_wpc = aln_walk_wpc();
-    P.horder = nullptr;
-    if (n_heavy && aln_walk_order()) {
-        HIP_TRY(H.horder.grow(n_heavy));
-        HIP_TRY(smem_launch_aln_heavy_order(&P, n_heavy, H.horder.p, st));
-        P.horder = H.horder.p;
+    P.walk_waves = 0;
+    P.rgiant = nullptr, P.gtasks = nullptr, P.glq = nullptr;
+    // the giant split: heavy[] reordered (most seeds + chains first), its first n_giant reads the
+    // giants (lane path, candidate index, three streams)
+    const uint32_t n_giant = (P.lane_on && n_heavy && st2 && st3 && ev_join && ev_giant && aln_cand_on())
+                                 ? std::min<uint32_t>(n_heavy, aln_giants()) : 0u;
+    if (n_giant) {
+        const uint64_t nht = std::max<uint64_t>(n_seeds, 1);
+        HIP_TRY(H.heavy2.grow(n_heavy));
+        HIP_TRY(H.hcnt2.grow(n_heavy));
+        HIP_TRY(H.hscnt2.grow(n_heavy));
+        HIP_TRY(H.rgiant.grow(n));
+        HIP_TRY(H.gctr.grow(smem::ALN_CTRS));
+        HIP_TRY(H.gtasks.grow(nht));
+        HIP_TRY(H.gtorder.grow(nht));
+        HIP_TRY(H.gtfail.grow(nht));
+        HIP_TRY(H.glq.grow(smem::LQ_WORDS));
+        HIP_TRY(hipMemsetAsync(H.gctr.p, 0, sizeof(uint32_t) * smem::ALN_CTRS, st));
+        HIP_TRY(hipMemsetAsync(H.glq.p, 0, sizeof(uint32_t) * smem::LQ_WORDS, st));
+        HIP_TRY(smem_launch_aln_heavy_split(&P, n_heavy, n_giant, H.heavy2.p, H.hcnt2.p, H.hscnt2.p, H.rgiant.p,
+                                            H.gctr.p, P.ctr, st));
+        P.heavy = H.heavy2.p, P.hcnt = H.hcnt2.p, P.hscnt = H.hscnt2.p;
+        P.rgiant = H.rgiant.p, P.gtasks = H.gtasks.p, P.glq = H.glq.p;
     }
-    smem::CandParams C{};
+    smem::CandParams C{}, Cg{};
+    uint64_t m_giant = 0;  // the giants' candidate slots (first in the index arrays)
     if (n_heavy && P.lane_on) {  // the walk's scratch (its chains were prepared by the lane path)
         // the bin hash (0.54 GB at 256 CUs) only serves a walk without the candidate index
         // (aln_heavy_kernel: `hashed` needs !indexed)
@@ -2025,20 +2069,43 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         HIP_TRY(H.rnext.grow(std::max<uint64_t>(n_seeds, 1)));
         P.ht = H.ht.p, P.rnext = H.rnext.p;
         if (aln_cand_on()) {
-            // the candidate index's size: every heavy read's seeds and chains
-            HIP_TRY(H.ccnt.grow(n_heavy));
-            HIP_TRY(H.coff.grow(n_heavy + 1));
+            // the candidate index's size: every heavy read's seeds and chains, in two
+            // instances under the giant split -- the giants (heavy[0 .. n_giant)) and the
+            // rest (heavy[n_giant ..)), each with its read -> segment map (hord, the other
+            // instance's reads unmapped) and its slots (the giants' first)
+            const uint32_t nr = n_heavy - n_giant;
+            smem::AlnParams Pr = P;
+            Pr.heavy = P.heavy + n_giant, Pr.hcnt = P.hcnt + n_giant, Pr.hscnt = P.hscnt + n_giant;
+            HIP_TRY(H.ccnt.grow(std::max<uint32_t>(nr, 1)));
+            HIP_TRY(H.coff.grow(nr + 1));
             HIP_TRY(H.chord.grow(std::max(n, 1)));
-            HIP_TRY(smem_launch_aln_cand_count(&P, n_heavy, H.ccnt.p, H.chord.p, st));
+            HIP_TRY(hipMemsetAsync(H.chord.p, 0xFF, sizeof(uint32_t) * (size_t)std::max(n, 1), st));
             size_t tb = 0;
             HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)n_heavy, nullptr, &tb, st));
             HIP_TRY(H.tmp.grow(tb + 256));
-            tb = H.tmp.n;
-            HIP_TRY(smem_launch_offsets(H.ccnt.p, H.coff.p, (int)n_heavy, H.tmp.p, &tb, st));
-            HIP_TRY(hipMemcpyAsync(&hs[1], H.coff.p + n_heavy, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            if (nr) {
+                HIP_TRY(smem_launch_aln_cand_count(&Pr, nr, H.ccnt.p, H.chord.p, st));
+                tb = H.tmp.n;
+                HIP_TRY(smem_launch_offsets(H.ccnt.p, H.coff.p, (int)nr, H.tmp.p, &tb, st));
+            } else {
+                HIP_TRY(hipMemsetAsync(H.coff.p, 0, sizeof(uint64_t), st));
+            }
+            HIP_TRY(hipMemcpyAsync(&hs[1], H.coff.p + nr, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            hs[3] = 0;
+            if (n_giant) {
+                HIP_TRY(H.ccnt_g.grow(n_giant));
+                HIP_TRY(H.coff_g.grow(n_giant + 1));
+                HIP_TRY(H.chord_g.grow(std::max(n, 1)));
+                HIP_TRY(hipMemsetAsync(H.chord_g.p, 0xFF, sizeof(uint32_t) * (size_t)std::max(n, 1), st));
+                HIP_TRY(smem_launch_aln_cand_count(&P, n_giant, H.ccnt_g.p, H.chord_g.p, st));
+                tb = H.tmp.n;
+                HIP_TRY(smem_launch_offsets(H.ccnt_g.p, H.coff_g.p, (int)n_giant, H.tmp.p, &tb, st));
+                HIP_TRY(hipMemcpyAsync(&hs[3], H.coff_g.p + n_giant, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            }
             HIP_TRY(hipStreamSynchronize(st));
             const uint64_t m = hs[1];
-            const uint64_t mm = std::max<uint64_t>(m, 1);
+            m_giant = hs[3];
+            const uint64_t mm = std::max<uint64_t>(m + m_giant, 1);
             HIP_TRY(H.ckey.grow(mm));
             HIP_TRY(H.ckey2.grow(mm));
             HIP_TRY(H.cval.grow(mm));
@@ -2051,11 +2118,20 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
             HIP_TRY(H.cpos_s.grow(std::max<uint64_t>(n_seeds, 1)));
             HIP_TRY(H.cpos_c.grow(std::max<uint64_t>(n_chains, 1)));
             HIP_TRY(H.crng.grow(std::max<uint64_t>(n_seeds, 1)));
-            C.key = H.ckey.p, C.key2 = H.ckey2.p, C.val = H.cval.p, C.val2 = H.cval2.p, C.off = H.coff.p;
-            C.hmax = H.chmax.p, C.hord = H.chord.p, C.n_heavy = n_heavy, C.m = m, C.n_chains = n_chains;
+            const uint64_t mg = m_giant;
+            C.key = H.ckey.p + mg, C.key2 = H.ckey2.p + mg, C.val = H.cval.p + mg, C.val2 = H.cval2.p + mg;
+            C.off = H.coff.p, C.hmax = H.chmax.p + n_giant, C.hord = H.chord.p, C.n_heavy = nr, C.m = m;
+            C.n_chains = n_chains;
             size_t sb = 0;
-            HIP_TRY(smem_launch_aln_cand(&P, &C, nullptr, &sb, g->n_cu, st));
+            HIP_TRY(smem_launch_aln_cand(&Pr, &C, nullptr, &sb, g->n_cu, st));
             HIP_TRY(H.ctmp.grow(sb + 256));
+            if (n_giant) {
+                Cg.key = H.ckey.p, Cg.key2 = H.ckey2.p, Cg.val = H.cval.p, Cg.val2 = H.cval2.p, Cg.off = H.coff_g.p;
+                Cg.hmax = H.chmax.p, Cg.hord = H.chord_g.p, Cg.n_heavy = n_giant, Cg.m = mg, Cg.n_chains = n_chains;
+                sb = 0;
+                HIP_TRY(smem_launch_aln_cand(&P, &Cg, nullptr, &sb, g->n_cu, st));
+                HIP_TRY(H.ctmp_g.grow(sb + 256));
+            }
             P.cand_rb = H.crb.p, P.cand_re = H.cre.p, P.cand_q = H.cq.p, P.cand_made = H.cmade.p;
             P.cand_pos_s = H.cpos_s.p, P.cand_pos_c = H.cpos_c.p, P.cand_rng = H.crng.p;
         }
@@ -2084,14 +2160,51 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         // walk on st2
         const int lr = long_reads ? 1 : 0;
         HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, st));
-        smem::AlnParams Ph = P;  // the heavy list
+        smem::AlnParams Ph = P;  // the heavy list (under the giant split: the rest)
         Ph.tasks = H.htasks.p, Ph.torder = H.htorder.p, Ph.tfail = H.htfail.p, Ph.lq = H.hlq.p;
+        Ph.heavy = P.heavy + n_giant, Ph.hcnt = P.hcnt + n_giant, Ph.hscnt = P.hscnt + n_giant;
+        if (Ph.cand_made) {
+            Ph.cand_rb += m_giant, Ph.cand_re += m_giant, Ph.cand_q += m_giant, Ph.cand_made += m_giant;
+        }
         // the heavy walk's candidate index once the regions it holds are computed
         auto cand = [&]() -> hipError_t {
             if (!Ph.cand_made) return hipSuccess;
             size_t sb = H.ctmp.n;
             return smem_launch_aln_cand(&Ph, &C, H.ctmp.p, &sb, g->n_cu, st);
         };
+        if (n_giant) {
+            // four queues of work, each enqueued before the host blocks again (the candidate
+            // index's segmented sort reads its partition sizes back):
+            //   st:  the rest's passes, then their candidate index and walk
+            //   st2: the light reads' passes and walk
+            //   st3: the giants' passes, candidate index and walk (one wave each)
+            smem::AlnParams Pg = P;
+            Pg.tasks = H.gtasks.p, Pg.torder = H.gtorder.p, Pg.tfail = H.gtfail.p, Pg.lq = H.glq.p;
+            Pg.ctr = H.gctr.p, Pg.walk_waves = n_giant;
+            HIP_TRY(hipEventRecord(ev_join, st));
+            HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
+            HIP_TRY(hipStreamWaitEvent(st3, ev_join, 0));
+            HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
+            HIP_TRY(smem_launch_aln_passes(&P, g->n_cu, lr, st2));
+            P.light_claims = aln_light_claims();
+            HIP_TRY(smem_launch_aln(&P, g->n_cu, lr, st2));
+            P.light_claims = 0;
+            HIP_TRY(hipEventRecord(ev_join, st2));
+            HIP_TRY(smem_launch_aln_passes(&Pg, g->n_cu, lr, st3));
+            {
+                size_t sb = H.ctmp_g.n;
+                HIP_TRY(smem_launch_aln_cand(&Pg, &Cg, H.ctmp_g.p, &sb, g->n_cu, st3));
+            }
+            HIP_TRY(smem_launch_aln_heavy(&Pg, g->n_cu, lr, 2, st3));
+            HIP_TRY(hipEventRecord(ev_giant, st3));
+            if (n_heavy > n_giant) {
+                HIP_TRY(cand());
+                HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));
+            }
+            HIP_TRY(hipStreamWaitEvent(st, ev_join, 0));
+            HIP_TRY(hipStreamWaitEvent(st, ev_giant, 0));
+            return SMEM_OK;
+        }
         if (n_heavy && st2 && ev_join) {
             HIP_TRY(hipEventRecord(ev_join, st));
             HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
@@ -2191,7 +2304,8 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     // the light reads' kernels on the pair's low-priority stream
     if (aln_two_streams() && !b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
     if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->h_tot.p + 8, b->st,
-                         aln_two_streams() ? b->st2 : nullptr, b->ev_join))
+                         aln_two_streams() ? b->st2 : nullptr, b->ev_join, aln_two_streams() ? b->st3 : nullptr,
+                         b->ev_giant))
         return rc;
     if (int rc = aln_guard_check(P, b->st, b->h_tot.p + 8)) return rc;
     tmp = b->d_sa_tmp.n;
@@ -2648,6 +2762,7 @@ static int batch_prealloc(smem_batch_t* b) {
     HIP_TRY(b->h_aln_regs.grow(R * 4));  // pinned: the regions fetched (~3 per read)
     if (!b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
     if (!b->ev_fork) HIP_TRY(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    if (!b->ev_giant) HIP_TRY(hipEventCreateWithFlags(&b->ev_giant, hipEventDisableTiming));
     return SMEM_OK;
 }
 
@@ -2981,8 +3096,58 @@ static void gpu_chain(smem_gpu_t* g, const char* what, std::function<int()> step
     }).share();
 }
 
+// SMEM_GPU_CRASH_TRACE=1 (diagnostics): a host SIGSEGV / SIGBUS / SIGFPE / SIGABRT prints the
+// faulting thread's backtrace (module + offset, resolved offline with addr2line) and the
+// executable mappings of the program and this library to stderr, then takes the default action
+static char g_crash_maps[1 << 20];
+static void crash_trace(int sig, siginfo_t* si, void*) {
+    char buf[160];
+    int n = snprintf(buf, sizeof buf, "[smem crash] signal %d at %p, thread %ld\n", sig, si ? si->si_addr : nullptr,
+                     (long)syscall(SYS_gettid));
+    if (write(2, buf, (size_t)n) < 0) {}
+    void* fr[64];
+    backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        size_t m = 0;
+        ssize_t r;
+        while (m < sizeof g_crash_maps - 1 && (r = read(fd, g_crash_maps + m, sizeof g_crash_maps - 1 - m)) > 0)
+            m += (size_t)r;
+        close(fd);
+        g_crash_maps[m] = 0;
+        for (char* l = g_crash_maps; *l;) {
+            char* e = strchr(l, '\n');
+            const size_t len = e ? (size_t)(e - l + 1) : strlen(l);
+            const char save = l[len];
+            l[len] = 0;
+            if (strstr(l, "r-xp") && (strstr(l, "bwa") || strstr(l, "smemgpu")))
+                if (write(2, l, len) < 0) {}
+            l[len] = save;
+            l += len;
+        }
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+static void crash_trace_install() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* e = getenv("SMEM_GPU_CRASH_TRACE");
+        if (!e || !atoi(e)) return;
+        void* fr[4];
+        (void)backtrace(fr, 4);  // libgcc loaded now, not inside the handler
+        struct sigaction sa;
+        memset(&sa, 0, sizeof sa);
+        sa.sa_sigaction = crash_trace;
+        sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+        for (int sg : {SIGSEGV, SIGBUS, SIGFPE, SIGABRT}) sigaction(sg, &sa, nullptr);
+    });
+}
+
 int smem_gpu_open_async(smem_gpu_t** out, int device, const uint32_t* bwt, uint64_t bwt_size, uint64_t primary,
                         const uint64_t L2[5]) {
+    crash_trace_install();
     g_err[0] = 0;
     if (!out || !bwt || bwt_size < 16 || !L2) return fail(SMEM_E_ARG, "smem_gpu_open_async: bad index");
     *out = nullptr;

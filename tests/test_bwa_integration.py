@@ -122,8 +122,18 @@ def _run(fa, g, kind, threads, batch, env=None):
     """batch None: no -b (the binding's batch plan)."""
     args = [BWA, "mem", "-t", str(threads)] + ([] if batch is None else ["-b", str(batch)]) + \
            (["-p"] if kind == "pe" else []) + [fa, os.path.join(GOLD, "sam", f"{g}_{kind}.fq.gz")]
-    p = subprocess.run(args, capture_output=True, text=True, env=dict(os.environ, **(env or {})), timeout=600)
-    assert p.returncode == 0, p.stderr[-2000:]
+    # SMEM_GPU_CRASH_TRACE: a host crash prints its backtrace (the library's handler); the whole
+    # stderr of a failed run is kept under gpurun_out/ (merged back from a GPU box)
+    p = subprocess.run(args, capture_output=True, text=True,
+                       env=dict(os.environ, SMEM_GPU_CRASH_TRACE="1", **(env or {})), timeout=600)
+    if p.returncode != 0:
+        d = os.path.join(ROOT, "gpurun_out", "bwa_fail")
+        os.makedirs(d, exist_ok=True)
+        tag = f"{g}_{kind}_t{threads}_b{batch}_" + "_".join(f"{k}={v}" for k, v in (env or {}).items()).replace(",", ".")
+        with open(os.path.join(d, tag[:120] + ".err"), "w") as fh:
+            fh.write(" ".join(args) + "\n" + p.stderr)
+    crash = p.stderr.find("[smem crash]")
+    assert p.returncode == 0, (p.stderr[crash:crash + 3000] if crash >= 0 else p.stderr[-2000:])
     return [l for l in p.stdout.split("\n") if l and not l.startswith("@PG")], p.stderr
 
 
