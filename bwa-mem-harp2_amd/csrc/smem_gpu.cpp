@@ -161,6 +161,15 @@ struct Arena {
 thread_local Arena* t_dev_arena = nullptr;
 thread_local Arena* t_host_arena = nullptr;
 
+// SMEM_GPU_GUARD=1 (diagnostics): every device buffer allocated on its own is followed by
+// GUARD_BYTES of a known pattern, checked after each call on a batch (guard_check): a kernel
+// writing past the end of its buffer is named by the buffer's place in batch_bufs' order
+constexpr size_t GUARD_BYTES = 64 << 10;
+static bool guard_on() {
+    static const bool on = getenv("SMEM_GPU_GUARD") && atoi(getenv("SMEM_GPU_GUARD"));
+    return on;
+}
+
 template <class T>
 struct DevBuf {
     T* p = nullptr;
@@ -175,7 +184,9 @@ struct DevBuf {
                 p = static_cast<T*>(a), n = m, own = false;
                 return hipSuccess;
             }
-        hipError_t e = hipMalloc(&p, m * sizeof(T));
+        const size_t extra = guard_on() ? GUARD_BYTES : 0;
+        hipError_t e = hipMalloc(&p, m * sizeof(T) + extra);
+        if (e == hipSuccess && extra) e = hipMemset(reinterpret_cast<char*>(p) + m * sizeof(T), 0xA5, extra);
         if (e == hipSuccess) n = m, own = true;
         return e;
     }
@@ -502,6 +513,32 @@ static void batch_bufs(smem_batch_t* b, D&& d, H&& h) {
     d(b->d_pintv); h(b->h_pintv); h(b->h_intv_off); h(b->h_call_off);
 }
 
+static void guard_check(smem_batch_t* b, hipStream_t st, hipStream_t st2, hipStream_t st3) {
+    (void)hipStreamSynchronize(st3);
+    (void)hipStreamSynchronize(st2);
+    (void)hipStreamSynchronize(st);
+    std::vector<uint8_t> h(GUARD_BYTES);
+    int k = 0;
+    batch_bufs(b, [&](auto& x) {
+        if (x.p && x.own) {
+            const char* tail = reinterpret_cast<const char*>(x.p) + x.n * sizeof(*x.p);
+            if (hipMemcpy(h.data(), tail, GUARD_BYTES, hipMemcpyDeviceToHost) == hipSuccess) {
+                size_t bad = 0, first = GUARD_BYTES;
+                for (size_t i = 0; i < GUARD_BYTES; ++i)
+                    if (h[i] != 0xA5) bad += 1, first = std::min(first, i);
+                if (bad) {
+                    fprintf(stderr, "[smem guard] batch %p (max_reads %d, max_len %d, ran %d/%d/%d/%d): buffer #%d of "
+                            "%zu x %zu B written past its end: %zu guard bytes, the first at +%zu\n",
+                            (void*)b, b->max_reads, b->max_len, (int)b->ran, (int)b->sa_ran, (int)b->chain_ran,
+                            (int)b->aln_ran, k, x.n, sizeof(*x.p), bad, first);
+                    (void)hipMemset(const_cast<char*>(tail), 0xA5, GUARD_BYTES);
+                }
+            }
+        }
+        ++k;
+    }, [](auto&) {});
+}
+
 // ---- admission and the drain on the way out of every device call
 static int gpu_check(smem_gpu_t* g) {
     if (!g->faulted.load()) return SMEM_OK;
@@ -550,7 +587,10 @@ struct DeviceCall {
             e = hipStreamCreateWithFlags(&a, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
             if (e == hipSuccess) e = hipStreamCreateWithPriority(&b, hipStreamNonBlocking, least);
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking);
+            // the third stream (the giant reads' passes, candidate index and walk: the
+            // alignment stage's critical path) at the highest priority: its small kernels
+            // otherwise wait behind the other streams' lane passes for every CU
+            if (e == hipSuccess) e = hipStreamCreateWithPriority(&c, hipStreamNonBlocking, greatest);
             if (e != hipSuccess) {
                 if (a) (void)hipStreamDestroy(a);
                 if (b) (void)hipStreamDestroy(b);
@@ -586,13 +626,18 @@ struct DeviceCall {
     }
 };
 
+static void guard_check(smem_batch_t* b, hipStream_t st, hipStream_t st2, hipStream_t st3);
+
 // a batch's call: the leased pair is the batch's st / st2 for its duration
 struct BatchCall : DeviceCall {
     smem_batch_t* b;
     explicit BatchCall(smem_batch_t* b_) : DeviceCall(b_->g), b(b_) {
         if (rc == SMEM_OK) b->st = st, b->st2 = st2, b->st3 = st3;
     }
-    ~BatchCall() { b->st = b->st2 = b->st3 = nullptr; }
+    ~BatchCall() {
+        if (pair >= 0 && guard_on()) guard_check(b, st, st2, st3);
+        b->st = b->st2 = b->st3 = nullptr;
+    }
 };
 
 extern "C" {
@@ -2303,6 +2348,7 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     HIP_TRY(hipEventRecord(b->ev[0], b->st));
     // the light reads' kernels on the pair's low-priority stream
     if (aln_two_streams() && !b->ev_join) HIP_TRY(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    if (aln_two_streams() && !b->ev_giant) HIP_TRY(hipEventCreateWithFlags(&b->ev_giant, hipEventDisableTiming));
     if (int rc = run_aln(g, P, b->tot_chains, b->tot_seeds, b->max_len > 256, b->aln_heavy, b->h_tot.p + 8, b->st,
                          aln_two_streams() ? b->st2 : nullptr, b->ev_join, aln_two_streams() ? b->st3 : nullptr,
                          b->ev_giant))
