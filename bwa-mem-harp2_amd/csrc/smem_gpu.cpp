@@ -349,6 +349,8 @@ struct smem_gpu {
     hipStream_t init_st = nullptr;
     hipEvent_t sa_ready = nullptr;
     uint64_t* d_sa_raw = nullptr;  // the .sa as uploaded (kept: the lookups use it until sa_ready has passed)
+    uint64_t* d_link = nullptr;    // the densification's link scratch until sa_ready has passed (link_mu)
+    std::mutex link_mu;
     uint32_t sa_shift_raw = 0;
     std::vector<std::shared_future<int>> reserve;  // smem_gpu_reserve_slots: one per slot
     // smem_gpu_init_devices_async: the upload running on a host thread; every
@@ -914,6 +916,7 @@ void smem_gpu_shutdown(smem_gpu_t* g) {
     if (g->d_occ192) (void)hipFree(g->d_occ192);
     if (g->d_kt) (void)hipFree(g->d_kt);
     if (g->init_st) (void)hipStreamSynchronize(g->init_st);
+    if (g->d_link) (void)hipFree(g->d_link);
     if (g->d_sa) (void)hipFree(g->d_sa);
     if (g->d_sa_raw) (void)hipFree(g->d_sa_raw);
     if (g->d_pac) (void)hipFree(g->d_pac);
@@ -1331,6 +1334,47 @@ static hipError_t trim_default_pool(smem_gpu_t* g) {
     return e;
 }
 
+// The link scratch of the default (SMEM_GPU_DENSIFY_POOL unset) densification is an allocation
+// of its own, freed here once sa_ready has passed (hipFree waits for the device: once per
+// handle).  The default pool is shared by every handle of the process: with eight handles on
+// one GPU (the N = 8 fan-out rehearsed on one card) densifying side by side, a block one
+// handle freed with hipFreeAsync came back to another while still in use and the dense SA
+// came out wrong in ~15 % of runs (tools/flaky_probe.py, profiles/r06/multi_ctx).
+static hipError_t release_link(smem_gpu_t* g, bool wait) {
+    std::lock_guard<std::mutex> lk(g->link_mu);
+    if (!g->d_link) return hipSuccess;
+    if (wait) {
+        hipError_t e = hipEventSynchronize(g->sa_ready);
+        if (e != hipSuccess) return e;
+    } else if (hipEventQuery(g->sa_ready) != hipSuccess) {
+        (void)hipGetLastError();  // (not ready: a status, not an error of the caller's next call)
+        return hipSuccess;
+    }
+    hipError_t e = hipFree(g->d_link);
+    g->d_link = nullptr;
+    return e;
+}
+
+// SMEM_GPU_SA_CHECK=1 (diagnostics, small indexes): every stored sample against the dense
+// copy's row at the same position, after sa_ready; mismatches on stderr
+static void sa_check(smem_gpu_t* g) {
+    if (!getenv("SMEM_GPU_SA_CHECK") || !g->d_sa_raw || g->n_sa > (1ull << 28)) return;
+    if (hipEventSynchronize(g->sa_ready) != hipSuccess) return;
+    const uint64_t n_raw = (g->L2[4] >> g->sa_shift_raw) + 1, step = 1ull << (g->sa_shift_raw - g->sa_shift);
+    std::vector<uint64_t> raw(n_raw), dense(g->n_sa);
+    if (hipMemcpy(raw.data(), g->d_sa_raw, n_raw * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    if (hipMemcpy(dense.data(), g->d_sa, g->n_sa * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t bad = 0, first = UINT64_MAX;
+    for (uint64_t i = 0; i < n_raw && i * step < g->n_sa; ++i)
+        if (raw[i] != dense[i * step]) bad += 1, first = std::min(first, i);
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over every dense row: equal across handles of one index
+    for (uint64_t v : dense) h = (h ^ v) * 1099511628211ull;
+    fprintf(stderr, "[M::sa_check] handle %p device %d: %llu of %llu stored samples differ from the dense SA "
+            "(dense hash %016llx)%s\n", (void*)g, g->device, (unsigned long long)bad, (unsigned long long)n_raw,
+            (unsigned long long)h, bad ? " (first at sample " : "");
+    if (bad) fprintf(stderr, "[M::sa_check]   %llu)\n", (unsigned long long)first);
+}
+
 int smem_gpu_load_sa(smem_gpu_t* g, const smem_sa_t* sa) {
     g_err[0] = 0;
     gpu_wait(g);
@@ -1348,6 +1392,7 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
     if (g->d_sa || g->d_sa_raw) {
         // a reload: no batch may still read the old copy
         HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(release_link(g, true));
         if (g->d_sa) (void)hipFree(g->d_sa);
         if (g->d_sa_raw) (void)hipFree(g->d_sa_raw);
         g->d_sa = g->d_sa_raw = nullptr;
@@ -1389,14 +1434,22 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
         const char* dv = getenv("SMEM_GPU_DENSIFY");
         if (e == hipSuccess && n_dense < (1ull << 32) && !(dv && !strcmp(dv, "walk"))) {
             uint64_t* link = nullptr;
-            e = hipMallocAsync((void**)&link, n_dense * sizeof(uint64_t), g->init_st);
+            const char* pv = getenv("SMEM_GPU_DENSIFY_POOL");  // 1: the default pool (rounds 4-5; A/B only)
+            const bool pool = pv && atoi(pv);
+            e = pool ? hipMallocAsync((void**)&link, n_dense * sizeof(uint64_t), g->init_st)
+                     : hipMalloc(&link, n_dense * sizeof(uint64_t));
             if (e == hipSuccess) {
                 // the whole chip (capped at 4 blocks per CU so that the first
                 // batches ran beside it, it finished later and they were no
                 // faster: profiles/r04/e2e/probe_preload_densify_cap.log)
                 e = smem_launch_sa_densify2(&S, dshift, n_dense, link, dense, 0u, g->init_st);
-                hipError_t f = hipFreeAsync(link, g->init_st);
-                if (e == hipSuccess) e = f;
+                if (pool) {
+                    hipError_t f = hipFreeAsync(link, g->init_st);
+                    if (e == hipSuccess) e = f;
+                } else {
+                    std::lock_guard<std::mutex> lk(g->link_mu);
+                    g->d_link = link;  // release_link, once sa_ready has passed
+                }
             }
         } else if (e == hipSuccess) {
             e = smem_launch_sa_densify(&S, dshift, n_dense, dense, g->init_st);
@@ -1410,6 +1463,7 @@ static int load_sa_impl(smem_gpu_t* g, const smem_sa_t* sa) {
         if (e == hipSuccess && getenv("SMEM_GPU_SYNC_INIT")) {
             e = hipStreamSynchronize(g->init_st);
             if (e == hipSuccess) e = trim_default_pool(g);
+            if (e == hipSuccess) e = release_link(g, true);
         }
         if (e != hipSuccess) {
             (void)hipDeviceSynchronize();
@@ -1446,10 +1500,13 @@ int smem_batch_sa(smem_batch_t* b, int min_seed_len, int max_occ) {
         const char* rv = getenv("SMEM_GPU_SA_RAW");
         hipError_t q = (rv && atoi(rv)) ? hipErrorNotReady : hipEventQuery(g->sa_ready);
         if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
             sa_rows = g->d_sa_raw;
             sa_shift = g->sa_shift_raw;
         } else if (q != hipSuccess) {
             return fail(SMEM_E_DEVICE, "smem_batch_sa: densification", q);
+        } else if (g->d_link) {
+            HIP_TRY(release_link(g, false));
         }
     }
     const uint64_t ni = b->tot_intv;
@@ -3266,7 +3323,9 @@ int smem_gpu_wait_ready(smem_gpu_t* g) {
     if (g->sa_ready) {  // the .sa densification on the init stream (batches do not
         HIP_TRY(hipSetDevice(g->device));  // need it: their lookups use the uploaded
         HIP_TRY(hipEventSynchronize(g->sa_ready));  // samples until it is done)
+        HIP_TRY(release_link(g, true));
         HIP_TRY(trim_default_pool(g));
+        sa_check(g);
     }
     return SMEM_OK;
 }

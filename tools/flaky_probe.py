@@ -28,6 +28,9 @@ SETTINGS = {
     "ctx8_t16_b37_saraw": (16, 37, {"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_SA_RAW": "1"}),
     "ctx2_t16_b37": (16, 37, {"SMEM_GPU_DEVICES": "0,0"}),
     "ctx8_t16_b37_guard": (16, 37, {"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_GUARD": "1"}),
+    "ctx8_t16_b37_pool_check": (16, 37, {"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_DENSIFY_POOL": "1",
+                                         "SMEM_GPU_SA_CHECK": "1"}),
+    "ctx8_t16_b37_check": (16, 37, {"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_SA_CHECK": "1"}),
     "ctx1_t16_b37_guard": (16, 37, {"SMEM_GPU_DEVICES": "0", "SMEM_GPU_GUARD": "1"}),
     "ctx8_t8_b37_guard": (8, 37, {"SMEM_GPU_DEVICES": ",".join(["0"] * 8), "SMEM_GPU_GUARD": "1"}),
     "ctx1_t1_b37_guard": (1, 37, {"SMEM_GPU_DEVICES": "0", "SMEM_GPU_GUARD": "1"}),
@@ -68,7 +71,11 @@ def main():
                  "s": round(time.time() - t0, 2)}
             if diff:
                 r["first"] = [got[diff[0]][:300], want[diff[0]][:300]]
-            gl = [l for l in pr.stderr.split("\n") if l.startswith("[smem guard]")]
+            gl = [l for l in pr.stderr.split("\n") if l.startswith("[smem guard]") or
+                  (l.startswith("[M::sa_check]") and " 0 of " not in l)]
+            hs = sorted(set(l.split("dense hash ")[1][:16] for l in pr.stderr.split("\n") if "dense hash " in l))
+            if hs:
+                r["sa_hashes"] = hs
             if gl:
                 r["guard"] = gl[:20]
             if pr.returncode:
