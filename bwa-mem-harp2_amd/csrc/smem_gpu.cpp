@@ -2030,12 +2030,14 @@ static uint32_t aln_walk_wpc() {
     const int v = e ? atoi(e) : smem::ALN_WALK_WAVES;
     return (uint32_t)std::max(4, std::min(16, v / 4 * 4));
 }
-// the giant split's reads (SMEM_ALN_GIANTS, default 128; 0: off): the heaviest heavy reads by
-// seeds + chains (a read of ~10k seeds walks ~10 ms on its wave; the human-like profile's 1M reads
-// hold dozens), their passes and walk on the batch's third stream from the start
+// the giant split's reads (SMEM_ALN_GIANTS, default 2048; 0: off): the heaviest heavy reads by
+// seeds + chains (a read of ~10k seeds walks ~17 ms on its wave; the human-like profile's 1M reads
+// hold dozens), their passes and walk on the batch's third stream from the start.  Measured on
+// the human-like 1M reads (profiles/r06/aln/s6q_giants.log): 0 63.5 ms, 128 64.8 (giants after
+// the others' passes), 512 60.4, 1024 59.7, 2048 59.4, 4096 61.9, all 38k heavy reads 63.2
 static uint32_t aln_giants() {
     const char* e = getenv("SMEM_ALN_GIANTS");
-    return e ? (uint32_t)std::max(0, atoi(e)) : 128u;
+    return e ? (uint32_t)std::max(0, atoi(e)) : 2048u;
 }
 // SMEM_ALN_LANE=0: no regions computed ahead one seed per lane (the walks
 // extend every seed one wave per problem, round-2 style)
@@ -2283,22 +2285,37 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
             smem::AlnParams Pg = P;
             Pg.tasks = H.gtasks.p, Pg.torder = H.gtorder.p, Pg.tfail = H.gtfail.p, Pg.lq = H.glq.p;
             Pg.ctr = H.gctr.p, Pg.walk_waves = n_giant;
+            // SMEM_ALN_GIANT_FIRST (default 2): the giants' passes and candidate index run
+            // before the other heavy reads' passes start (ev_giant, recorded twice: the
+            // waits enqueued between take the first record), the light reads' passes
+            // beside them from the start (1: the light reads' wait too; 0: nobody waits)
+            // -- the lane passes hold every CU until their queues drain, so the giants'
+            // small kernels beside them waited ~30 ms for CUs (profiles/r06/aln, the s6n
+            // timeline); their walk, one wave a read, then runs beside the rest
+            const char* gf = getenv("SMEM_ALN_GIANT_FIRST");
+            const int first = gf ? atoi(gf) : 2;
             HIP_TRY(hipEventRecord(ev_join, st));
-            HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
             HIP_TRY(hipStreamWaitEvent(st3, ev_join, 0));
+            HIP_TRY(smem_launch_aln_passes(&Pg, g->n_cu, lr, st3));
+            {
+                size_t sb = H.ctmp_g.n;
+                HIP_TRY(smem_launch_aln_cand(&Pg, &Cg, H.ctmp_g.p, &sb, g->n_cu, st3));
+            }
+            if (first) {
+                HIP_TRY(hipEventRecord(ev_giant, st3));
+                HIP_TRY(hipStreamWaitEvent(st, ev_giant, 0));
+                HIP_TRY(hipStreamWaitEvent(st2, first == 2 ? ev_join : ev_giant, 0));
+            } else {
+                HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
+            }
+            HIP_TRY(smem_launch_aln_heavy(&Pg, g->n_cu, lr, 2, st3));
+            HIP_TRY(hipEventRecord(ev_giant, st3));
             HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
             HIP_TRY(smem_launch_aln_passes(&P, g->n_cu, lr, st2));
             P.light_claims = aln_light_claims();
             HIP_TRY(smem_launch_aln(&P, g->n_cu, lr, st2));
             P.light_claims = 0;
             HIP_TRY(hipEventRecord(ev_join, st2));
-            HIP_TRY(smem_launch_aln_passes(&Pg, g->n_cu, lr, st3));
-            {
-                size_t sb = H.ctmp_g.n;
-                HIP_TRY(smem_launch_aln_cand(&Pg, &Cg, H.ctmp_g.p, &sb, g->n_cu, st3));
-            }
-            HIP_TRY(smem_launch_aln_heavy(&Pg, g->n_cu, lr, 2, st3));
-            HIP_TRY(hipEventRecord(ev_giant, st3));
             if (n_heavy > n_giant) {
                 HIP_TRY(cand());
                 HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));

@@ -110,6 +110,13 @@ def _heavy_env(monkeypatch, heavy):
             # the heavy walk without the candidate index (the bin hash of the
             # regions made so far)
             monkeypatch.setenv("SMEM_ALN_CAND", "0")
+        elif opt.startswith("giants"):
+            # the giant split's size (SMEM_ALN_GIANTS; 0: off): the heaviest heavy reads'
+            # passes, candidate index and walk on the batch's third stream
+            monkeypatch.setenv("SMEM_ALN_GIANTS", opt[len("giants"):])
+        elif opt.startswith("gfirst"):
+            # whose passes wait for the giants' (SMEM_ALN_GIANT_FIRST 0 / 1 / 2)
+            monkeypatch.setenv("SMEM_ALN_GIANT_FIRST", opt[len("gfirst"):])
     if heavy and "/" in heavy:
         heavy, _, streams = heavy.partition("/")
         monkeypatch.setenv("SMEM_ALN_STREAMS", streams)
@@ -150,7 +157,8 @@ def test_pack_matches_reference_pac():
                                        (20, 1, "3"), (100, 1, "0"), (100, 1, "1000:3"), (100, 1, "3/1"),
                                        (100, 1, "1+inline"), (100, 2, "3+inline"), (100, 1, "0+nolane"),
                                        (100, 1, "1+nolane"), (100, 2, "3+nolane"), (100, 1, "1+nocand"),
-                                       (100, 2, "3+nocand")])
+                                       (100, 2, "3+nocand"), (100, 1, "1+giants0"), (100, 1, "1+giants7"),
+                                       (100, 2, "3+giants64+gfirst0"), (100, 1, "1+giants100000+gfirst1")])
 def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a, heavy, monkeypatch):
     """600 kbp, 60 % diverged repeat copies; 4000 reads of 70..700 bp (both
     kernel instantiations) with substitutions and Ns; chains from the GPU
@@ -160,7 +168,8 @@ def test_aln_gpu_vs_oracle_repeat_dense(gpu_device, w, a, heavy, monkeypatch):
     (-A 2 scaling, b 8, gaps 12 + 2) sends the short path's longer queries
     through ksw_align2's 16-bit branch.  heavy: SMEM_ALN_HEAVY_MIN (1: every
     read through the heavy-read path, 3: reads with 3+ chains, 0: none,
-    1000:3 reads with 3+ seeds)."""
+    1000:3 reads with 3+ seeds); giants<N>: the giant split's size (0: off,
+    100000: every heavy read), gfirst<K>: whose passes wait for the giants'."""
     _heavy_env(monkeypatch, heavy)
     import smemgpu
     from smemgpu import synth

@@ -46,7 +46,7 @@ def main():
     settings = [s for s in own.env_sweep.replace("/", ";").split(";") if s] or [""]
     first = None
     for setting in settings:
-        kv = dict(x.split("=", 1) for x in setting.split(",") if x)
+        kv = dict(x.split("=", 1) for x in setting.replace("+", ",").split(",") if x)
         saved = {k: os.environ.get(k) for k in kv}
         os.environ.update(kv)
         for k in range(own.launches):
