@@ -2891,6 +2891,53 @@ static int batch_prealloc(smem_batch_t* b) {
     HIP_TRY(H.hscnt.grow(R));
     HIP_TRY(H.hoff.grow(R + 1));
     HIP_TRY(H.rnext.grow(ns));
+    {
+        // the heavy walk's candidate index (the heavy reads' seeds + chains: ~4 a read
+        // human-like, 8 reserved) and the giant split's lists, carved with the rest of the
+        // slot: made on a worker's first batch they were ~13 allocations a slot inside
+        // mem_process_seqs (and as many hipFree calls at exit)
+        const uint64_t mc = R * 8, G = std::min<uint64_t>(R, 2048);
+        size_t tb = 0;
+        HIP_TRY(smem_launch_offsets(nullptr, nullptr, (int)R, nullptr, &tb, nullptr));
+        HIP_TRY(H.tmp.grow(tb + 256));
+        HIP_TRY(H.ccnt.grow(R));
+        HIP_TRY(H.coff.grow(R + 1));
+        HIP_TRY(H.chord.grow(R));
+        HIP_TRY(H.ckey.grow(mc));
+        HIP_TRY(H.ckey2.grow(mc));
+        HIP_TRY(H.cval.grow(mc));
+        HIP_TRY(H.cval2.grow(mc));
+        HIP_TRY(H.chmax.grow(R));
+        HIP_TRY(H.crb.grow(mc));
+        HIP_TRY(H.cre.grow(mc));
+        HIP_TRY(H.cq.grow(mc));
+        HIP_TRY(H.cmade.grow(mc));
+        HIP_TRY(H.cpos_s.grow(ns));
+        HIP_TRY(H.cpos_c.grow(nc));
+        HIP_TRY(H.crng.grow(ns));
+        smem::AlnParams P0{};
+        smem::CandParams C0{};
+        C0.m = mc, C0.n_heavy = (uint32_t)R;
+        size_t sb = 0;
+        HIP_TRY(smem_launch_aln_cand(&P0, &C0, nullptr, &sb, 1, nullptr));
+        HIP_TRY(H.ctmp.grow(sb + 256));
+        HIP_TRY(H.heavy2.grow(R));
+        HIP_TRY(H.hcnt2.grow(R));
+        HIP_TRY(H.hscnt2.grow(R));
+        HIP_TRY(H.rgiant.grow(R));
+        HIP_TRY(H.gctr.grow(smem::ALN_CTRS));
+        HIP_TRY(H.gtasks.grow(ns));
+        HIP_TRY(H.gtorder.grow(ns));
+        HIP_TRY(H.gtfail.grow(ns));
+        HIP_TRY(H.glq.grow(smem::LQ_WORDS));
+        HIP_TRY(H.ccnt_g.grow(G));
+        HIP_TRY(H.coff_g.grow(G + 1));
+        HIP_TRY(H.chord_g.grow(R));
+        C0.n_heavy = (uint32_t)G;
+        sb = 0;
+        HIP_TRY(smem_launch_aln_cand(&P0, &C0, nullptr, &sb, 1, nullptr));
+        HIP_TRY(H.ctmp_g.grow(sb + 256));
+    }
     // (H.ht, the walk's bin hash, is grown by run_aln only for a walk without the candidate index)
     HIP_TRY(b->d_aln_out.grow(R * 4));
     HIP_TRY(b->h_aln_regoff.grow(R + 1));
