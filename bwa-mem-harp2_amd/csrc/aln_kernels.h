@@ -32,13 +32,18 @@ struct RegTask {
 // the lane path's queue words (AlnParams::lq)
 constexpr int LQ_NTASK = 0;     // tasks listed
 constexpr int LQ_NSW = 1;       // heavy chains listed for mem_chain2aln_short's SW
-constexpr int LQ_QUEUES = 9;    // 16-column queues: pass lengths 1 .. 144 (LQ_MAXQ)
+constexpr int LQ_QUEUES = 16;   // 16-column queues: pass lengths 1 .. 256 (LQ_MAXQ)
 constexpr int LQ_MAXQ = 16 * LQ_QUEUES;
 constexpr int LQ_BOUNDS = 8;    // [LQ_QUEUES + 1] queue q = order[bounds[q] .. bounds[q + 1]): lengths 16q + 1 .. 16q + 16
-constexpr int LQ_HEADS = 24;    // [LQ_QUEUES] claim counters
-constexpr int LQ_HIST = 40;     // [LQ_BUCKETS] tasks per pass length (0..LQ_MAXQ, longer), then cursors
+constexpr int LQ_HEADS = 25;    // [LQ_QUEUES] claim counters
+constexpr int LQ_HIST = 41;     // [LQ_BUCKETS] tasks per pass length (0..LQ_MAXQ, longer), then cursors
 constexpr int LQ_BUCKETS = LQ_MAXQ + 2;
-constexpr int LQ_WORDS = 192;
+constexpr int LQ_WORDS = 320;
+// the lane engine's tiers: columns, and the queues each takes (32: 0-1, 64: 2-3, 144: 4-8,
+// 256: 9-15 -- the 250-bp reads' extensions; its column array is past the 256 VGPRs a lane
+// has at two waves a SIMD, so that tier runs one wave a SIMD with the rest in AGPRs)
+constexpr int LQ_TIER_Q0(int kcol) { return kcol == 32 ? 0 : kcol == 64 ? 2 : kcol == 144 ? 4 : 9; }
+constexpr int LQ_TIER_Q1(int kcol) { return kcol == 32 ? 2 : kcol == 64 ? 4 : kcol == 144 ? 9 : LQ_QUEUES; }
 static_assert(LQ_BOUNDS + LQ_QUEUES + 1 <= LQ_HEADS && LQ_HEADS + LQ_QUEUES <= LQ_HIST &&
               LQ_HIST + LQ_BUCKETS <= LQ_WORDS, "lane queue words");
 

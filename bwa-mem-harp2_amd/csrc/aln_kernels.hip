@@ -1393,14 +1393,13 @@ __global__ __launch_bounds__(256) void aln_task_hist_kernel(AlnParams P, int sid
 __global__ __launch_bounds__(64) void aln_task_scan_kernel(AlnParams P) {
     if (threadIdx.x != 0) return;
     uint32_t a = 0;
-    uint32_t c[LQ_BUCKETS];
-    for (int k = 0; k < LQ_BUCKETS; ++k) {
-        c[k] = a;
-        a += P.lq[LQ_HIST + k];
+    for (int k = 0; k < LQ_BUCKETS; ++k) {  // in place (a private array of LQ_BUCKETS went to scratch)
+        const uint32_t v = P.lq[LQ_HIST + k];
+        P.lq[LQ_HIST + k] = a;
+        a += v;
     }
-    for (int k = 0; k < LQ_BUCKETS; ++k) P.lq[LQ_HIST + k] = c[k];
     P.lq[LQ_BOUNDS] = 0;
-    for (int q = 1; q <= LQ_QUEUES; ++q) P.lq[LQ_BOUNDS + q] = c[16 * q + 1];
+    for (int q = 1; q <= LQ_QUEUES; ++q) P.lq[LQ_BOUNDS + q] = P.lq[LQ_HIST + 16 * q + 1];
     for (int q = 0; q < LQ_QUEUES; ++q) P.lq[LQ_HEADS + q] = 0;
 }
 
@@ -1511,19 +1510,21 @@ struct RegionPol {
 };
 
 // KCOL-column lane engine over the pass's queues of query lengths up to KCOL
-// (32: queues 0-1, 64: 2-3, 144: 4-8).  The top tier is 144 columns, not 128:
-// a 150-bp read's seeds near its ends make extensions of 129-131 columns (2.8 %
+// (32: queues 0-1, 64: 2-3, 144: 4-8, 256: 9-15).  The 144 tier, not 128: a
+// 150-bp read's seeds near its ends make extensions of 129-131 columns (2.8 %
 // of the human-like profile's tasks), which one wave each took 6.2 ms of the
 // heavy reads' critical path (profiles/r06/aln/s6d_human_kernel_stats.csv).
+// The 256 tier takes the 250-bp reads' longer extensions (c4), one wave each
+// before: its 257-entry column array needs one wave a SIMD (VGPRs + AGPRs).
 template <int KCOL>
-__global__ __launch_bounds__(256, KCOL > 64 ? 2 : 4) void aln_region_lane_kernel(AlnParams P, int side) {
+__global__ __launch_bounds__(256, KCOL > 144 ? 1 : KCOL > 64 ? 2 : 4) void aln_region_lane_kernel(AlnParams P,
+                                                                                                 int side) {
     __shared__ uint32_t stab[10];
     __shared__ uint2 qsl[4][KCOL / 8 * 64];
     if (threadIdx.x < 5) kswl::row_scores(P.mat, threadIdx.x, stab[2 * threadIdx.x], stab[2 * threadIdx.x + 1]);
     __syncthreads();
     RegionPol pol{&P, side, P.top};
-    kswl::lane_engine<KCOL, 8>(pol, P.lq + LQ_BOUNDS, P.lq + LQ_HEADS, KCOL == 32 ? 0 : KCOL == 64 ? 2 : 4,
-                               KCOL == 32 ? 2 : KCOL == 64 ? 4 : LQ_QUEUES, stab,
+    kswl::lane_engine<KCOL, 8>(pol, P.lq + LQ_BOUNDS, P.lq + LQ_HEADS, LQ_TIER_Q0(KCOL), LQ_TIER_Q1(KCOL), stab,
                                qsl[threadIdx.x >> 6], P.o_del, P.e_del, P.o_ins, P.e_ins, P.top);
 }
 
@@ -1739,7 +1740,8 @@ extern "C" hipError_t smem_launch_aln_passes(const smem::AlnParams* P, int n_cu,
         hipLaunchKernelGGL(smem::aln_task_scatter_kernel, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<32>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<64>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
-        hipLaunchKernelGGL(smem::aln_region_lane_kernel<smem::LQ_MAXQ>, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_region_lane_kernel<144>, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
+        hipLaunchKernelGGL(smem::aln_region_lane_kernel<256>, dim3(n_cu), dim3(256), 0, st, *P, side);
     }
     hipLaunchKernelGGL(smem::aln_region_cov_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
     hipLaunchKernelGGL(smem::aln_region_rest_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);
