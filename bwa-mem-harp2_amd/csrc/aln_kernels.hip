@@ -1370,7 +1370,7 @@ __device__ __forceinline__ int task_key(const AlnParams& P, uint32_t t, int side
         if (P.tfail[t]) return LQ_BUCKETS - 1;
         q = (int)(P.offs[T.r + 1] - P.offs[T.r]) - s.qbeg - s.len;
     }
-    return q <= LQ_MAXQ ? q : LQ_BUCKETS - 1;
+    return q <= LQ_MAXQ && (q < LQ_GAP_LO || q > LQ_GAP_HI) ? q : LQ_BUCKETS - 1;
 }
 
 // counting sort of the tasks by the pass's query length: block histograms in
@@ -1741,7 +1741,8 @@ extern "C" hipError_t smem_launch_aln_passes(const smem::AlnParams* P, int n_cu,
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<32>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<64>, dim3(n_cu * 4), dim3(256), 0, st, *P, side);
         hipLaunchKernelGGL(smem::aln_region_lane_kernel<144>, dim3(n_cu * 2), dim3(256), 0, st, *P, side);
-        hipLaunchKernelGGL(smem::aln_region_lane_kernel<256>, dim3(n_cu), dim3(256), 0, st, *P, side);
+        if (P->max_len <= 0 || P->max_len > smem::LQ_GAP_HI + 1)
+            hipLaunchKernelGGL(smem::aln_region_lane_kernel<256>, dim3(n_cu), dim3(256), 0, st, *P, side);
     }
     hipLaunchKernelGGL(smem::aln_region_cov_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
     hipLaunchKernelGGL(smem::aln_region_rest_kernel<4>, dim3(n_cu * 8), dim3(256), 0, st, *P);

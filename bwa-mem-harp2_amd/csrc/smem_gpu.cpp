@@ -424,6 +424,7 @@ struct smem_batch {
     hipStream_t st3 = nullptr;  // chains -> regions: the giant reads' passes and walk (ev_giant joins them)
     hipEvent_t ev_join = nullptr, ev_fork = nullptr, ev_giant = nullptr;
     int max_reads = 0, max_len = 0;
+    int read_len_max = 0;  // the longest read of the reads set (set_reads*)
     uint64_t max_bases = 0;
     uint32_t cap_intv = 0, cap_calls = 0, cap_list = 0;
     int lanes = 0;
@@ -1019,6 +1020,9 @@ int smem_batch_create(smem_gpu_t* g, int max_reads, uint64_t max_bases, int max_
 
 // the staged reads host -> device, under the caller's BatchCall
 static int upload_reads(smem_batch_t* b, int n_reads) {
+    int ml = 0;
+    for (int i = 0; i < n_reads; ++i) ml = std::max<int>(ml, (int)(b->h_offs.p[i + 1] - b->h_offs.p[i]));
+    b->read_len_max = ml;
     b->ran = b->fetched = false;
     b->n_reads = 0;
     const uint64_t nb = b->h_offs.p[n_reads];
@@ -2408,6 +2412,7 @@ int smem_batch_chain2aln(smem_batch_t* b, const smem_aln_opt_t* opt) {
     P.seeds = b->d_out_seed.p;
     P.seed_off = b->d_seed_off.p;  // a read's chains' seeds are contiguous: its region capacity
     P.pac = g->d_pac, P.l_pac = g->l_pac, P.n_reads = n;
+    P.max_len = b->read_len_max > 0 ? b->read_len_max : b->max_len;
     aln_opt_params(opt, P);
     P.srt = b->d_aln_srt.p, P.raw = b->d_aln_raw.p, P.n_regs = b->d_aln_nregs.p, P.ctr = b->d_aln_ctr.p;
     // diagnostics: SMEM_ALN_CYCLES=<file> writes the shader cycles each read took (u64 per read),
@@ -2510,7 +2515,9 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     const uint64_t n_chains = chain_off[n_reads];
     std::vector<uint64_t> cap(n_reads + 1, 0);
     bool long_reads = false;
+    int max_len = 0;
     for (int r = 0; r < n_reads; ++r) {
+        max_len = std::max<int>(max_len, (int)std::min<uint64_t>(offs[r + 1] - offs[r], 1u << 30));
         if (offs[r + 1] < offs[r] || offs[r + 1] - offs[r] > 1024 || chain_off[r + 1] < chain_off[r])
             return fail(SMEM_E_ARG, "smem_chain2aln: read longer than 1024 bp or offsets not ascending");
         long_reads |= offs[r + 1] - offs[r] > 256;
@@ -2600,6 +2607,7 @@ int smem_chain2aln(smem_gpu_t* g, int n_reads, const uint8_t* codes, const uint6
     std::memset(&P, 0, sizeof(P));
     P.codes = dcodes.p, P.offs = doffs.p, P.chains = dch.p, P.chain_off = dchoff.p, P.seeds = dseeds.p;
     P.seed_off = dseedoff.p, P.pac = pac ? dpac.p : g->d_pac, P.l_pac = l_pac, P.n_reads = n_reads;
+    P.max_len = max_len;
     aln_opt_params(opt, P);
     P.srt = dsrt.p, P.raw = draw.p, P.n_regs = dnregs.p, P.ctr = dctr.p;
     HIP_TRY(hipEventRecord(ev[0], st));
