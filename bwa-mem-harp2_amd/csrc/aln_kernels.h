@@ -42,11 +42,12 @@ constexpr int LQ_WORDS = 320;
 // the lane engine's tiers: columns, and the queues each takes (32: 0-1, 64: 2-3, 144: 4-8,
 // 256: 9-15 -- the 250-bp reads' extensions; its column array is past the 256 VGPRs a lane
 // has at two waves a SIMD, so that tier runs one wave a SIMD with the rest in AGPRs)
-constexpr int LQ_TIER_Q0(int kcol) { return kcol == 32 ? 0 : kcol == 64 ? 2 : kcol == 144 ? 4 : 10; }
-// pass lengths the lanes leave to one wave each (aln_region_rest_kernel): queue 9, 145-160 columns --
-// a 150-bp read's seeds in its last 5 bases; the 256 tier is then launched only for batches of
-// reads past 161 bp (its launch, one block a CU with 64 KB of LDS, waited for CUs behind the other
-// streams' lane passes even with nothing to do: 59.4 -> 61.0 ms human-like)
+constexpr int LQ_TIER_Q0(int kcol) { return kcol == 32 ? 0 : kcol == 64 ? 2 : kcol == 144 ? 4 : 9; }
+// in a batch of reads of at most LQ_GAP_HI + 1 bp the 256 tier is not launched, and the pass
+// lengths LQ_GAP_LO .. LQ_GAP_HI (queue 9: a 150-bp read's seeds in its last 5 bases) go to one
+// wave each (aln_region_rest_kernel) -- the tier's launch, one block a CU with 64 KB of LDS,
+// waited for CUs behind the other streams' lane passes even with nothing to do: 59.4 -> 61.0 ms
+// human-like; with longer reads queue 9 is the 256 tier's (c4: 242 -> 212 ms)
 constexpr int LQ_GAP_LO = 145, LQ_GAP_HI = 160;
 constexpr int LQ_TIER_Q1(int kcol) { return kcol == 32 ? 2 : kcol == 64 ? 4 : kcol == 144 ? 9 : LQ_QUEUES; }
 static_assert(LQ_BOUNDS + LQ_QUEUES + 1 <= LQ_HEADS && LQ_HEADS + LQ_QUEUES <= LQ_HIST &&

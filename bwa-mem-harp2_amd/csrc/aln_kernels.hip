@@ -1370,7 +1370,8 @@ __device__ __forceinline__ int task_key(const AlnParams& P, uint32_t t, int side
         if (P.tfail[t]) return LQ_BUCKETS - 1;
         q = (int)(P.offs[T.r + 1] - P.offs[T.r]) - s.qbeg - s.len;
     }
-    return q <= LQ_MAXQ && (q < LQ_GAP_LO || q > LQ_GAP_HI) ? q : LQ_BUCKETS - 1;
+    const bool gap = P.max_len > 0 && P.max_len <= LQ_GAP_HI + 1;  // no 256 tier in this batch
+    return q <= LQ_MAXQ && !(gap && q >= LQ_GAP_LO && q <= LQ_GAP_HI) ? q : LQ_BUCKETS - 1;
 }
 
 // counting sort of the tasks by the pass's query length: block histograms in
