@@ -81,13 +81,14 @@ CONFIGS = {
     "c3": dict(read_len=150, sub=0.02, k=19, pairs=True, stream_reads=25_000_000,
                what="C3 on one GPU: its shard of 100M x 150 bp PE on 8 GPUs = 12.5M pairs, insert N(500, 50), "
                     "mates interleaved in one chunk"),
-    # c4 / c5 stream in 1M-read chunks with 4 workers: their reads carry ~1.7x the intervals of
-    # c2's, and 2M-read chunks (1.7 GB of pinned results each) fetched at 10-15 GB/s instead of
-    # 30 (profiles/r06/stream/stream_c5.jsonl: 15.8 -> 32.5 M reads/s)
-    "c4": dict(read_len=250, sub=0.02, k=19, pairs=False, stream_reads=10_000_000, stream_chunk=1 << 20,
-               stream_workers=4, what="C4: 10M x 250 bp, min-seed-len 19 with re-seeding"),
-    "c5": dict(read_len=150, sub=0.05, k=19, pairs=False, stream_reads=10_000_000, stream_chunk=1 << 20,
-               stream_workers=4, what="C5: 10M x 150 bp at 5 % substitutions"),
+    # c4 / c5 stream in 256k-read chunks with 8 workers: their reads carry ~1.7x the intervals of
+    # c2's, and a chunk's pinned results fetch slower the larger they are (2M-read chunks, 1.7 GB:
+    # 10-15 GB/s; profiles/r06/stream/: 2M 15.8-18.3, 1M 23.3-32.5, 512k 25.1-33.5, 256k
+    # 30.5-32.5 M reads/s at c5 over repeated sweeps -- the 256k chunks the steadiest)
+    "c4": dict(read_len=250, sub=0.02, k=19, pairs=False, stream_reads=10_000_000, stream_chunk=1 << 18,
+               stream_workers=8, what="C4: 10M x 250 bp, min-seed-len 19 with re-seeding"),
+    "c5": dict(read_len=150, sub=0.05, k=19, pairs=False, stream_reads=10_000_000, stream_chunk=1 << 18,
+               stream_workers=8, what="C5: 10M x 150 bp at 5 % substitutions"),
 }
 
 
