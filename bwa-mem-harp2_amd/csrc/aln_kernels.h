@@ -204,6 +204,9 @@ hipError_t smem_launch_aln_cand(const smem::AlnParams* P, const smem::CandParams
 // (lq / hlq zeroed; heavy_min / heavy_seeds set): every chain's prep and
 // tasks (light reads' to tasks / lq, heavy reads' to htasks / hlq), then, per
 // list (P with tasks / lq, torder, tfail of that list), the passes
-hipError_t smem_launch_aln_prep(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st);
+// parts: 1 every chain's prep and the light / heavy task lists, 2 the heavy chains' short SW
+// (aln_heavy_sw_kernel: their tasks when it declines), 3 both -- the light reads' passes need
+// only part 1 (c4's 250-bp reads: part 2 is 36 ms of one-wave-a-chain SW)
+hipError_t smem_launch_aln_prep(const smem::AlnParams* P, uint64_t n_chains, int n_cu, int parts, hipStream_t st);
 hipError_t smem_launch_aln_passes(const smem::AlnParams* P, int n_cu, int long_reads, hipStream_t st);
 }

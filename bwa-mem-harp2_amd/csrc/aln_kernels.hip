@@ -1721,13 +1721,16 @@ extern "C" hipError_t smem_launch_aln_cand(const smem::AlnParams* P, const smem:
 // right) the sort and the three tiers of the lane engine, the coverage pass
 // and the tasks the lanes left (smem_launch_aln_passes; long_reads: the batch
 // holds reads past 256 bp)
-extern "C" hipError_t smem_launch_aln_prep(const smem::AlnParams* P, uint64_t n_chains, int n_cu, hipStream_t st) {
+extern "C" hipError_t smem_launch_aln_prep(const smem::AlnParams* P, uint64_t n_chains, int n_cu, int parts,
+                                           hipStream_t st) {
     if (P->n_reads <= 0) return hipSuccess;
-    const int rb = std::max(1, std::min(n_cu * 4, (P->n_reads + 255) / 256));
-    const int cb = std::max<int>(1, (int)std::min<uint64_t>((uint64_t)n_cu * 8, (n_chains + 255) / 256));
-    hipLaunchKernelGGL(smem::aln_chain_read_kernel, dim3(rb), dim3(256), 0, st, *P);
-    hipLaunchKernelGGL(smem::aln_chain_prep_kernel, dim3(cb), dim3(256), 0, st, *P, (uint32_t)n_chains);
-    hipLaunchKernelGGL(smem::aln_heavy_sw_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
+    if (parts & 1) {
+        const int rb = std::max(1, std::min(n_cu * 4, (P->n_reads + 255) / 256));
+        const int cb = std::max<int>(1, (int)std::min<uint64_t>((uint64_t)n_cu * 8, (n_chains + 255) / 256));
+        hipLaunchKernelGGL(smem::aln_chain_read_kernel, dim3(rb), dim3(256), 0, st, *P);
+        hipLaunchKernelGGL(smem::aln_chain_prep_kernel, dim3(cb), dim3(256), 0, st, *P, (uint32_t)n_chains);
+    }
+    if (parts & 2) hipLaunchKernelGGL(smem::aln_heavy_sw_kernel, dim3(n_cu * 4), dim3(256), 0, st, *P);
     return hipGetLastError();
 }
 

@@ -2282,7 +2282,9 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         // read's thousands of chains) on st, beside the light reads' passes and
         // walk on st2
         const int lr = long_reads ? 1 : 0;
-        HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, st));
+        // the heavy chains' short SW (prep part 2) is enqueued after the light reads' stream
+        // has forked off: their passes need only the task lists (part 1)
+        HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, (n_heavy && st2 && ev_join) ? 1 : 3, st));
         smem::AlnParams Ph = P;  // the heavy list (under the giant split: the rest)
         Ph.tasks = H.htasks.p, Ph.torder = H.htorder.p, Ph.tfail = H.htfail.p, Ph.lq = H.hlq.p;
         Ph.heavy = P.heavy + n_giant, Ph.hcnt = P.hcnt + n_giant, Ph.hscnt = P.hscnt + n_giant;
@@ -2313,8 +2315,11 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
             // timeline); their walk, one wave a read, then runs beside the rest
             const char* gf = getenv("SMEM_ALN_GIANT_FIRST");
             const int first = gf ? atoi(gf) : 2;
-            HIP_TRY(hipEventRecord(ev_join, st));
-            HIP_TRY(hipStreamWaitEvent(st3, ev_join, 0));
+            HIP_TRY(hipEventRecord(ev_join, st));  // the task lists are made
+            if (first != 1) HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
+            HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, 2, st));  // the heavy chains' short SW
+            HIP_TRY(hipEventRecord(ev_giant, st));
+            HIP_TRY(hipStreamWaitEvent(st3, ev_giant, 0));
             HIP_TRY(smem_launch_aln_passes(&Pg, g->n_cu, lr, st3));
             {
                 size_t sb = H.ctmp_g.n;
@@ -2323,9 +2328,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
             if (first) {
                 HIP_TRY(hipEventRecord(ev_giant, st3));
                 HIP_TRY(hipStreamWaitEvent(st, ev_giant, 0));
-                HIP_TRY(hipStreamWaitEvent(st2, first == 2 ? ev_join : ev_giant, 0));
-            } else {
-                HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
+                if (first == 1) HIP_TRY(hipStreamWaitEvent(st2, ev_giant, 0));
             }
             HIP_TRY(smem_launch_aln_heavy(&Pg, g->n_cu, lr, 2, st3));
             HIP_TRY(hipEventRecord(ev_giant, st3));
@@ -2346,6 +2349,7 @@ static int run_aln(smem_gpu_t* g, smem::AlnParams& P, uint64_t n_chains, uint64_
         if (n_heavy && st2 && ev_join) {
             HIP_TRY(hipEventRecord(ev_join, st));
             HIP_TRY(hipStreamWaitEvent(st2, ev_join, 0));
+            HIP_TRY(smem_launch_aln_prep(&P, n_chains, g->n_cu, 2, st));  // the heavy chains' short SW
             HIP_TRY(smem_launch_aln_passes(&Ph, g->n_cu, lr, st));
             HIP_TRY(cand());
             HIP_TRY(smem_launch_aln_heavy(&Ph, g->n_cu, lr, 2, st));
