@@ -657,6 +657,13 @@ def _mem_times(stderr: str) -> tuple:
     return n, real
 
 
+def _main_real(stderr: str):
+    """main()'s "[main] Real time: R sec" (software/main.c), or None"""
+    import re
+    m = re.search(r"\[main\] Real time: ([\d.]+) sec", stderr)
+    return float(m.group(1)) if m else None
+
+
 def _mem_chunks(stderr: str) -> list:
     """(reads, real seconds) of each mem_process_seqs chunk: the first chunk
     also pays each worker batch's first-use device and pinned allocations."""
@@ -802,6 +809,9 @@ def _e2e_legs(d: str, legs, env_base: dict, m: int, tag: str = "") -> dict | Non
         os.unlink(sam)
         runs[name] = {"wall_s": round(wall, 3), "mem_process_seqs_real_s": round(real, 3),
                       "outside_mem_process_seqs_s": round(wall - real, 3),
+                      # main()'s own "[main] Real time" (software/main.c): what is left of the wall
+                      # clock after it is the process's exit (the runtime's teardown)
+                      "main_real_s": _main_real(err),
                       "reads_per_s_wall": round(m / wall, 1),
                       "reads_per_s_mem_process_seqs": round(m / real, 1) if real > 0 else None,
                       "reads_processed": n_proc, "sam_sha256": digest, "sam_lines": n_lines,
